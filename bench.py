@@ -1,0 +1,207 @@
+"""Benchmark: overlap-pairs/s of the GPU scoring step (BASELINE.json metric).
+
+A step = one pass of the hot path (aligners.py:27-57 for every candidate pair
+of overlapGraphs.py:43-53) over the candidate list of one synthetic read set,
+with reads (bit-plane packed) and pairs already resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W --config cfg2]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+N > 1: one process per GPU; rank r scores its own seeded read set of the same
+config (weak scaling: per-GPU work fixed, no data-path collective).  The time
+is the max over ranks between barriers; value = pairs of all ranks / time.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
+
+METRIC = "overlap-pairs/sec (candidate read-pair alignments) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+WORKLOAD_DESC = {
+    "cfg1": "PhiX N=500 l=100 p=0.0 k=5 (BASELINE configs[0])",
+    "cfg2": "PhiX N=10000 l=100 p=0.01 k=5 (BASELINE configs[1], the 1xMI355X metric config)",
+    "cfg3": "PhiX N=50000 l=150 p=0.02 k=5 (BASELINE configs[2])",
+    "cfg4": "random 1 Mbp genome N=200000 l=100 p=0.01 k=5 (BASELINE configs[3])",
+    "cfg5": "PhiX N=50000 l=250 p=0.05 k=5 (BASELINE configs[4], full band)",
+    "target": "PhiX N=50000 l=100 p=0.01 k=5 (north_star target point)",
+}
+
+
+def algorithmic_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> int:
+    """ceil(n/4) + ceil(m/4) 2-bit read bytes + 8 B indices + 8 B (score, end) per pair."""
+    q = (lens + 3) // 4
+    return int(q[a].sum() + q[b].sum() + 16 * a.shape[0])
+
+
+def load_traffic(workload: str, kernel_ms: float):
+    """HBM bytes per launch from the committed PMC summary (profiles/*pmc*.json) for this workload."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for name in sorted(os.listdir(pdir), reverse=True):
+        if "pmc" in name and name.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(pdir, name)))
+            except Exception:
+                continue
+            if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+                return int(d["hbm_bytes_per_launch"])
+    return None
+
+
+def cpu_baseline(reads, a, b, budget_s: float = 12.0):
+    """The oracle's C restatement of aligners.py:27-57 (full DP, per-pair tables) on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    enc = oracle.encode(reads)
+    cal = min(a.shape[0], 4000)
+    t0 = time.perf_counter()
+    oracle.batch_dp(reads, a[:cal], b[:cal], threads=threads, encoded=enc)
+    per_pair = (time.perf_counter() - t0) / max(cal, 1)
+    n = int(min(a.shape[0], max(cal, budget_s / max(per_pair, 1e-9))))
+    idx = np.linspace(0, a.shape[0] - 1, n).astype(np.int64) if n < a.shape[0] else np.arange(n)
+    t0 = time.perf_counter()
+    oracle.batch_dp(reads, a[idx], b[idx], threads=threads, encoded=enc)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "overlap-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} of {a.shape[0]} candidate pairs (evenly strided) through oracle/ovl_oracle.c "
+                      f"oracle_batch_dp (full int32 DP + int8 traceback per pair, OpenMP {threads} threads), "
+                      f"{dt:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOAD_DESC))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ovlgraph import OverlapEngine
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import CONFIGS, config_reads
+
+    cfg = CONFIGS[args.config]
+    t_setup = time.perf_counter()
+    reads, _ = dedup_reads(config_reads(args.config, seed=rank))
+    a, b = enumerate_candidates(reads, cfg["k"])
+    t_enum = time.perf_counter() - t_setup
+    eng = OverlapEngine(local)
+    t0 = time.perf_counter()
+    eng.set_reads(reads)
+    t_pack = time.perf_counter() - t0
+    kernel = eng.plan()
+    n_pairs = int(a.shape[0])
+    da = torch.as_tensor(a, device=dev)
+    db = torch.as_tensor(b, device=dev)
+    ds = torch.empty(n_pairs, dtype=torch.int32, device=dev)
+    de = torch.empty(n_pairs, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        eng.score_tensors(da, db, ds, de)
+    torch.cuda.synchronize(dev)
+    eng.check_device_errors()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        eng.score_tensors(da, db, ds, de)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+
+    stats = torch.tensor([elapsed, kernel_ms, float(n_pairs)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot = stats.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, kernel_ms = float(mx[0]), float(mx[1])
+        total_pairs = int(tot[2])
+    else:
+        total_pairs = n_pairs
+
+    if rank == 0:
+        lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
+        algo = algorithmic_bytes(lens, a, b)
+        achieved = algo / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+        line = {
+            "metric": METRIC,
+            "value": total_pairs * args.steps / elapsed,
+            "unit": "overlap-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{args.config}: {WORKLOAD_DESC[args.config]}",
+                "reads_per_gpu": len(reads),
+                "pairs_per_gpu": n_pairs,
+                "read_length": cfg["l"],
+                "parallelism": f"pair-sharded x{world} (one process per GPU, own seeded read set per rank)",
+                "kernel": kernel,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(args.config, kernel_ms),
+                "kernel_ms": kernel_ms,
+                "algorithmic_bytes_per_launch": algo,
+            },
+            "host_setup_s": {"read_sim_and_enumeration": round(t_enum, 3), "upload_and_pack": round(t_pack, 4)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(reads, a, b, args.cpu_budget)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

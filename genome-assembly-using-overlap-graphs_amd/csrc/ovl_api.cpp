@@ -1,0 +1,471 @@
+// ovl_api.cpp — the C ABI of include/ovl.h on top of the gfx950 kernels.
+//
+// Owns: the HIP stream, the resident read store (codes + bit-plane layouts in
+// HBM), scratch for host-array calls and the device error flag.  Chooses the
+// kernel per call (ovl_plan): the ungapped popcount kernel whenever gaps
+// provably cannot win and the read store has a bit-plane layout, else the
+// int64-exact DP kernel.  Never falls back to the CPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ovl.h"
+#include "ovl_kernels.h"
+
+#define OVL_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int32_t kFastMaxLen = 256;   // bit-plane layout up to 8 words of 32 bases
+constexpr int32_t kDpMaxLen = 8192;    // DP kernel: LDS row of the t read
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+thread_local std::string g_err;
+
+}  // namespace
+
+struct ovl_ctx {
+    int32_t device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int32_t cu_count = 256;
+    // resident reads
+    int32_t n_reads = -1;
+    int32_t lmax = 0;
+    int32_t planes = 2;
+    int32_t wmax = 0;  // 0: no bit-plane layout (reads longer than kFastMaxLen)
+    int32_t zs = 0;
+    DevBuf codes, off, len, sfx, pfx, lut;
+    // scratch
+    DevBuf a, b, score, end, tb, err_flag;
+};
+
+namespace {
+
+int fail(const ovl_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    if (c) const_cast<ovl_ctx*>(c)->err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                           \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess)                                                                       \
+            return fail((ctx), e_ == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP, "%s: %s", #expr, \
+                        hipGetErrorString(e_));                                                     \
+    } while (0)
+
+hipError_t ensure(DevBuf& b, size_t bytes) {
+    if (bytes < 16) bytes = 16;
+    if (b.bytes >= bytes) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e == hipSuccess) b.bytes = bytes;
+    return e;
+}
+
+void release(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+template <typename T>
+T* as(DevBuf& b) { return reinterpret_cast<T*>(b.p); }
+
+int64_t iabs64(int64_t v) { return v < 0 ? -v : v; }
+
+// aligners.py:40: diag is taken whenever diag >= up and diag >= left.  Every dp
+// value is a sum of <= lmax diagonal terms when that always holds, so it does if
+// indel <= min(0, lmax*min(match,mismatch)) - max(0, lmax*max(match,mismatch)).
+bool gaps_cannot_win(int64_t match, int64_t mismatch, int64_t indel, int64_t lmax) {
+    const int64_t lo = std::min<int64_t>(0, lmax * std::min(match, mismatch));
+    const int64_t hi = std::max<int64_t>(0, lmax * std::max(match, mismatch));
+    return indel <= lo - hi;
+}
+
+struct Plan {
+    int kernel = OVL_KERNEL_NONE;
+    bool key64 = false;
+    bool wide = true;
+};
+
+int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* out) {
+    if (band >= 0)
+        return fail(c, OVL_E_UNSUPPORTED, "band=%d: only the full DP (band < 0) is implemented in ABI v%d", band,
+                    OVL_ABI_VERSION);
+    if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
+    const int64_t L = std::max<int32_t>(c->lmax, 1);
+    const int64_t amax = std::max(iabs64(match), iabs64(mismatch));
+    Plan p;
+    // ungapped closed form: exact when gaps cannot win and no int32 store can wrap
+    if (c->wmax > 0 && gaps_cannot_win(match, mismatch, indel, L) && amax * L < (int64_t(1) << 31)) {
+        p.kernel = OVL_KERNEL_UNGAPPED;
+        const int64_t top = L * std::max<int64_t>(0, std::max<int64_t>(match, mismatch));
+        p.key64 = !(top < (1 << 15) && L < (1 << 16));
+    } else {
+        if (c->lmax > kDpMaxLen)
+            return fail(c, OVL_E_UNSUPPORTED, "gapped DP supports reads up to %d bases (longest is %d)", kDpMaxLen,
+                        c->lmax);
+        p.kernel = OVL_KERNEL_DP;
+        const int64_t M = std::max(amax, iabs64(indel));
+        // |dp| <= 2*lmax*M; one more term for the candidates: int32 is exact below 2^31
+        p.wide = !(indel > INT32_MIN && M < (int64_t(1) << 31) && (2 * L + 1) * M < (int64_t(1) << 31));
+    }
+    *out = p;
+    return OVL_OK;
+}
+
+int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
+                 int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
+                 hipStream_t s) {
+    if (n_pairs == 0) return OVL_OK;
+    if (pl.kernel == OVL_KERNEL_UNGAPPED) {
+        OvlUngappedArgs g{};
+        g.sfx = as<uint32_t>(c->sfx);
+        g.pfx = as<uint32_t>(c->pfx);
+        g.len = as<int32_t>(c->len);
+        g.n_reads = c->n_reads;
+        g.a_idx = d_a;
+        g.b_idx = d_b;
+        g.n_pairs = n_pairs;
+        int32_t tile = 64;
+        const int64_t want_waves = (int64_t)c->cu_count * 32;
+        while (tile > 8 && (n_pairs + tile - 1) / tile < want_waves) tile >>= 1;
+        g.tile = tile;
+        g.match = match;
+        g.mismatch = mismatch;
+        g.out_score = d_score;
+        g.out_end = d_end;
+        g.err_flag = as<uint32_t>(c->err_flag);
+        g.planes = c->planes;
+        g.wmax = c->wmax;
+        g.key64 = pl.key64 ? 1 : 0;
+        g.max_blocks = (int64_t)c->cu_count * 8;
+        HIPCHK(c, ovl_launch_ungapped(&g, s));
+    } else {
+        OvlDpArgs g{};
+        g.codes = as<uint8_t>(c->codes);
+        g.off = as<int64_t>(c->off);
+        g.len = as<int32_t>(c->len);
+        g.n_reads = c->n_reads;
+        g.a_idx = d_a;
+        g.b_idx = d_b;
+        g.n_pairs = n_pairs;
+        g.mcap = std::max<int32_t>(c->lmax, 1);
+        g.match = match;
+        g.mismatch = mismatch;
+        g.indel = indel;
+        g.out_score = d_score;
+        g.out_end = d_end;
+        g.tb = nullptr;
+        g.err_flag = as<uint32_t>(c->err_flag);
+        g.wide = pl.wide ? 1 : 0;
+        HIPCHK(c, ovl_launch_dp(&g, s));
+    }
+    return OVL_OK;
+}
+
+int check_indices(const ovl_ctx* c, const int32_t* a, const int32_t* b, int64_t n) {
+    for (int64_t p = 0; p < n; ++p) {
+        if (a[p] < 0 || a[p] >= c->n_reads || b[p] < 0 || b[p] >= c->n_reads)
+            return fail(c, OVL_E_INDEX, "pair %lld = (%d, %d) outside [0, %d)", (long long)p, a[p], b[p],
+                        c->n_reads);
+    }
+    return OVL_OK;
+}
+
+}  // namespace
+
+OVL_API int ovl_version(void) { return OVL_ABI_VERSION; }
+
+OVL_API const char* ovl_last_error(const ovl_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+OVL_API int ovl_device_count(int32_t* out_count) {
+    if (!out_count) return fail(nullptr, OVL_E_ARG, "out_count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *out_count = 0;
+        return fail(nullptr, OVL_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *out_count = n;
+    return OVL_OK;
+}
+
+OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
+    if (!out_ctx) return fail(nullptr, OVL_E_ARG, "out_ctx is NULL");
+    *out_ctx = nullptr;
+    int n = 0;
+    HIPCHK(nullptr, hipGetDeviceCount(&n));
+    if (n <= 0) return fail(nullptr, OVL_E_HIP, "no HIP device visible");
+    if (device < 0) HIPCHK(nullptr, hipGetDevice(&device));
+    if (device >= n) return fail(nullptr, OVL_E_ARG, "device %d >= device count %d", device, n);
+    HIPCHK(nullptr, hipSetDevice(device));
+    ovl_ctx* c = new ovl_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu_count = prop.multiProcessorCount;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = ensure(c->err_flag, 16);
+    if (e == hipSuccess) e = hipMemset(c->err_flag.p, 0, 16);
+    if (e != hipSuccess) {
+        int rc = fail(nullptr, OVL_E_HIP, "context setup: %s", hipGetErrorString(e));
+        ovl_destroy(c);
+        return rc;
+    }
+    *out_ctx = c;
+    return OVL_OK;
+}
+
+OVL_API int ovl_destroy(ovl_ctx* c) {
+    if (!c) return OVL_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->a, &c->b, &c->score, &c->end,
+                      &c->tb, &c->err_flag})
+        release(*b);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return OVL_OK;
+}
+
+OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
+    if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t base = n_reads > 0 ? offsets[0] : 0;
+    if (base < 0) return fail(c, OVL_E_ARG, "offsets[0] < 0");
+    std::vector<int64_t> off((size_t)n_reads + 1, 0);
+    std::vector<int32_t> len((size_t)std::max(n_reads, 1), 0);
+    int32_t lmax = 0;
+    for (int32_t r = 0; r < n_reads; ++r) {
+        const int64_t l = offsets[r + 1] - offsets[r];
+        if (l < 0) return fail(c, OVL_E_ARG, "offsets not non-decreasing at read %d", r);
+        if (l > INT32_MAX / 2) return fail(c, OVL_E_UNSUPPORTED, "read %d is too long", r);
+        off[r + 1] = offsets[r + 1] - base;
+        len[r] = (int32_t)l;
+        lmax = std::max(lmax, (int32_t)l);
+    }
+    const int64_t total = n_reads > 0 ? off[n_reads] : 0;
+    if (total > 0 && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
+    // alphabet: dense codes in byte order (equality-preserving)
+    bool present[256] = {false};
+    const uint8_t* src = seqs ? seqs + base : nullptr;
+    for (int64_t i = 0; i < total; ++i) present[src[i]] = true;
+    uint8_t lut[256] = {0};
+    int k = 0;
+    for (int v = 0; v < 256; ++v)
+        if (present[v]) lut[v] = (uint8_t)k++;
+    const int planes = k <= 4 ? 2 : (k <= 16 ? 4 : 8);
+    int32_t wmax = 0;
+    if (lmax <= 64) wmax = 2;
+    else if (lmax <= 128) wmax = 4;
+    else if (lmax <= kFastMaxLen) wmax = 8;
+    const int32_t nch = wmax ? (32 * wmax + 64) / 64 : 0;
+    const int32_t zs = wmax ? 2 * nch + 2 : 0;
+
+    c->n_reads = -1;  // invalid until fully built
+    DevBuf raw;
+    HIPCHK(c, ensure(c->off, sizeof(int64_t) * off.size()));
+    HIPCHK(c, ensure(c->len, sizeof(int32_t) * len.size()));
+    HIPCHK(c, ensure(c->codes, (size_t)total));
+    HIPCHK(c, ensure(c->lut, 256));
+    hipError_t e = ensure(raw, (size_t)total);
+    if (e != hipSuccess) return fail(c, OVL_E_OOM, "raw read buffer: %s", hipGetErrorString(e));
+    int rc = OVL_OK;
+    do {
+        e = hipMemcpyAsync(c->off.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(c->len.p, len.data(), sizeof(int32_t) * len.size(), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(c->lut.p, lut, 256, hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) break;
+        if (total > 0) {
+            e = hipMemcpyAsync(raw.p, src, (size_t)total, hipMemcpyHostToDevice, c->stream);
+            if (e != hipSuccess) break;
+            e = ovl_launch_map_codes(as<uint8_t>(raw), as<uint8_t>(c->lut), as<uint8_t>(c->codes), total, c->stream);
+            if (e != hipSuccess) break;
+        }
+        if (wmax > 0) {
+            const size_t words = (size_t)std::max(n_reads, 1) * planes;
+            e = ensure(c->sfx, words * wmax * sizeof(uint32_t));
+            if (e != hipSuccess) break;
+            e = ensure(c->pfx, words * zs * sizeof(uint32_t));
+            if (e != hipSuccess) break;
+            e = ovl_launch_pack(planes, as<uint8_t>(c->codes), as<int64_t>(c->off), as<int32_t>(c->len), n_reads,
+                                wmax, zs, as<uint32_t>(c->sfx), as<uint32_t>(c->pfx), c->stream);
+            if (e != hipSuccess) break;
+        }
+        e = hipStreamSynchronize(c->stream);
+    } while (false);
+    release(raw);
+    if (e != hipSuccess)
+        return fail(c, e == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP, "ovl_set_reads: %s", hipGetErrorString(e));
+    c->lmax = lmax;
+    c->planes = planes;
+    c->wmax = wmax;
+    c->zs = zs;
+    c->n_reads = n_reads;
+    return rc;
+}
+
+OVL_API int ovl_reads_info(const ovl_ctx* c, int32_t* n_reads, int32_t* lmax, int32_t* planes, int64_t* device_bytes) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n_reads) *n_reads = c->n_reads;
+    if (lmax) *lmax = c->lmax;
+    if (planes) *planes = c->planes;
+    if (device_bytes)
+        *device_bytes = (int64_t)(c->codes.bytes + c->off.bytes + c->len.bytes + c->sfx.bytes + c->pfx.bytes);
+    return OVL_OK;
+}
+
+OVL_API int ovl_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                     int32_t* out_kernel) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!out_kernel) return fail(c, OVL_E_ARG, "out_kernel is NULL");
+    Plan p;
+    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    if (rc != OVL_OK) return rc;
+    *out_kernel = p.kernel;
+    return OVL_OK;
+}
+
+OVL_API int ovl_score_device(ovl_ctx* c, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs, int32_t match,
+                             int32_t mismatch, int64_t indel, int32_t band, int32_t* d_score, int32_t* d_end,
+                             void* stream) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n_pairs < 0) return fail(c, OVL_E_ARG, "n_pairs < 0");
+    if (n_pairs > 0 && (!d_a || !d_b || !d_score || !d_end)) return fail(c, OVL_E_ARG, "NULL device pointer");
+    Plan p;
+    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    if (rc != OVL_OK) return rc;
+    if (n_pairs > 0 && c->n_reads == 0) return fail(c, OVL_E_INDEX, "pairs given but the read set is empty");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    return launch_score(c, p, d_a, d_b, n_pairs, match, mismatch, indel, d_score, d_end, s);
+}
+
+OVL_API int ovl_check_device_errors(ovl_ctx* c) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    uint32_t flag = 0;
+    HIPCHK(c, hipMemcpy(&flag, c->err_flag.p, sizeof(flag), hipMemcpyDeviceToHost));
+    if (flag) {
+        HIPCHK(c, hipMemset(c->err_flag.p, 0, sizeof(uint32_t)));
+        return fail(c, OVL_E_INDEX, "a device scoring call saw a pair index outside [0, n_reads)");
+    }
+    return OVL_OK;
+}
+
+OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs, int32_t match,
+                           int32_t mismatch, int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n_pairs < 0) return fail(c, OVL_E_ARG, "n_pairs < 0");
+    if (n_pairs > 0 && (!a_idx || !b_idx || !out_score || !out_end)) return fail(c, OVL_E_ARG, "NULL host pointer");
+    Plan p;
+    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    if (rc != OVL_OK) return rc;
+    if (n_pairs == 0) return OVL_OK;
+    rc = check_indices(c, a_idx, b_idx, n_pairs);
+    if (rc != OVL_OK) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t bytes = sizeof(int32_t) * (size_t)n_pairs;
+    HIPCHK(c, ensure(c->a, bytes));
+    HIPCHK(c, ensure(c->b, bytes));
+    HIPCHK(c, ensure(c->score, bytes));
+    HIPCHK(c, ensure(c->end, bytes));
+    HIPCHK(c, hipMemcpyAsync(c->a.p, a_idx, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->b.p, b_idx, bytes, hipMemcpyHostToDevice, c->stream));
+    rc = launch_score(c, p, as<int32_t>(c->a), as<int32_t>(c->b), n_pairs, match, mismatch, indel,
+                      as<int32_t>(c->score), as<int32_t>(c->end), c->stream);
+    if (rc != OVL_OK) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_score, c->score.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out_end, c->end.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return OVL_OK;
+}
+
+OVL_API int ovl_score_pairs(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                            const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs, int32_t match,
+                            int32_t mismatch, int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end) {
+    int rc = ovl_set_reads(c, seqs, offsets, n_reads);
+    if (rc != OVL_OK) return rc;
+    return ovl_score_host(c, a_idx, b_idx, n_pairs, match, mismatch, indel, band, out_score, out_end);
+}
+
+OVL_API int ovl_align_one(ovl_ctx* c, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
+                          int32_t* out_score, int32_t* out_end, int8_t* traceback) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!out_score || !out_end) return fail(c, OVL_E_ARG, "NULL output pointer");
+    if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
+    if (a < 0 || a >= c->n_reads || b < 0 || b >= c->n_reads)
+        return fail(c, OVL_E_INDEX, "pair (%d, %d) outside [0, %d)", a, b, c->n_reads);
+    if (c->lmax > kDpMaxLen) return fail(c, OVL_E_UNSUPPORTED, "DP supports reads up to %d bases", kDpMaxLen);
+    HIPCHK(c, hipSetDevice(c->device));
+    // lengths from the host-visible offsets copy
+    int64_t offs[2][2];
+    HIPCHK(c, hipMemcpy(offs[0], as<int64_t>(c->off) + a, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(offs[1], as<int64_t>(c->off) + b, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+    const int64_t n = offs[0][1] - offs[0][0], m = offs[1][1] - offs[1][0];
+    const size_t cells = (size_t)(n + 1) * (size_t)(m + 1);
+    int32_t idx[2] = {a, b};
+    HIPCHK(c, ensure(c->a, sizeof(int32_t) * 2));
+    HIPCHK(c, ensure(c->score, sizeof(int32_t) * 2));
+    if (traceback) {
+        HIPCHK(c, ensure(c->tb, cells));
+        HIPCHK(c, hipMemsetAsync(c->tb.p, 0, cells, c->stream));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->a.p, idx, sizeof(idx), hipMemcpyHostToDevice, c->stream));
+    const int64_t amax = std::max(iabs64(match), iabs64(mismatch));
+    const int64_t M = std::max(amax, iabs64(indel));
+    const int64_t L = std::max<int32_t>(c->lmax, 1);
+    OvlDpArgs g{};
+    g.codes = as<uint8_t>(c->codes);
+    g.off = as<int64_t>(c->off);
+    g.len = as<int32_t>(c->len);
+    g.n_reads = c->n_reads;
+    g.a_idx = as<int32_t>(c->a);
+    g.b_idx = as<int32_t>(c->a) + 1;
+    g.n_pairs = 1;
+    g.mcap = (int32_t)std::max<int64_t>(m, 1);
+    g.match = match;
+    g.mismatch = mismatch;
+    g.indel = indel;
+    g.out_score = as<int32_t>(c->score);
+    g.out_end = as<int32_t>(c->score) + 1;
+    g.tb = traceback ? as<int8_t>(c->tb) : nullptr;
+    g.err_flag = as<uint32_t>(c->err_flag);
+    g.wide = !(indel > INT32_MIN && M < (int64_t(1) << 31) && (2 * L + 1) * M < (int64_t(1) << 31));
+    HIPCHK(c, ovl_launch_dp(&g, c->stream));
+    int32_t res[2];
+    HIPCHK(c, hipMemcpyAsync(res, c->score.p, sizeof(res), hipMemcpyDeviceToHost, c->stream));
+    if (traceback) HIPCHK(c, hipMemcpyAsync(traceback, c->tb.p, cells, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *out_score = res[0];
+    *out_end = res[1];
+    return OVL_OK;
+}

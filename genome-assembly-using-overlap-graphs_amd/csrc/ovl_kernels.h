@@ -1,0 +1,51 @@
+// ovl_kernels.h — launch interface between the C ABI (ovl_api.cpp) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct OvlUngappedArgs {
+    const uint32_t* sfx;
+    const uint32_t* pfx;
+    const int32_t* len;
+    int32_t n_reads;
+    const int32_t* a_idx;
+    const int32_t* b_idx;
+    int64_t n_pairs;
+    int32_t tile;        // pairs per wavefront tile (8..64)
+    int32_t match;
+    int32_t mismatch;
+    int32_t* out_score;
+    int32_t* out_end;
+    uint32_t* err_flag;
+    int32_t planes;      // 2, 4 or 8 bit planes per base
+    int32_t wmax;        // 2, 4 or 8 words of 32 bases (read length <= 32*wmax)
+    int32_t key64;       // 64-bit (score, end) keys when scores can reach 2^15
+    int64_t max_blocks;  // grid cap (grid-stride beyond it)
+};
+
+struct OvlDpArgs {
+    const uint8_t* codes;
+    const int64_t* off;
+    const int32_t* len;
+    int32_t n_reads;
+    const int32_t* a_idx;
+    const int32_t* b_idx;
+    int64_t n_pairs;
+    int32_t mcap;        // longest t read (LDS row capacity)
+    int64_t match;
+    int64_t mismatch;
+    int64_t indel;
+    int32_t* out_score;
+    int32_t* out_end;
+    int8_t* tb;          // optional traceback (single pair)
+    uint32_t* err_flag;
+    int32_t wide;        // int64 arithmetic (else int32, when magnitudes allow)
+};
+
+extern "C" hipError_t ovl_launch_map_codes(const uint8_t* raw, const uint8_t* lut, uint8_t* codes, int64_t n,
+                                           hipStream_t stream);
+extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const int64_t* off, const int32_t* len,
+                                      int32_t n_reads, int32_t wmax, int32_t zs, uint32_t* sfx, uint32_t* pfx,
+                                      hipStream_t stream);
+extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream_t stream);
+extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);

@@ -1,0 +1,97 @@
+"""ctypes binding of libovl.so (the C ABI declared in include/ovl.h).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()``)
+into ``genome-assembly-using-overlap-graphs_amd/build/libovl.so``.  There is no
+CPU fallback: if the library is missing or no GPU is visible the engine
+raises ``OvlError``.  ctypes releases the GIL for the duration of each call.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "build", "libovl.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+
+ABI_VERSION = 1
+
+OVL_OK = 0
+ERRORS = {
+    -1: "OVL_E_ARG", -2: "OVL_E_HIP", -3: "OVL_E_OOM", -4: "OVL_E_UNSUPPORTED",
+    -5: "OVL_E_RANGE", -6: "OVL_E_STATE", -7: "OVL_E_INDEX",
+}
+KERNELS = {0: "none", 1: "ungapped", 2: "dp"}
+
+# name -> (restype, argtypes); mirrors include/ovl.h exactly
+_P = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_pi32 = ctypes.POINTER(ctypes.c_int32)
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+SIGNATURES = {
+    "ovl_version": (ctypes.c_int, []),
+    "ovl_device_count": (ctypes.c_int, [_pi32]),
+    "ovl_create": (ctypes.c_int, [_i32, ctypes.POINTER(_P)]),
+    "ovl_destroy": (ctypes.c_int, [_P]),
+    "ovl_last_error": (ctypes.c_char_p, [_P]),
+    "ovl_score_pairs": (ctypes.c_int, [_P, _P, _P, _i32, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P]),
+    "ovl_set_reads": (ctypes.c_int, [_P, _P, _P, _i32]),
+    "ovl_reads_info": (ctypes.c_int, [_P, _pi32, _pi32, _pi32, _pi64]),
+    "ovl_plan": (ctypes.c_int, [_P, _i32, _i32, _i64, _i32, _pi32]),
+    "ovl_score_host": (ctypes.c_int, [_P, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P]),
+    "ovl_score_device": (ctypes.c_int, [_P, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P, _P]),
+    "ovl_check_device_errors": (ctypes.c_int, [_P]),
+    "ovl_align_one": (ctypes.c_int, [_P, _i32, _i32, _i32, _i32, _i64, _pi32, _pi32, _P]),
+}
+
+
+class OvlError(RuntimeError):
+    """A libovl call failed (or the library / GPU is unavailable)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libovl.so for gfx950 with hipcc (cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+def load():
+    """Load and type libovl.so; raises OvlError if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise OvlError(-2, f"{LIB_PATH} not built: run __graft_entry__.build() "
+                                   "(make -C genome-assembly-using-overlap-graphs_amd/csrc)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            v = lib.ovl_version()
+            if v != ABI_VERSION:
+                raise OvlError(-1, f"libovl ABI {v} != expected {ABI_VERSION}")
+            _lib = lib
+        return _lib
+
+
+def last_error(ctx=None) -> str:
+    msg = load().ovl_last_error(ctx)
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc != OVL_OK:
+        raise OvlError(rc, last_error(ctx))

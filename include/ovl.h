@@ -1,0 +1,117 @@
+/*
+ * ovl.h — C ABI of the MI355X-native overlap-scoring engine (libovl.so).
+ *
+ * Replaces the per-pair Python->Numba boundary of the reference:
+ *   overlapGraphs.py:53   overlap_alignment(read_a, read_b) once per candidate pair
+ *   aligners.py:6-82      @njit overlap_alignment(s, t, match_score=10, mismatch=-1, indel=-2**31)
+ * with one batched call per candidate list.  Only (score, end) reach the
+ * graph (overlapGraphs.py:53-60), so that is what the batch entry points return.
+ *
+ * Conventions
+ *  - Plain C types only; the caller owns every pointer it passes in.
+ *  - Return value 0 (OVL_OK) on success, a negative OVL_E_* code on failure;
+ *    ovl_last_error() then describes it.  Nothing throws or aborts across the ABI.
+ *  - One call at a time per ovl_ctx.  Contexts are independent; a process
+ *    drives one GPU through one context (one process per GPU).
+ *  - Read i is the byte string seqs[offsets[i] .. offsets[i+1]).  Bytes are
+ *    symbols compared for equality only (any alphabet of <= 256 symbols).
+ *  - Semantics are the reference's: DP fill of aligners.py:27-48 with int64
+ *    arithmetic and int32 stores, last-row strict-'>' first argmax of
+ *    aligners.py:50-57.  score >= 0 and 0 <= end <= len(t) always.
+ */
+#ifndef OVL_H
+#define OVL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OVL_ABI_VERSION 1
+
+enum {
+    OVL_OK = 0,
+    OVL_E_ARG = -1,          /* bad argument (null pointer, negative size, bad offsets) */
+    OVL_E_HIP = -2,          /* HIP runtime error */
+    OVL_E_OOM = -3,          /* device allocation failed */
+    OVL_E_UNSUPPORTED = -4,  /* band >= 0 (not in this ABI version), read too long, >256 symbols */
+    OVL_E_RANGE = -5,        /* scoring magnitudes would overflow the int32 DP table */
+    OVL_E_STATE = -6,        /* no resident reads (ovl_set_reads not called) */
+    OVL_E_INDEX = -7         /* a pair index is outside [0, n_reads) */
+};
+
+enum {
+    OVL_KERNEL_NONE = 0,
+    OVL_KERNEL_UNGAPPED = 1, /* 2-bit (or 4/8-bit) bit-plane popcount kernel; exact when gaps cannot win */
+    OVL_KERNEL_DP = 2        /* anti-diagonal wavefront DP, int64-exact, any scoring */
+};
+
+typedef struct ovl_ctx ovl_ctx;
+
+/* ABI version (OVL_ABI_VERSION). */
+int ovl_version(void);
+
+/* Number of visible HIP devices. */
+int ovl_device_count(int32_t* out_count);
+
+/* Create a context on `device` (-1 = the current device). */
+int ovl_create(int32_t device, ovl_ctx** out_ctx);
+int ovl_destroy(ovl_ctx* ctx);
+
+/* Last error message of `ctx`, or of the calling thread when ctx is NULL. */
+const char* ovl_last_error(const ovl_ctx* ctx);
+
+/*
+ * One-shot batch scoring: uploads and packs the reads, scores
+ * n_pairs candidates (a_idx[p], b_idx[p]) and writes out_score[p], out_end[p].
+ * Replaces the loop body of overlapGraphs.py:50-53 for a whole candidate list.
+ * band < 0 means the full DP (the only mode of this ABI version).
+ */
+int ovl_score_pairs(ovl_ctx* ctx, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                    const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                    int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                    int32_t* out_score, int32_t* out_end);
+
+/* Upload + pack a read set and keep it resident in HBM (replaces any previous set). */
+int ovl_set_reads(ovl_ctx* ctx, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads);
+
+/* Resident read-set facts: count, longest read, bit planes per base, device bytes held. */
+int ovl_reads_info(const ovl_ctx* ctx, int32_t* n_reads, int32_t* lmax, int32_t* planes,
+                   int64_t* device_bytes);
+
+/* Which kernel a score call with these parameters would use on the resident reads. */
+int ovl_plan(const ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+             int32_t* out_kernel);
+
+/* Score against the resident reads; host pair/result arrays; synchronous. */
+int ovl_score_host(ovl_ctx* ctx, const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                   int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                   int32_t* out_score, int32_t* out_end);
+
+/*
+ * Score against the resident reads with DEVICE pointers, asynchronously on
+ * `stream` (a hipStream_t; NULL = the context's stream).  Pairs with an index
+ * outside [0, n_reads) get score = end = -1 and set a device error flag that
+ * ovl_check_device_errors() reports.
+ */
+int ovl_score_device(ovl_ctx* ctx, const int32_t* d_a_idx, const int32_t* d_b_idx, int64_t n_pairs,
+                     int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                     int32_t* d_score, int32_t* d_end, void* stream);
+
+/* Synchronise the device; OVL_E_INDEX if a previous ovl_score_device saw a bad index (flag is cleared). */
+int ovl_check_device_errors(ovl_ctx* ctx);
+
+/*
+ * One resident pair (a, b) through the DP kernel, optionally returning the
+ * (len(a)+1) x (len(b)+1) int8 traceback table of aligners.py:30,42-48
+ * (0 = diagonal, 1 = up, 2 = left) for the backtrack of aligners.py:59-78.
+ */
+int ovl_align_one(ovl_ctx* ctx, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
+                  int32_t* out_score, int32_t* out_end, int8_t* traceback);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OVL_H */

@@ -1,0 +1,144 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's overlap scoring, used as the parity
+ * checker by tests/, by __graft_entry__.smoke() and as bench.py's
+ * cpu_baseline leg.  Nothing in the product path (ovlgraph/, csrc/) may link,
+ * load or call this file.
+ *
+ * Follows, line by line in behaviour (not in text):
+ *   aligners.py:27-30  n, m; int32 dp table and int8 traceback table, zeroed
+ *                      (row 0 and column 0 stay 0: free overhangs)
+ *   aligners.py:33-48  fill: diag = dp[i-1][j-1] + (match | mismatch),
+ *                      up = dp[i-1][j] + indel, left = dp[i][j-1] + indel;
+ *                      pick diag if diag>=up && diag>=left, elif up>=left up,
+ *                      else left; store into the int32 table.
+ *   aligners.py:50-57  last-row scan j = 0..m from -inf with strict '>':
+ *                      best score and FIRST j attaining it.
+ * Arithmetic is int64 and stores wrap to int32, as Numba compiles it
+ * (integer binops are typed at >= intp width: numba/core/typing/builtins.py
+ * :141-166; the omitted default indel is typed from its literal, int64).
+ *
+ * Parity pinning: tests/golden/ fixtures were produced by executing the
+ * reference's own aligners.py/overlapGraphs.py source (see oracle/gen_golden.py
+ * and DESIGN.md §Oracle for how, and for the caveat that Numba itself is absent).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORACLE_ABI_VERSION 1
+
+int oracle_version(void) { return ORACLE_ABI_VERSION; }
+
+/* Full DP, aligners.py:27-57.  tb (nullable) receives the (n+1)*(m+1) int8
+ * traceback table, row-major.  Returns 0, or -1 on allocation failure. */
+int oracle_overlap_dp(const uint8_t* s, int32_t n, const uint8_t* t, int32_t m,
+                      int64_t match, int64_t mismatch, int64_t indel,
+                      int32_t* out_score, int32_t* out_end, int8_t* tb)
+{
+    const size_t W = (size_t)m + 1;
+    const size_t cells = ((size_t)n + 1) * W;
+    /* the reference allocates both tables per call (aligners.py:28,30) */
+    int32_t* dp = (int32_t*)calloc(cells, sizeof(int32_t));
+    int8_t* tr = tb ? tb : (int8_t*)calloc(cells, 1);
+    if (!dp || !tr) { free(dp); if (!tb) free(tr); return -1; }
+    if (tb) memset(tb, 0, cells);
+    for (int32_t i = 1; i <= n; ++i) {
+        const int32_t* prev = dp + (size_t)(i - 1) * W;
+        int32_t* cur = dp + (size_t)i * W;
+        int8_t* trow = tr + (size_t)i * W;
+        const uint8_t si = s[i - 1];
+        for (int32_t j = 1; j <= m; ++j) {
+            int64_t diag = (int64_t)prev[j - 1] + (si == t[j - 1] ? match : mismatch);
+            int64_t up = (int64_t)prev[j] + indel;
+            int64_t left = (int64_t)cur[j - 1] + indel;
+            if (diag >= up && diag >= left) { cur[j] = (int32_t)diag; trow[j] = 0; }
+            else if (up >= left)            { cur[j] = (int32_t)up;   trow[j] = 1; }
+            else                            { cur[j] = (int32_t)left; trow[j] = 2; }
+        }
+    }
+    double best = -INFINITY;
+    int32_t end = 0;
+    const int32_t* last = dp + (size_t)n * W;
+    for (int32_t j = 0; j <= m; ++j) {
+        if ((double)last[j] > best) { best = (double)last[j]; end = j; }
+    }
+    *out_score = (int32_t)best;
+    *out_end = end;
+    free(dp);
+    if (!tb) free(tr);
+    return 0;
+}
+
+/* Closed form of the DP when gaps cannot win:
+ * dp[n][j] = sum over the L=min(n,j) diagonal cells ending at (n, j). */
+void oracle_overlap_ungapped(const uint8_t* s, int32_t n, const uint8_t* t, int32_t m,
+                             int64_t match, int64_t mismatch,
+                             int32_t* out_score, int32_t* out_end)
+{
+    int64_t best = 0;  /* j = 0 scores 0 and is scanned first */
+    int32_t end = 0;
+    for (int32_t j = 1; j <= m; ++j) {
+        const int32_t L = n < j ? n : j;
+        const uint8_t* sp = s + (n - L);
+        const uint8_t* tp = t + (j - L);
+        int64_t sum = 0;
+        for (int32_t q = 0; q < L; ++q) sum += (sp[q] == tp[q]) ? match : mismatch;
+        if (sum > best) { best = sum; end = j; }
+    }
+    *out_score = (int32_t)best;
+    *out_end = end;
+}
+
+static int batch_common(int mode, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                        const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                        int64_t match, int64_t mismatch, int64_t indel,
+                        int32_t* out_score, int32_t* out_end, int32_t threads)
+{
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        if (a_idx[p] < 0 || a_idx[p] >= n_reads || b_idx[p] < 0 || b_idx[p] >= n_reads) return -2;
+    }
+    int err = 0;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 256) num_threads(threads) reduction(| : err)
+#endif
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        const int32_t a = a_idx[p], b = b_idx[p];
+        const uint8_t* s = seqs + offsets[a];
+        const uint8_t* t = seqs + offsets[b];
+        const int32_t n = (int32_t)(offsets[a + 1] - offsets[a]);
+        const int32_t m = (int32_t)(offsets[b + 1] - offsets[b]);
+        if (mode == 0) {
+            err |= oracle_overlap_dp(s, n, t, m, match, mismatch, indel, out_score + p, out_end + p, NULL);
+        } else {
+            oracle_overlap_ungapped(s, n, t, m, match, mismatch, out_score + p, out_end + p);
+        }
+    }
+    (void)threads;
+    return err ? -1 : 0;
+}
+
+/* Batch over a pair list; threads <= 0 means all OpenMP threads. */
+int oracle_batch_dp(const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                    const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                    int64_t match, int64_t mismatch, int64_t indel,
+                    int32_t* out_score, int32_t* out_end, int32_t threads)
+{
+    return batch_common(0, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, indel,
+                        out_score, out_end, threads);
+}
+
+int oracle_batch_ungapped(const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                          const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                          int64_t match, int64_t mismatch,
+                          int32_t* out_score, int32_t* out_end, int32_t threads)
+{
+    return batch_common(1, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, 0,
+                        out_score, out_end, threads);
+}

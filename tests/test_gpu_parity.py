@@ -1,0 +1,288 @@
+"""GPU parity: the HIP path (through the C ABI) vs the reference's golden vectors and the oracle.
+
+Bit-exact for every comparison (integer scores and end positions).
+"""
+import contextlib
+import io
+import random
+
+import numpy as np
+import pytest
+
+from conftest import assert_graph_matches_record
+
+pytestmark = pytest.mark.gpu
+
+INDEL = -(2 ** 31)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from ovlgraph import OverlapEngine
+    eng = OverlapEngine(0)
+    yield eng
+    eng.close()
+
+
+def _pairs_to_reads(pairs):
+    reads = []
+    for p in pairs:
+        reads += [p["s"], p["t"]]
+    a = np.arange(0, len(reads), 2, dtype=np.int32)
+    return reads, a, a + 1
+
+
+def _rand(rng, n, alphabet="ACGT"):
+    return "".join(rng.choice(alphabet) for _ in range(n))
+
+
+# ----------------------------------------------------------------------------- golden vectors
+
+def test_golden_default_batch(engine, golden_default):
+    reads, a, b = _pairs_to_reads(golden_default["pairs"])
+    engine.set_reads(reads)
+    assert engine.plan() == "ungapped"
+    sc, en = engine.score(a, b)
+    assert sc.tolist() == [p["score"] for p in golden_default["pairs"]]
+    assert en.tolist() == [p["end"] for p in golden_default["pairs"]]
+
+
+def test_golden_default_through_dp_kernel(engine, golden_default):
+    # the gapped kernel must agree in the ungapped regime too (finite but huge indel -> DP plan)
+    reads, a, b = _pairs_to_reads(golden_default["pairs"])
+    engine.set_reads(reads)
+    # indel -2**31 with a 300-base read set forces the DP kernel once lmax > 256
+    long_reads = reads + ["A" * 300]
+    engine.set_reads(long_reads)
+    assert engine.plan() == "dp"
+    sc, en = engine.score(a, b)
+    assert sc.tolist() == [p["score"] for p in golden_default["pairs"]]
+    assert en.tolist() == [p["end"] for p in golden_default["pairs"]]
+
+
+def test_golden_params(engine, golden_params):
+    by_params = {}
+    for p in golden_params["pairs"]:
+        by_params.setdefault((p["match"], p["mismatch"], p["indel"]), []).append(p)
+    for (ma, mm, ind), pairs in by_params.items():
+        reads, a, b = _pairs_to_reads(pairs)
+        engine.set_reads(reads)
+        sc, en = engine.score(a, b, ma, mm, ind)
+        assert sc.tolist() == [p["score"] for p in pairs], (ma, mm, ind)
+        assert en.tolist() == [p["end"] for p in pairs], (ma, mm, ind)
+
+
+def test_golden_alphabet(engine, golden_alphabet):
+    reads, a, b = _pairs_to_reads(golden_alphabet["pairs"])
+    engine.set_reads(reads)
+    sc, en = engine.score(a, b)
+    assert sc.tolist() == [p["score"] for p in golden_alphabet["pairs"]]
+    assert en.tolist() == [p["end"] for p in golden_alphabet["pairs"]]
+    # per-alphabet read sets (2-, 4- and 8-plane layouts)
+    for lo in range(0, len(golden_alphabet["pairs"]), 30):
+        chunk = golden_alphabet["pairs"][lo:lo + 30]
+        reads, a, b = _pairs_to_reads(chunk)
+        engine.set_reads(reads)
+        sc, en = engine.score(a, b)
+        assert sc.tolist() == [p["score"] for p in chunk]
+        assert en.tolist() == [p["end"] for p in chunk]
+
+
+def test_overlap_alignment_tuple(engine, golden_default, golden_params, golden_alphabet):
+    from ovlgraph.aligners import overlap_alignment
+    for p in golden_default["pairs"]:
+        if "to_print" in p:
+            got = overlap_alignment(p["s"], p["t"], engine=engine)
+            assert list(got) == [p["to_print"], p["align_s"], p["align_t"], p["score"], p["end"]]
+    for p in golden_params["pairs"][::3]:
+        got = overlap_alignment(p["s"], p["t"], p["match"], p["mismatch"], p["indel"], engine=engine)
+        assert list(got) == [p["to_print"], p["align_s"], p["align_t"], p["score"], p["end"]]
+    for p in golden_alphabet["pairs"][::4]:
+        got = overlap_alignment(p["s"], p["t"], engine=engine)
+        assert list(got) == [p["to_print"], p["align_s"], p["align_t"], p["score"], p["end"]]
+
+
+def test_golden_graphs(engine, golden_graphs):
+    from ovlgraph import overlapGraphs as og
+    for rec in golden_graphs["graphs"]:
+        copies = None
+        if rec["fn"] == "construct_overlap_graph_nx_k":
+            G, copies = og.construct_overlap_graph_nx_k(rec["reads"], engine=engine, **rec["kwargs"])
+        elif rec["fn"] == "construct_overlap_graph_string":
+            G, copies = og.construct_overlap_graph_string(rec["reads"], engine=engine)
+        else:
+            with contextlib.redirect_stdout(io.StringIO()):
+                G = og.construct_string_graph(rec["reads"], engine=engine)
+        assert_graph_matches_record(G, rec, copies)
+
+
+# ----------------------------------------------------------------------------- seeded vs oracle
+
+@pytest.mark.parametrize("lmax", [20, 64, 65, 100, 128, 129, 150, 200, 256])
+def test_random_lengths_vs_oracle(engine, oracle_mod, lmax):
+    rng = random.Random(lmax)
+    reads = [_rand(rng, rng.randint(1, lmax)) for _ in range(300)]
+    reads += [_rand(rng, lmax) for _ in range(100)]
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(4000)], dtype=np.int32)
+    b = np.array([rng.randrange(n) for _ in range(4000)], dtype=np.int32)
+    engine.set_reads(reads)
+    sc, en = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+    # slice against the full DP restatement too
+    ds, de = oracle_mod.batch_dp(reads, a[:400], b[:400])
+    np.testing.assert_array_equal(sc[:400], ds)
+    np.testing.assert_array_equal(en[:400], de)
+
+
+def test_overlapping_reads_vs_oracle(engine, oracle_mod):
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import read_genome_from_fasta, simulate_reads
+    g = read_genome_from_fasta()
+    for l, p in ((100, 0.01), (150, 0.02), (250, 0.05), (40, 0.0)):
+        reads, _ = dedup_reads(simulate_reads(g, l, 3000, p, seed=l))
+        a, b = enumerate_candidates(reads, 5)
+        engine.set_reads(reads)
+        sc, en = engine.score(a, b)
+        rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
+        assert (sc > 0).mean() > 0.9
+
+
+@pytest.mark.parametrize("params", [(10, -1, -1), (1, -1, -1), (2, -3, -5), (10, -1, -30), (5, -4, -8)])
+def test_gapped_vs_oracle(engine, oracle_mod, params):
+    ma, mm, ind = params
+    rng = random.Random(sum(params) + 99)
+    reads = [_rand(rng, rng.randint(1, 130)) for _ in range(200)]
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(1500)], dtype=np.int32)
+    b = np.array([rng.randrange(n) for _ in range(1500)], dtype=np.int32)
+    engine.set_reads(reads)
+    assert engine.plan(ma, mm, ind) == "dp"
+    sc, en = engine.score(a, b, ma, mm, ind)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b, ma, mm, ind)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+def test_long_reads_dp_path(engine, oracle_mod):
+    rng = random.Random(5)
+    reads = [_rand(rng, rng.randint(200, 700)) for _ in range(40)]
+    a = np.array([rng.randrange(40) for _ in range(120)], dtype=np.int32)
+    b = np.array([rng.randrange(40) for _ in range(120)], dtype=np.int32)
+    engine.set_reads(reads)
+    assert engine.plan() == "dp"
+    sc, en = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+def test_wide_arithmetic_wraps_like_numba(engine, oracle_mod):
+    # magnitudes where int32 stores wrap: the int64 DP kernel must reproduce it
+    rng = random.Random(77)
+    reads = [_rand(rng, rng.randint(1, 40)) for _ in range(60)]
+    a = np.array([rng.randrange(60) for _ in range(300)], dtype=np.int32)
+    b = np.array([rng.randrange(60) for _ in range(300)], dtype=np.int32)
+    engine.set_reads(reads)
+    for ma, mm, ind in ((2 ** 28, -(2 ** 28), -(2 ** 27)), (2 ** 30, -1, -(2 ** 33)), (7, -3, -(2 ** 40))):
+        sc, en = engine.score(a, b, ma, mm, ind)
+        rs, re_ = oracle_mod.batch_dp(reads, a, b, ma, mm, ind)
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
+
+
+def test_traceback_matches_oracle(engine, oracle_mod):
+    rng = random.Random(3)
+    for params in ((10, -1, -1), (10, -1, INDEL), (2, -3, -5)):
+        for _ in range(10):
+            s, t = _rand(rng, rng.randint(0, 50)), _rand(rng, rng.randint(0, 50))
+            engine.set_reads([s, t])
+            got = engine.align_one(0, 1, len(s), len(t), *params, traceback=True)
+            want = oracle_mod.dp_one(s, t, *params, want_tb=True)
+            assert got[:2] == want[:2]
+            np.testing.assert_array_equal(got[2], want[2])
+
+
+# ----------------------------------------------------------------------------- edge cases
+
+def test_empty_and_degenerate(engine):
+    engine.set_reads(["", "A", "ACGT", ""])
+    sc, en = engine.score([0, 1, 2, 0, 3, 2], [1, 0, 3, 0, 2, 2])
+    assert sc.tolist() == [0, 0, 0, 0, 0, 40]
+    assert en.tolist() == [0, 0, 0, 0, 0, 4]
+    sc, en = engine.score(np.zeros(0, np.int32), np.zeros(0, np.int32))
+    assert sc.size == 0
+
+
+def test_errors(engine):
+    from ovlgraph import OvlError
+    engine.set_reads(["ACGT", "CGTA"])
+    with pytest.raises(OvlError, match="OVL_E_INDEX"):
+        engine.score([0, 2], [1, 0])
+    with pytest.raises(OvlError, match="OVL_E_UNSUPPORTED"):
+        engine.score([0], [1], band=8)
+    with pytest.raises(OvlError, match="OVL_E_ARG"):
+        engine.score([0, 1], [1])
+
+
+def test_device_api_flags_bad_index(engine):
+    import torch
+    from ovlgraph import OvlError
+    engine.set_reads(["ACGTACGT", "CGTACGTA", "TTTT"])
+    a = torch.tensor([0, 1, 5, 2], dtype=torch.int32, device="cuda")
+    b = torch.tensor([1, 0, 0, -1], dtype=torch.int32, device="cuda")
+    s = torch.empty(4, dtype=torch.int32, device="cuda")
+    e = torch.empty(4, dtype=torch.int32, device="cuda")
+    engine.score_tensors(a, b, s, e)
+    with pytest.raises(OvlError, match="OVL_E_INDEX"):
+        engine.check_device_errors()
+    assert s.cpu().tolist()[2:] == [-1, -1] and e.cpu().tolist()[2:] == [-1, -1]
+    engine.check_device_errors()  # flag cleared
+
+
+def test_one_shot_abi(oracle_mod):
+    import ctypes
+    from ovlgraph import _lib
+    from ovlgraph.engine import encode_reads
+    L = _lib.load()
+    ctx = ctypes.c_void_p()
+    _lib.check(L.ovl_create(0, ctypes.byref(ctx)))
+    reads = ["ACGTACGTTT", "GTTTACGA", "TTACG", "CCCC"]
+    buf, offs = encode_reads(reads)
+    a = np.array([0, 1, 2, 3, 0], np.int32)
+    b = np.array([1, 2, 0, 0, 0], np.int32)
+    sc = np.zeros(5, np.int32)
+    en = np.zeros(5, np.int32)
+    p = lambda x: ctypes.c_void_p(x.ctypes.data)
+    _lib.check(L.ovl_score_pairs(ctx, p(buf), p(offs), 4, p(a), p(b), 5, 10, -1, INDEL, -1, p(sc), p(en)), ctx)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b)
+    assert sc.tolist() == rs.tolist() and en.tolist() == re_.tolist()
+    L.ovl_destroy(ctx)
+
+
+# ----------------------------------------------------------------------------- full-size configs
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "target"])
+def test_full_config_vs_oracle(engine, oracle_mod, cfg):
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import CONFIGS, config_reads
+    reads, _ = dedup_reads(config_reads(cfg, seed=0))
+    a, b = enumerate_candidates(reads, CONFIGS[cfg]["k"])
+    engine.set_reads(reads)
+    sc, en = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+    # determinism and permutation invariance (size-independent properties)
+    perm = np.random.default_rng(1).permutation(a.shape[0])
+    sc2, en2 = engine.score(a[perm], b[perm])
+    np.testing.assert_array_equal(sc2, sc[perm])
+    np.testing.assert_array_equal(en2, en[perm])
+    # a slice through the full-DP restatement (the reference recurrence itself)
+    ds, de = oracle_mod.batch_dp(reads, a[:2000], b[:2000])
+    np.testing.assert_array_equal(sc[:2000], ds)
+    np.testing.assert_array_equal(en[:2000], de)
