@@ -43,7 +43,7 @@ def algorithmic_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> int:
     return int(q[a].sum() + q[b].sum() + 16 * a.shape[0])
 
 
-def load_traffic(workload: str, kernel_ms: float):
+def load_traffic(workload: str):
     """HBM bytes per launch from the committed PMC summary (profiles/*pmc*.json) for this workload."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
@@ -59,8 +59,13 @@ def load_traffic(workload: str, kernel_ms: float):
     return None
 
 
-def cpu_baseline(reads, a, b, budget_s: float = 12.0):
-    """The oracle's C restatement of aligners.py:27-57 (full DP, per-pair tables) on host cores."""
+def cpu_baseline(reads, a, b, budget_s: float = 10.0):
+    """The oracle's C restatement of aligners.py:27-57 (full DP, per-pair tables) on host cores.
+
+    The whole candidate list is scored repeatedly until ~budget_s of wall time
+    (at least once); a strided sample is used instead when one pass would
+    exceed the budget.
+    """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
@@ -70,25 +75,90 @@ def cpu_baseline(reads, a, b, budget_s: float = 12.0):
     t0 = time.perf_counter()
     oracle.batch_dp(reads, a[:cal], b[:cal], threads=threads, encoded=enc)
     per_pair = (time.perf_counter() - t0) / max(cal, 1)
-    n = int(min(a.shape[0], max(cal, budget_s / max(per_pair, 1e-9))))
-    idx = np.linspace(0, a.shape[0] - 1, n).astype(np.int64) if n < a.shape[0] else np.arange(n)
+    n_fit = int(budget_s / max(per_pair, 1e-9))
+    if n_fit < a.shape[0]:
+        idx = np.linspace(0, a.shape[0] - 1, max(n_fit, cal)).astype(np.int64)
+        sa, sb, reps = a[idx], b[idx], 1
+        what = f"{idx.shape[0]} of {a.shape[0]} candidate pairs (evenly strided)"
+    else:
+        sa, sb = a, b
+        reps = max(1, int(n_fit // a.shape[0]))
+        what = f"all {a.shape[0]} candidate pairs x {reps} passes"
     t0 = time.perf_counter()
-    oracle.batch_dp(reads, a[idx], b[idx], threads=threads, encoded=enc)
+    for _ in range(reps):
+        oracle.batch_dp(reads, sa, sb, threads=threads, encoded=enc)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "overlap-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} of {a.shape[0]} candidate pairs (evenly strided) through oracle/ovl_oracle.c "
-                      f"oracle_batch_dp (full int32 DP + int8 traceback per pair, OpenMP {threads} threads), "
-                      f"{dt:.1f} s"}
+    return {"value": sa.shape[0] * reps / dt, "unit": "overlap-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{what} through oracle/ovl_oracle.c oracle_batch_dp (full int32 DP + int8 traceback "
+                      f"per pair, as aligners.py:27-57; OpenMP {threads} threads), {dt:.1f} s"}
+
+
+class Workload:
+    """One rank's read set + candidate list resident on its GPU."""
+
+    def __init__(self, name: str, seed: int, dev, engine=None):
+        import torch
+        from ovlgraph import OverlapEngine
+        from ovlgraph.candidates import dedup_reads, enumerate_candidates
+        from ovlgraph.reads import CONFIGS, config_reads
+
+        self.name = name
+        self.cfg = CONFIGS[name]
+        t0 = time.perf_counter()
+        self.reads, _ = dedup_reads(config_reads(name, seed=seed))
+        self.a, self.b = enumerate_candidates(self.reads, self.cfg["k"])
+        self.t_enum = time.perf_counter() - t0
+        self.eng = engine or OverlapEngine(dev.index)
+        t0 = time.perf_counter()
+        self.eng.set_reads(self.reads)
+        self.t_pack = time.perf_counter() - t0
+        self.kernel = self.eng.plan()
+        self.n_pairs = int(self.a.shape[0])
+        self.da = torch.as_tensor(self.a, device=dev)
+        self.db = torch.as_tensor(self.b, device=dev)
+        self.ds = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
+        self.de = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
+        self.launch = self.eng.launcher(self.da, self.db, self.ds, self.de)
+
+    def algo_bytes(self) -> int:
+        lens = np.fromiter((len(r) for r in self.reads), dtype=np.int64, count=len(self.reads))
+        return algorithmic_bytes(lens, self.a, self.b)
+
+
+def timed_steps(w: Workload, steps: int, warmup: int, dev, world: int):
+    """Warmup, then K steps between barriers; returns (wall seconds, HIP-event ms per launch)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        w.launch()
+    torch.cuda.synchronize(dev)
+    w.eng.check_device_errors()
+    stream = torch.cuda.current_stream(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        w.launch()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / max(steps, 1)
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOAD_DESC))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra single-GPU configs")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
 
     import torch
@@ -102,49 +172,10 @@ def main() -> None:
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from ovlgraph import OverlapEngine
-    from ovlgraph.candidates import dedup_reads, enumerate_candidates
-    from ovlgraph.reads import CONFIGS, config_reads
+    w = Workload(args.config, seed=rank, dev=dev)
+    elapsed, kernel_ms = timed_steps(w, args.steps, args.warmup, dev, world)
 
-    cfg = CONFIGS[args.config]
-    t_setup = time.perf_counter()
-    reads, _ = dedup_reads(config_reads(args.config, seed=rank))
-    a, b = enumerate_candidates(reads, cfg["k"])
-    t_enum = time.perf_counter() - t_setup
-    eng = OverlapEngine(local)
-    t0 = time.perf_counter()
-    eng.set_reads(reads)
-    t_pack = time.perf_counter() - t0
-    kernel = eng.plan()
-    n_pairs = int(a.shape[0])
-    da = torch.as_tensor(a, device=dev)
-    db = torch.as_tensor(b, device=dev)
-    ds = torch.empty(n_pairs, dtype=torch.int32, device=dev)
-    de = torch.empty(n_pairs, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    for _ in range(args.warmup):
-        eng.score_tensors(da, db, ds, de)
-    torch.cuda.synchronize(dev)
-    eng.check_device_errors()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        eng.score_tensors(da, db, ds, de)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
-
-    stats = torch.tensor([elapsed, kernel_ms, float(n_pairs)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, kernel_ms, float(w.n_pairs)], dtype=torch.float64, device=dev)
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -153,11 +184,10 @@ def main() -> None:
         elapsed, kernel_ms = float(mx[0]), float(mx[1])
         total_pairs = int(tot[2])
     else:
-        total_pairs = n_pairs
+        total_pairs = w.n_pairs
 
     if rank == 0:
-        lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
-        algo = algorithmic_bytes(lens, a, b)
+        algo = w.algo_bytes()
         achieved = algo / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         line = {
             "metric": METRIC,
@@ -174,11 +204,11 @@ def main() -> None:
             "data": "synthetic",
             "config": {
                 "workload": f"{args.config}: {WORKLOAD_DESC[args.config]}",
-                "reads_per_gpu": len(reads),
-                "pairs_per_gpu": n_pairs,
-                "read_length": cfg["l"],
+                "reads_per_gpu": len(w.reads),
+                "pairs_per_gpu": w.n_pairs,
+                "read_length": w.cfg["l"],
                 "parallelism": f"pair-sharded x{world} (one process per GPU, own seeded read set per rank)",
-                "kernel": kernel,
+                "kernel": w.kernel,
             },
             "roofline": {
                 "bound": "hbm",
@@ -186,14 +216,29 @@ def main() -> None:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(args.config, kernel_ms),
+                "traffic": load_traffic(args.config),
                 "kernel_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": algo,
             },
-            "host_setup_s": {"read_sim_and_enumeration": round(t_enum, 3), "upload_and_pack": round(t_pack, 4)},
+            "host_setup_s": {"read_sim_and_enumeration": round(w.t_enum, 3), "upload_and_pack": round(w.t_pack, 4)},
         }
+        if world == 1 and not args.no_extra:
+            extra = {}
+            for name in ("target", "cfg3"):
+                if name == args.config:
+                    continue
+                x = Workload(name, seed=0, dev=dev, engine=w.eng)
+                el, km = timed_steps(x, max(20, args.steps // 4), 3, dev, 1)
+                xa = x.algo_bytes()
+                extra[name] = {"workload": WORKLOAD_DESC[name], "pairs": x.n_pairs,
+                               "value": x.n_pairs * max(20, args.steps // 4) / el, "kernel_ms": km,
+                               "kernel_pairs_per_s": x.n_pairs / (km * 1e-3),
+                               "roofline_frac": xa / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel": x.kernel}
+                del x
+            line["extra_configs"] = extra
+            w.eng.set_reads(w.reads)
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(reads, a, b, args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(w.reads, w.a, w.b, args.cpu_budget)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

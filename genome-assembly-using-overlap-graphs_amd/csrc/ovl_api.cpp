@@ -21,7 +21,7 @@
 
 namespace {
 
-constexpr int32_t kFastMaxLen = 256;   // bit-plane layout up to 8 words of 32 bases
+constexpr int32_t kFastMaxLen = 256;   // bit-plane layouts up to W = 8 words of 32 bases
 constexpr int32_t kDpMaxLen = 8192;    // DP kernel: LDS row of the t read
 
 struct DevBuf {
@@ -43,10 +43,12 @@ struct ovl_ctx {
     int32_t lmax = 0;
     int32_t planes = 2;
     int32_t wmax = 0;  // 0: no bit-plane layout (reads longer than kFastMaxLen)
-    int32_t zs = 0;
+    int32_t srow = 0;  // sfx row stride (words)
+    int32_t trow = 0;  // pfx row stride (words)
     DevBuf codes, off, len, sfx, pfx, lut;
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
+    DevBuf side, counters;  // side-list regions of non-uniform pairs + per-region counts
 };
 
 namespace {
@@ -121,8 +123,12 @@ int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, 
     // ungapped closed form: exact when gaps cannot win and no int32 store can wrap
     if (c->wmax > 0 && gaps_cannot_win(match, mismatch, indel, L) && amax * L < (int64_t(1) << 31)) {
         p.kernel = OVL_KERNEL_UNGAPPED;
-        const int64_t top = L * std::max<int64_t>(0, std::max<int64_t>(match, mismatch));
-        p.key64 = !(top < (1 << 15) && L < (1 << 16));
+        // 32-bit keys (score << 16) - j need |score| < 2^15 on both sides, and the
+        // folded form X * ((mismatch - match) << 16) + ... a 24-bit multiplier
+        const int64_t dms = (int64_t)mismatch - (int64_t)match;
+        // (the uniform sweep compares keys without their block constant: |score| + 32*amax
+        //  must stay below 2^15 as well)
+        p.key64 = !(amax * (2 * L + 32) < (1 << 15) && iabs64(dms) < 128);
     } else {
         if (c->lmax > kDpMaxLen)
             return fail(c, OVL_E_UNSUPPORTED, "gapped DP supports reads up to %d bases (longest is %d)", kDpMaxLen,
@@ -136,9 +142,26 @@ int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, 
     return OVL_OK;
 }
 
+int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
+                       int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
+                       hipStream_t s);
+
+// Kernels index pairs of one launch with int32 (side-list entries); split huge lists.
 int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                  int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                  hipStream_t s) {
+    constexpr int64_t kChunk = int64_t(1) << 30;
+    for (int64_t lo = 0; lo < n_pairs; lo += kChunk) {
+        const int64_t n = std::min(kChunk, n_pairs - lo);
+        int rc = launch_score_chunk(c, pl, d_a + lo, d_b + lo, n, match, mismatch, indel, d_score + lo, d_end + lo, s);
+        if (rc != OVL_OK) return rc;
+    }
+    return OVL_OK;
+}
+
+int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
+                       int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
+                       hipStream_t s) {
     if (n_pairs == 0) return OVL_OK;
     if (pl.kernel == OVL_KERNEL_UNGAPPED) {
         OvlUngappedArgs g{};
@@ -149,10 +172,26 @@ int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* 
         g.a_idx = d_a;
         g.b_idx = d_b;
         g.n_pairs = n_pairs;
-        int32_t tile = 64;
-        const int64_t want_waves = (int64_t)c->cu_count * 32;
-        while (tile > 8 && (n_pairs + tile - 1) / tile < want_waves) tile >>= 1;
-        g.tile = tile;
+        // split a pair's 32 bit shifts over 1, 2 or 4 lanes until the grid has
+        // enough wavefronts to fill every SIMD a few times
+        int32_t rs_log2 = 0;
+        const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
+        while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
+        g.rs_log2 = rs_log2;
+        // uniform-length fast path (2 bit planes): reads of length lmax; the rest go
+        // through the side list (capacity n_pairs)
+        g.lw = c->planes == 2 ? c->lmax : 0;
+        g.max_blocks = (int64_t)c->cu_count * 8;
+        if (g.lw > 0) {
+            int32_t regions = 0, cap = 0;
+            const int64_t entries = ovl_uniform_side_layout(n_pairs, g.max_blocks, &regions, &cap);
+            HIPCHK(c, ensure(c->side, sizeof(int4) * (size_t)entries));
+            HIPCHK(c, ensure(c->counters, sizeof(int32_t) * (size_t)regions));
+            g.side = as<int4>(c->side);
+            g.side_cnt = as<int32_t>(c->counters);
+            g.side_cap = cap;
+            g.side_regions = regions;
+        }
         g.match = match;
         g.mismatch = mismatch;
         g.out_score = d_score;
@@ -244,7 +283,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->a, &c->b, &c->score, &c->end,
-                      &c->tb, &c->err_flag})
+                      &c->tb, &c->err_flag, &c->side, &c->counters})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -280,12 +319,11 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     for (int v = 0; v < 256; ++v)
         if (present[v]) lut[v] = (uint8_t)k++;
     const int planes = k <= 4 ? 2 : (k <= 16 ? 4 : 8);
+    // bit-plane layouts: W = ceil(lmax/32) words of 32 bases, rows padded to 16 bytes
     int32_t wmax = 0;
-    if (lmax <= 64) wmax = 2;
-    else if (lmax <= 128) wmax = 4;
-    else if (lmax <= kFastMaxLen) wmax = 8;
-    const int32_t nch = wmax ? (32 * wmax + 64) / 64 : 0;
-    const int32_t zs = wmax ? 2 * nch + 2 : 0;
+    if (lmax <= kFastMaxLen) wmax = std::max(1, (lmax + 31) / 32);
+    const int32_t srow = wmax ? ((wmax * planes + 3) & ~3) : 0;
+    const int32_t trow = wmax ? (((wmax + 1) * planes + 3) & ~3) : 0;
 
     c->n_reads = -1;  // invalid until fully built
     DevBuf raw;
@@ -310,13 +348,17 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
             if (e != hipSuccess) break;
         }
         if (wmax > 0) {
-            const size_t words = (size_t)std::max(n_reads, 1) * planes;
-            e = ensure(c->sfx, words * wmax * sizeof(uint32_t));
+            const size_t rows = (size_t)std::max(n_reads, 1);
+            e = ensure(c->sfx, rows * srow * sizeof(uint32_t));
             if (e != hipSuccess) break;
-            e = ensure(c->pfx, words * zs * sizeof(uint32_t));
+            e = ensure(c->pfx, rows * trow * sizeof(uint32_t));
+            if (e != hipSuccess) break;
+            e = hipMemsetAsync(c->sfx.p, 0, rows * srow * sizeof(uint32_t), c->stream);
+            if (e != hipSuccess) break;
+            e = hipMemsetAsync(c->pfx.p, 0, rows * trow * sizeof(uint32_t), c->stream);
             if (e != hipSuccess) break;
             e = ovl_launch_pack(planes, as<uint8_t>(c->codes), as<int64_t>(c->off), as<int32_t>(c->len), n_reads,
-                                wmax, zs, as<uint32_t>(c->sfx), as<uint32_t>(c->pfx), c->stream);
+                                wmax, srow, trow, as<uint32_t>(c->sfx), as<uint32_t>(c->pfx), c->stream);
             if (e != hipSuccess) break;
         }
         e = hipStreamSynchronize(c->stream);
@@ -327,7 +369,8 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     c->lmax = lmax;
     c->planes = planes;
     c->wmax = wmax;
-    c->zs = zs;
+    c->srow = srow;
+    c->trow = trow;
     c->n_reads = n_reads;
     return rc;
 }
@@ -364,7 +407,7 @@ OVL_API int ovl_score_device(ovl_ctx* c, const int32_t* d_a, const int32_t* d_b,
     if (rc != OVL_OK) return rc;
     if (n_pairs > 0 && c->n_reads == 0) return fail(c, OVL_E_INDEX, "pairs given but the read set is empty");
     HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the default (null) stream
     return launch_score(c, p, d_a, d_b, n_pairs, match, mismatch, indel, d_score, d_end, s);
 }
 

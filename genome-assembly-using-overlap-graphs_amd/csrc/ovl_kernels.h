@@ -11,15 +11,20 @@ struct OvlUngappedArgs {
     const int32_t* a_idx;
     const int32_t* b_idx;
     int64_t n_pairs;
-    int32_t tile;        // pairs per wavefront tile (8..64)
+    int32_t rs_log2;     // lanes per pair = 1 << rs_log2 (splits the bit shifts r)
     int32_t match;
     int32_t mismatch;
     int32_t* out_score;
     int32_t* out_end;
     uint32_t* err_flag;
     int32_t planes;      // 2, 4 or 8 bit planes per base
-    int32_t wmax;        // 2, 4 or 8 words of 32 bases (read length <= 32*wmax)
-    int32_t key64;       // 64-bit (score, end) keys when scores can reach 2^15
+    int32_t wmax;        // W = 1..8 words of 32 bases (read length <= 32*W)
+    int32_t key64;       // 64-bit (score, end) keys (else 32-bit folded keys)
+    int32_t lw;          // uniform read length for uniform_kernel (0: general kernel only)
+    int4* side;          // side-list regions {pair, a, b, 0}: side_regions x side_cap entries
+    int32_t* side_cnt;   // entries per region (written by uniform_kernel every call)
+    int32_t side_cap;
+    int32_t side_regions;
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
 };
 
@@ -45,7 +50,9 @@ struct OvlDpArgs {
 extern "C" hipError_t ovl_launch_map_codes(const uint8_t* raw, const uint8_t* lut, uint8_t* codes, int64_t n,
                                            hipStream_t stream);
 extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const int64_t* off, const int32_t* len,
-                                      int32_t n_reads, int32_t wmax, int32_t zs, uint32_t* sfx, uint32_t* pfx,
-                                      hipStream_t stream);
+                                      int32_t n_reads, int32_t w, int32_t srow, int32_t trow, uint32_t* sfx,
+                                      uint32_t* pfx, hipStream_t stream);
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream_t stream);
+// side-list geometry of the uniform path for n_pairs: regions (= wavefronts) and entries per region
+extern "C" int64_t ovl_uniform_side_layout(int64_t n_pairs, int64_t max_blocks, int32_t* regions, int32_t* cap);
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);

@@ -7,26 +7,27 @@
 // Kernels
 //   map_codes     bytes -> dense symbol codes (LUT), one lane per byte.
 //   pack_planes   codes -> bit-plane words in two layouts (prefix / suffix),
-//                 one lane per (read, word).  HBM-bound byte work, run once per read set.
+//                 one lane per (read, word).  Byte work, run once per read set.
 //   ungapped      THE hot kernel.  Exact whenever gaps cannot win (the reference's
 //                 default indel = -2**31): dp[n][j] is the sum over
 //                 the L=min(n,j) diagonal cells ending at (n, j), so
 //                   score(j) = match*L + (mismatch-match)*X(j),  X = mismatch count.
-//                 One wavefront per pair; lane l owns end positions j = 64*c + l.
-//                 Bases are bit-planes (P planes, 32 bases per uint32 word); a
-//                 mismatch word is OR_p(S_p ^ T_p) and X accumulates with v_bcnt.
-//                 No MFMA: this is integer compare/popcount work (BASELINE north_star).
+//                 Lane-per-pair: a lane holds both reads as bit-planes (P planes, 32
+//                 bases per uint32 word) and sweeps every end position j; a mismatch
+//                 word is OR_p(S_p ^ T_p) and X accumulates with v_bcnt.  No MFMA:
+//                 integer compare/popcount work (BASELINE north_star).
 //   dp            anti-diagonal wavefront DP for any scoring (finite indel), int64
 //                 arithmetic with int32 stores like Numba; lanes own rows, the row
 //                 carried between 64-row strips and the t symbols are staged in LDS.
 //
-// Layouts (per read r, uint32 words, P planes interleaved per word):
-//   sfx[r][k][p], k in [0, WMAX):   read right-aligned so that its last base is
-//                                   bit 31 of word WMAX-1 (position 32*WMAX-n+i).
-//   pfx[r][z][p], z in [0, ZS):     two zero words, then the read left-aligned
-//                                   (base i at word 2 + i/32, bit i%32), zero tail.
+// Layouts (per read, W = ceil(lmax/32) words of 32 bases, P planes interleaved per
+// word, rows padded to 16 bytes):
+//   sfx[r][k*P + p], k < W:       read right-aligned: base i at position 32W - n + i
+//   pfx[r][x*P + p], x < W + 1:   read left-aligned: base i at position i; word W is zero
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "ovl_kernels.h"
 
@@ -45,255 +46,406 @@ __global__ void map_codes_kernel(const uint8_t* __restrict__ raw, const uint8_t*
     for (; i < n; i += stride) codes[i] = lut[raw[i]];
 }
 
+// One lane per (read, word).  Both rows were zeroed beforehand (row padding and the
+// zero word W of the prefix layout stay zero).
 template <int P>
 __global__ void pack_planes_kernel(const uint8_t* __restrict__ codes, const int64_t* __restrict__ off,
-                                   const int32_t* __restrict__ len, int32_t n_reads, int32_t wmax,
-                                   int32_t zs, uint32_t* __restrict__ sfx, uint32_t* __restrict__ pfx) {
-    const int nw = wmax > zs ? wmax : zs;
+                                   const int32_t* __restrict__ len, int32_t n_reads, int32_t w,
+                                   int32_t srow, int32_t trow, uint32_t* __restrict__ sfx,
+                                   uint32_t* __restrict__ pfx) {
     int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)n_reads * nw;
+    const int64_t total = (int64_t)n_reads * w;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (; gid < total; gid += stride) {
-        const int32_t r = (int32_t)(gid / nw);
-        const int32_t w = (int32_t)(gid % nw);
+        const int32_t r = (int32_t)(gid / w);
+        const int32_t k = (int32_t)(gid % w);
         const int32_t n = len[r];
         const uint8_t* s = codes + off[r];
-        if (w < zs) {
-            uint32_t pl[P];
+        uint32_t pl[P], sl[P];
 #pragma unroll
-            for (int p = 0; p < P; ++p) pl[p] = 0u;
-            const int32_t d = w - 2;  // data word index
-            if (d >= 0) {
-                for (int b = 0; b < 32; ++b) {
-                    const int32_t i = 32 * d + b;
-                    if (i < n) {
-                        const uint32_t c = s[i];
+        for (int p = 0; p < P; ++p) { pl[p] = 0u; sl[p] = 0u; }
+        const int32_t shift = 32 * w - n;  // suffix layout: base i sits at position shift + i
+        for (int b = 0; b < 32; ++b) {
+            const int32_t i = 32 * k + b;      // prefix layout
+            if (i < n) {
+                const uint32_t c = s[i];
 #pragma unroll
-                        for (int p = 0; p < P; ++p) pl[p] |= ((c >> p) & 1u) << b;
-                    }
-                }
+                for (int p = 0; p < P; ++p) pl[p] |= ((c >> p) & 1u) << b;
             }
+            const int32_t u = i - shift;       // suffix layout
+            if (u >= 0 && u < n) {
+                const uint32_t c = s[u];
 #pragma unroll
-            for (int p = 0; p < P; ++p) pfx[((int64_t)r * zs + w) * P + p] = pl[p];
+                for (int p = 0; p < P; ++p) sl[p] |= ((c >> p) & 1u) << b;
+            }
         }
-        if (w < wmax) {
-            uint32_t pl[P];
 #pragma unroll
-            for (int p = 0; p < P; ++p) pl[p] = 0u;
-            const int32_t shift = 32 * wmax - n;  // position of base 0
-            for (int b = 0; b < 32; ++b) {
-                const int32_t i = 32 * w + b - shift;
-                if (i >= 0 && i < n) {
-                    const uint32_t c = s[i];
-#pragma unroll
-                    for (int p = 0; p < P; ++p) pl[p] |= ((c >> p) & 1u) << b;
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < P; ++p) sfx[((int64_t)r * wmax + w) * P + p] = pl[p];
+        for (int p = 0; p < P; ++p) {
+            pfx[(int64_t)r * trow + k * P + p] = pl[p];
+            sfx[(int64_t)r * srow + k * P + p] = sl[p];
         }
     }
 }
 
 // ----------------------------------------------------------------------------- ungapped
 
-template <typename KeyT>
-struct KeyOps;
+// (score, end) keys: key = score * 2^B - j, positive iff score > 0; the larger
+// score wins, then the smaller j -- exactly the strict '>' first-argmax scan of
+// aligners.py:54-57, which starts from dp[n][0] = 0 (so key <= 0 means (0, 0)).
+template <int KM>
+struct Key;
 
 template <>
-struct KeyOps<uint32_t> {
-    // score in [1, 2^15), j in [0, 2^16): max key = max score, then min j
-    __device__ static uint32_t make(int64_t score, int32_t j) {
-        return ((uint32_t)score << 16) | (uint32_t)(0xFFFF - j);
+struct Key<0> {  // int32 keys, B = 16: needs |score| < 2^15 and j < 2^16
+    using T = int32_t;
+    __device__ static T make(int32_t score, int32_t j) { return (int32_t)((uint32_t)score << 16) - j; }
+    // uniform pairs: key = X * (dms << 16) + j * ((match << 16) - 1), one v_mad_i32_i24
+    __device__ static T make_folded(uint32_t X, int32_t d2, int32_t kj) {
+        const int32_t xs = ((int32_t)X << 8) >> 8;   // both factors provably 24-bit:
+        const int32_t ds = (d2 << 8) >> 8;           // one v_mad_i32_i24
+        return xs * ds + kj;
     }
-    __device__ static uint32_t wave_max(uint32_t v) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const uint32_t o = (uint32_t)__shfl_xor((int)v, off, 64);
-            v = v > o ? v : o;
-        }
-        return v;
-    }
-    __device__ static void decode(uint32_t key, int32_t& score, int32_t& end) {
-        score = key ? (int32_t)(key >> 16) : 0;
-        end = key ? (int32_t)(0xFFFF - (key & 0xFFFF)) : 0;
+    __device__ static void decode(T key, int32_t& score, int32_t& end) {
+        score = key > 0 ? (key + 0xFFFF) >> 16 : 0;
+        end = key > 0 ? (int32_t)((uint32_t)score << 16) - key : 0;
     }
 };
 
 template <>
-struct KeyOps<uint64_t> {
-    __device__ static uint64_t make(int64_t score, int32_t j) {
-        return ((uint64_t)(uint32_t)score << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)j);
-    }
-    __device__ static uint64_t wave_max(uint64_t v) {
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, off, 64);
-            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), off, 64);
-            const uint64_t o = ((uint64_t)hi << 32) | lo;
-            v = v > o ? v : o;
-        }
-        return v;
-    }
-    __device__ static void decode(uint64_t key, int32_t& score, int32_t& end) {
-        score = key ? (int32_t)(uint32_t)(key >> 32) : 0;
-        end = key ? (int32_t)(0xFFFFFFFFu - (uint32_t)key) : 0;
+struct Key<1> {  // int64 keys, B = 32: any int32 score
+    using T = int64_t;
+    __device__ static T make(int32_t score, int32_t j) { return (int64_t)score * 4294967296ll - j; }
+    __device__ static void decode(T key, int32_t& score, int32_t& end) {
+        score = key > 0 ? (int32_t)((key + 0xFFFFFFFFll) >> 32) : 0;
+        end = key > 0 ? (int32_t)((int64_t)score * 4294967296ll - key) : 0;
     }
 };
 
-template <int P>
-__device__ __forceinline__ void load_planes(const uint32_t* __restrict__ src, uint32_t (&dst)[P]) {
-    if constexpr (P == 2) {
-        const uint2 v = *reinterpret_cast<const uint2*>(src);
-        dst[0] = v.x; dst[1] = v.y;
-    } else if constexpr (P % 4 == 0) {
+template <int N>
+__device__ __forceinline__ void load_words(const uint32_t* __restrict__ src, uint32_t (&dst)[N]) {
+    static_assert(N % 4 == 0, "rows are padded to 16 bytes");
 #pragma unroll
-        for (int q = 0; q < P / 4; ++q) {
-            const uint4 v = *reinterpret_cast<const uint4*>(src + 4 * q);
-            dst[4 * q + 0] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int p = 0; p < P; ++p) dst[p] = src[p];
+    for (int q = 0; q < N / 4; ++q) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + 4 * q);
+        dst[4 * q + 0] = v.x; dst[4 * q + 1] = v.y; dst[4 * q + 2] = v.z; dst[4 * q + 3] = v.w;
     }
 }
 
-// Score one pair; every lane returns the wave-wide best key.
-//   s = read a (suffix layout, right-aligned in WMAX words), length n, WP = ceil(n/32)
-//   t = read b (prefix layout), length m, nch = ceil((m+1)/64) chunks of 64 end positions.
-// Lane l = 32h + r handles j = 64c + l.  With j = 32q + r (q = 2c + h), position x of the
-// right-aligned s' (WP words) meets t position x + j - 32*WP; the t words it needs are
-//   T_r[y] = t-bits [32y - 32 + r, 32y + r)  (y >= 0; t-bit < 0 is padding)
-// and row q pairs s' word k = WP-1-(q-y) with T_r[y] for y in [max(0, q-WP+1), q].
-// Half h keeps the array U[z] = T_r[z - 1 + h], so row q = 2c+h reads U[y - h + 1]
-// with z = y' + 1, y' in [max(-1, 2c-WP+1), 2c]: a compile-time register index.
-// Invalid bits: t padding only in T_r[0] (bits < 32-r), s padding only in word k=0
-// (bits < 32*WP-n); both masked.  Everything else in the row is a real comparison.
-template <int P, int WMAX, int WP, typename KeyT>
-__device__ __forceinline__ KeyT score_pair_wp(const uint32_t* __restrict__ sfx_a,
-                                              const uint32_t* __restrict__ pfx_b, int32_t n,
-                                              int32_t m, int32_t match, int32_t mismatch,
-                                              int lane) {
-    constexpr int NCHMAX = (32 * WMAX + 64) / 64;  // ceil((32*WMAX + 1) / 64)
-    constexpr int NZ = 2 * NCHMAX;                 // U words z in [0, NZ)
-    const int nch = (m + 64) >> 6;
-    const uint32_t h = (uint32_t)lane >> 5;
-    const uint32_t r = (uint32_t)lane & 31u;
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
+}
 
-    // s words: wave-uniform (scalar loads / SGPR operands).
-    uint32_t S[WP][P];
-    const uint32_t* sp = sfx_a + (WMAX - WP) * P;
-#pragma unroll
-    for (int k = 0; k < WP; ++k) load_planes<P>(sp + k * P, S[k]);
+template <typename T>
+__device__ __forceinline__ T group_max(T best, int ppw) {
+    // combine the RS lanes of a pair (lanes slot, slot + ppw, ...)
+    for (int off = 32; off >= ppw; off >>= 1) {
+        if constexpr (sizeof(T) == 4) {
+            best = max(best, (T)__shfl_xor((int)best, off, 64));
+        } else {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)best, off, 64);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)best >> 32), off, 64);
+            const T o = (T)(((uint64_t)hi << 32) | lo);
+            best = o > best ? o : best;
+        }
+    }
+    return best;
+}
 
-    // t words for this half: Tw[y] = pfx word (y + h), y in [0, NZ].
-    uint32_t Tw[NZ + 1][P];
-    const uint32_t* tp = pfx_b + h * P;
+// Bit-shift body shared by both ungapped kernels.
+//
+// Coordinates: s is right-aligned in W words (s' position 32W - n + i holds
+// base i) and t is left-aligned behind W zero words (t'' position 32W + u holds
+// base u).  For end position j (aligners.py:54 scans j = 0..m of the last row),
+// s' position x meets t'' position x + j.  With j = 32q + r, s' word k meets the
+// funnel-shifted t'' word T_r[k + q] = bits [32(k+q) + r, 32(k+q) + r + 32) of t''.
+// Words k < W-1-q only meet t padding; T_r[W-1] is partly padding (bits < 32-r).
+// X(j) = popcount of OR_p(S_p ^ T_p) over the valid bits, and
+//   dp[n][j] = match * L + (mismatch - match) * X,   L = min(n, j)
+// whenever gaps cannot win.  T_r is built once per r and
+// reused for every q, so the inner loop is xor / bitop3 / popcount with
+// compile-time register indices.
+//
+// UNI (uniform pairs, n = m = lw = lmax): j <= n always, so L = j, the window never
+// reaches s padding (no per-lane mask) and the key folds to one mad24.
+template <int P, int W, int KM, bool UNI, bool RS1 = false>
+__device__ __forceinline__ typename Key<KM>::T sweep_shifts(const uint32_t* Sw, const uint32_t* Tw,
+                                                            const uint32_t* SV, int32_t n, int32_t m,
+                                                            int32_t jmax, int r0, int rs_log2,
+                                                            int32_t match, int32_t dms) {
+    using T = typename Key<KM>::T;
+    constexpr int TW = W + 1;
+    const int RS = RS1 ? 1 : 1 << rs_log2;
+    const int32_t d2 = (int32_t)((uint32_t)dms << 16);
+    const int32_t m2 = (int32_t)((uint32_t)match << 16) - 1;
+    T best = 0;
+    for (int it = 0; it < (RS1 ? 32 : (32 >> rs_log2)); ++it) {
+        // RS1: one lane per pair, every lane of the wavefront is on the same bit
+        // shift, so r and everything derived from it is scalar (SGPR)
+        const uint32_t r = RS1 ? (uint32_t)it : (uint32_t)(r0 + it * RS);
+        const int rmin = it * RS;                 // smallest / largest r in the wavefront
+        const int rmax = rmin + RS - 1;
+        if (rmin > jmax) break;                   // j = r > jmax for every lane
+        const uint32_t vt = r ? (0xFFFFFFFFu << (32u - r)) : 0u;  // valid bits of T_r[W-1]
+        // U[i] = T_r[W - 1 + i], i = 0..W   (T_r[W-1] takes its low word from zero padding)
+        uint32_t U[TW][P];
 #pragma unroll
-    for (int y = 0; y <= NZ; ++y) load_planes<P>(tp + y * P, Tw[y]);
-
-    const uint32_t vt = r ? (0xFFFFFFFFu << (32u - r)) : 0u;  // valid bits of T_r[0]
-    const uint32_t vu0 = h ? vt : 0u;
-    const uint32_t vu1 = h ? 0xFFFFFFFFu : vt;
-    const uint32_t sv0 = 0xFFFFFFFFu << (uint32_t)(32 * WP - n);  // valid bits of s' word 0
-
-    uint32_t U[NZ][P];
-    KeyT best = 0;
-    const int64_t dms = (int64_t)mismatch - (int64_t)match;
+        for (int i = 0; i < TW; ++i) {
 #pragma unroll
-    for (int c = 0; c < NCHMAX; ++c) {
-        if (c < nch) {  // wave-uniform
-            constexpr int dummy = 0; (void)dummy;
-            const int zlo = (2 * c - WP + 2) > 0 ? (2 * c - WP + 2) : 0;
-#pragma unroll
-            for (int z = 2 * c; z <= 2 * c + 1; ++z) {
-                if (z >= zlo) {
-#pragma unroll
-                    for (int p = 0; p < P; ++p) U[z][p] = alignbit(Tw[z + 1][p], Tw[z][p], r);
-                }
+            for (int c = 0; c < P; ++c) {
+                const uint32_t hi = Tw[i * P + c];
+                const uint32_t lo = i ? Tw[(i - 1) * P + c] : 0u;
+                U[i][c] = alignbit(hi, lo, r);
             }
+        }
+        const int32_t kr = (int32_t)r * m2;
+#pragma unroll
+        for (int q = 0; q <= W; ++q) {
+            if (32 * q + rmin > jmax) break;      // wave-uniform
+            const int32_t j = 32 * q + (int32_t)r;
             uint32_t X = 0;
 #pragma unroll
-            for (int z = zlo; z <= 2 * c + 1; ++z) {
-                const int k = WP - 2 - 2 * c + z;  // s word paired with U[z]
-                uint32_t mm = 0;
+            for (int k = (W - 1 - q > 0 ? W - 1 - q : 0); k < W; ++k) {
+                const int i = k + q - (W - 1);    // U index
+                // mismatch word: OR over planes of (S ^ T); v_bitop3 LUT 0xBE = (a ^ b) | c
+                uint32_t mm = Sw[k * P] ^ U[i][0];
 #pragma unroll
-                for (int p = 0; p < P; ++p) mm |= S[k][p] ^ U[z][p];
-                if (z == 0) mm &= vu0;
-                if (z == 1) mm &= vu1;
-                if (k == 0) mm &= sv0;
+                for (int c = 1; c < P; ++c) mm = __builtin_amdgcn_bitop3_b32(Sw[k * P + c], U[i][c], mm, 0xBE);
+                if (i == 0) mm &= vt;
+                if constexpr (!UNI) mm &= SV[k];
                 X += (uint32_t)__builtin_popcount(mm);
             }
-            const int32_t j = 64 * c + lane;
-            const int32_t L = n < j ? n : j;
-            const int64_t score = (int64_t)match * L + dms * (int64_t)X;
-            const bool valid = (j >= 1) & (j <= m) & (score > 0);
-            const KeyT key = valid ? KeyOps<KeyT>::make(score, j) : (KeyT)0;
-            best = key > best ? key : best;
+            T key;
+            if constexpr (UNI && KM == 0) {
+                key = Key<0>::make_folded(X, d2, kr + 32 * q * m2);
+            } else {
+                const int32_t L = n < j ? n : j;
+                key = Key<KM>::make(match * L + dms * (int32_t)X, j);
+            }
+            if constexpr (UNI && RS1) {
+                if (j <= jmax) best = key > best ? key : best;   // scalar condition
+            } else if (UNI && 32 * q + rmax <= jmax) {
+                best = key > best ? key : best;   // every lane's j is in range
+            } else {
+                best = (j <= m && key > best) ? key : best;
+            }
         }
     }
-    return KeyOps<KeyT>::wave_max(best);
+    return best;
 }
 
-template <int P, int WMAX, typename KeyT, int WP = 1>
-__device__ __forceinline__ KeyT score_pair(const uint32_t* __restrict__ sfx_a,
-                                           const uint32_t* __restrict__ pfx_b, int32_t n, int32_t m,
-                                           int32_t match, int32_t mismatch, int lane, int wp) {
-    if constexpr (WP == WMAX) {
-        return score_pair_wp<P, WMAX, WP, KeyT>(sfx_a, pfx_b, n, m, match, mismatch, lane);
+// Sweep for uniform pairs (n = m = lw, P = 2, one lane per pair): every lane of
+// the wavefront is on the same bit shift r, so r-derived values are scalar and
+// no per-lane masking is needed (j <= lw = n means L = j and the window never
+// reaches s padding).  Blocks q <= W-2 are always in range; block W-1 holds
+// j = 32(W-1) + r <= lw iff r <= rcut = lw - 32(W-1); block W only j = 32W
+// (r = 0, lw = 32W).  The r loop is split on rcut, so no end position needs a
+// branch.  Per block q the running max is kept without its q-constant
+// (key = keyq + 32q*M', M' = (match << 16) - 1), so an end position costs one
+// v_mad_i32_i24 and one v_max.
+template <int W, int KM>
+__device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw, const uint32_t* Tw, int32_t lw,
+                                                             int32_t match, int32_t dms) {
+    using T = typename Key<KM>::T;
+    constexpr int P = 2;
+    constexpr int TW = W + 1;
+    const int32_t rcut = lw - 32 * (W - 1);  // 1..32
+    T best[W + 1];
+    T qoff[W + 1];
+    T mq;  // M' as T
+    if constexpr (KM == 0) {
+        mq = (int32_t)((uint32_t)match << 16) - 1;
     } else {
-        if (wp == WP) return score_pair_wp<P, WMAX, WP, KeyT>(sfx_a, pfx_b, n, m, match, mismatch, lane);
-        return score_pair<P, WMAX, KeyT, WP + 1>(sfx_a, pfx_b, n, m, match, mismatch, lane, wp);
+        mq = (int64_t)match * 4294967296ll - 1;
     }
+#pragma unroll
+    for (int q = 0; q <= W; ++q) {
+        qoff[q] = (T)(32 * q) * mq;
+        best[q] = -qoff[q];  // "key <= 0" for block q
+    }
+    const int32_t d16 = (int32_t)((uint32_t)dms << 16);
+    const int32_t dv = __builtin_amdgcn_readfirstlane(d16);
+    // one r iteration over blocks [0, NQ) (NQ compile-time), r scalar
+    auto body = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        uint32_t U[TW][P];
+#pragma unroll
+        for (int i = 0; i < TW; ++i) {
+            if (i < NQ || (NQ > W && i <= W)) {
+#pragma unroll
+                for (int c = 0; c < P; ++c) {
+                    const uint32_t hi = Tw[i * P + c];
+                    const uint32_t lo = i ? Tw[(i - 1) * P + c] : 0u;
+                    U[i][c] = alignbit(hi, lo, r);
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            uint32_t X = 0;
+#pragma unroll
+            for (int k = (W - 1 - q > 0 ? W - 1 - q : 0); k < W; ++k) {
+                const int i = k + q - (W - 1);
+                uint32_t mm = __builtin_amdgcn_bitop3_b32(Sw[k * P + 1], U[i][1], Sw[k * P] ^ U[i][0], 0xBE);
+                if (i == 0) mm &= vt;
+                X += (uint32_t)__builtin_popcount(mm);
+            }
+            T key;
+            if constexpr (KM == 0) {
+                key = ((int32_t)X * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24
+            } else {
+                key = (int64_t)dms * 4294967296ll * (int64_t)X + rm;
+            }
+            best[q] = key > best[q] ? key : best[q];
+        }
+    };
+    // r = 0: j = 32q (q >= 1); block W only when lw == 32W
+    {
+        T rm0 = 0;
+        if (rcut == 32) {
+            body(0u, 0u, rm0, std::integral_constant<int, W + 1>{});
+        } else {
+            body(0u, 0u, rm0, std::integral_constant<int, W>{});
+        }
+    }
+    T rm = mq;
+    uint32_t r = 1;
+    const uint32_t rc = (uint32_t)(rcut < 31 ? rcut : 31);
+    for (; r <= rc; ++r) {  // blocks 0..W-1
+        const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> (r - 1));
+        body(r, vt, rm, std::integral_constant<int, W>{});
+        rm += mq;
+    }
+    for (; r < 32; ++r) {  // blocks 0..W-2
+        const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> (r - 1));
+        body(r, vt, rm, std::integral_constant<int, W - 1>{});
+        rm += mq;
+    }
+    T out = 0;
+#pragma unroll
+    for (int q = 0; q <= W; ++q) {
+        const T k = best[q] + qoff[q];
+        out = k > out ? k : out;
+    }
+    return out;
 }
 
-// Grid-stride over tiles of `tile` consecutive pairs; one wavefront per tile.
-// Lane i of the wave owns pair base+i: it gathers the indices and lengths
-// (coalesced) and keeps the result, stored once per tile (coalesced).
-template <int P, int WMAX, typename KeyT>
-__global__ __launch_bounds__(256) void ungapped_kernel(
+// Uniform-pair kernel (P = 2 bit planes, reads of one length lw = lmax, the
+// common case of simulated reads).  One lane per pair, so every lane of a
+// wavefront sweeps the same bit shift r (scalar).  Pairs that are not
+// (lw, lw) -- e.g. reads truncated at the genome end (generateErrorFreeReads.py
+// :45-46) -- are written to this wavefront's own region of the side list
+// (`cap` entries per wavefront, count in side_cnt[wave]); general_kernel scores
+// them next.  No atomics: the regions are disjoint and every count is rewritten
+// by every call.
+template <int W, int KM>
+__global__ __launch_bounds__(256) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
-    int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx,
-    int64_t n_pairs, int32_t tile, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score,
-    int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
-    constexpr int NCHMAX = (32 * WMAX + 64) / 64;
-    constexpr int ZS = 2 * NCHMAX + 2;
+    int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
+    int32_t lw, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score, int32_t* __restrict__ out_end,
+    int4* __restrict__ side, int32_t* __restrict__ side_cnt, int32_t cap, uint32_t* __restrict__ err_flag) {
+    constexpr int P = 2;
+    constexpr int SROW = (W * P + 3) & ~3;
+    constexpr int TROW = ((W + 1) * P + 3) & ~3;
     const int lane = threadIdx.x & 63;
-    const int64_t waves_per_block = blockDim.x >> 6;
-    const int64_t wave0 = (int64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
-    const int64_t n_waves = (int64_t)gridDim.x * waves_per_block;
-    const int64_t n_tiles = (n_pairs + tile - 1) / tile;
-    for (int64_t t = wave0; t < n_tiles; t += n_waves) {
-        const int64_t base = t * tile;
-        const int64_t p = base + lane;
-        const bool mine = (lane < tile) && (p < n_pairs);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int64_t n_tiles = (n_pairs + 63) >> 6;
+    int4* region = side + wave * cap;
+    int32_t n_side = 0;
+    for (int64_t tile = wave; tile < n_tiles; tile += n_waves) {
+        const int64_t p = tile * 64 + lane;
+        const bool mine = p < n_pairs;
         int32_t a = mine ? a_idx[p] : 0;
         int32_t b = mine ? b_idx[p] : 0;
-        bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
+        const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
         if (!ok) { a = 0; b = 0; }
-        int32_t na = len[a], nb = len[b];
-        ok = ok && na <= 32 * WMAX && nb <= 32 * WMAX;
+        const bool uni = ok && len[a] == lw && len[b] == lw;
         if (mine && !ok) atomicOr(err_flag, 1u);
-        if (!ok) { na = 0; nb = 0; }
-        int32_t res_s = ok ? 0 : -1, res_e = ok ? 0 : -1;
-        const int64_t rem = n_pairs - base;
-        const int cnt = rem < tile ? (int)rem : tile;
-        for (int i = 0; i < cnt; ++i) {
-            const int32_t A = __builtin_amdgcn_readlane(a, i);
-            const int32_t B = __builtin_amdgcn_readlane(b, i);
-            const int32_t n = __builtin_amdgcn_readlane(na, i);
-            const int32_t m = __builtin_amdgcn_readlane(nb, i);
-            KeyT key = 0;
-            if (n > 0 && m > 0) {
-                const int wp = (n + 31) >> 5;
-                key = score_pair<P, WMAX, KeyT>(sfx + (int64_t)A * (WMAX * P), pfx + (int64_t)B * (ZS * P),
-                                                n, m, match, mismatch, lane, wp);
-            }
-            if (lane == i && ok) KeyOps<KeyT>::decode(key, res_s, res_e);
+        const bool push = mine && ok && !uni;
+        const uint64_t pm = __ballot(push);
+        if (push) region[n_side + __popcll(pm & ((1ull << lane) - 1ull))] = make_int4((int32_t)p, a, b, 0);
+        n_side += __popcll(pm);
+        uint32_t Sw[SROW], Tw[TROW];
+        load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
+        load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+        const auto best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match);
+        if (mine && (uni || !ok)) {
+            int32_t sc, en;
+            Key<KM>::decode(best, sc, en);
+            out_score[p] = ok ? sc : -1;
+            out_end[p] = ok ? en : -1;
         }
-        if (mine) {
-            out_score[p] = res_s;
-            out_end[p] = res_e;
+    }
+    if (lane == 0 && wave < n_waves) side_cnt[wave] = n_side;
+}
+
+// General kernel: any lengths <= 32W and P bit planes, per-lane masks.  A pair
+// is owned by RS = 2^rs_log2 lanes (lanes slot, slot + 64/RS, ...); lane group g
+// sweeps the bit shifts r = g, g + RS, ...  With `side` it scores the side-list
+// regions left by uniform_kernel (wavefront w handles regions w, w + n_waves, ...);
+// otherwise pairs 0..n_pairs-1 directly.
+template <int P, int W, int KM>
+__global__ __launch_bounds__(256) void general_kernel(
+    const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
+    int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
+    const int4* __restrict__ side, const int32_t* __restrict__ side_cnt, int32_t cap, int32_t n_regions,
+    int32_t rs_log2, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score,
+    int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    constexpr int SROW = (W * P + 3) & ~3;
+    constexpr int TROW = ((W + 1) * P + 3) & ~3;
+    const int lane = threadIdx.x & 63;
+    const int ppw = 64 >> rs_log2;
+    const int slot = lane & (ppw - 1);
+    const int r0 = lane >> (6 - rs_log2);
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    // work units: (region, chunk of ppw entries) for the side list, or tiles of ppw pairs
+    const int64_t n_units_direct = (n_pairs + ppw - 1) / ppw;
+    const int64_t n_outer = side ? (int64_t)n_regions : 1;
+    for (int64_t reg = side ? wave : 0; reg < n_outer; reg += side ? n_waves : 1) {
+        const int64_t count = side ? (int64_t)side_cnt[reg] : n_pairs;
+        const int64_t n_units = side ? (count + ppw - 1) / ppw : n_units_direct;
+        for (int64_t u = side ? 0 : wave; u < n_units; u += side ? 1 : n_waves) {
+            const int64_t idx = u * ppw + slot;
+            const bool mine = idx < count;
+            int64_t p = 0;
+            int32_t a = 0, b = 0;
+            if (mine) {
+                if (side) {
+                    const int4 e = side[reg * cap + idx];
+                    p = e.x; a = e.y; b = e.z;
+                } else {
+                    p = idx; a = a_idx[p]; b = b_idx[p];
+                }
+            }
+            bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
+            if (!ok) { a = 0; b = 0; }
+            int32_t n = len[a], m = len[b];
+            ok = ok && n <= 32 * W && m <= 32 * W;
+            if (mine && !ok && r0 == 0) atomicOr(err_flag, 1u);
+            if (!ok) { n = 0; m = 0; }
+            uint32_t Sw[SROW], Tw[TROW];
+            load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
+            load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+            uint32_t SV[W];  // valid bits of s' word k: positions >= 32W - n
+            const int pad = 32 * W - n;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                const int lo = pad - 32 * k;
+                SV[k] = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
+            }
+            const int jmax = wave_max_i32(m);
+            const auto best = sweep_shifts<P, W, KM, false>(Sw, Tw, SV, n, m, jmax, r0, rs_log2, match,
+                                                            mismatch - match);
+            const auto full = group_max(best, ppw);
+            if (mine && r0 == 0) {
+                int32_t sc, en;
+                Key<KM>::decode(full, sc, en);
+                out_score[p] = ok ? sc : -1;
+                out_end[p] = ok ? en : -1;
+            }
         }
     }
 }
@@ -425,59 +577,116 @@ extern "C" hipError_t ovl_launch_map_codes(const uint8_t* raw, const uint8_t* lu
 }
 
 extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const int64_t* off, const int32_t* len,
-                                      int32_t n_reads, int32_t wmax, int32_t zs, uint32_t* sfx, uint32_t* pfx,
-                                      hipStream_t stream) {
+                                      int32_t n_reads, int32_t w, int32_t srow, int32_t trow, uint32_t* sfx,
+                                      uint32_t* pfx, hipStream_t stream) {
     if (n_reads <= 0) return hipSuccess;
-    const int64_t total = (int64_t)n_reads * (wmax > zs ? wmax : zs);
+    const int64_t total = (int64_t)n_reads * w;
     int64_t blocks = (total + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     switch (planes) {
-        case 2: pack_planes_kernel<2><<<(unsigned)blocks, 256, 0, stream>>>(codes, off, len, n_reads, wmax, zs, sfx, pfx); break;
-        case 4: pack_planes_kernel<4><<<(unsigned)blocks, 256, 0, stream>>>(codes, off, len, n_reads, wmax, zs, sfx, pfx); break;
-        case 8: pack_planes_kernel<8><<<(unsigned)blocks, 256, 0, stream>>>(codes, off, len, n_reads, wmax, zs, sfx, pfx); break;
+        case 2: pack_planes_kernel<2><<<(unsigned)blocks, 256, 0, stream>>>(codes, off, len, n_reads, w, srow, trow, sfx, pfx); break;
+        case 4: pack_planes_kernel<4><<<(unsigned)blocks, 256, 0, stream>>>(codes, off, len, n_reads, w, srow, trow, sfx, pfx); break;
+        case 8: pack_planes_kernel<8><<<(unsigned)blocks, 256, 0, stream>>>(codes, off, len, n_reads, w, srow, trow, sfx, pfx); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-template <int P, int WMAX, typename KeyT>
-static void launch_ungapped_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    ungapped_kernel<P, WMAX, KeyT><<<blocks, 256, 0, stream>>>(
-        g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.tile, g.match, g.mismatch,
-        g.out_score, g.out_end, g.err_flag);
+template <int W, int KM>
+static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    uniform_kernel<W, KM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs,
+                                                      g.lw, g.match, g.mismatch, g.out_score, g.out_end, g.side,
+                                                      g.side_cnt, g.side_cap, g.err_flag);
 }
 
-template <int P, typename KeyT>
-static hipError_t launch_ungapped_p(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+template <int P, int W, int KM>
+static void launch_general_t(const OvlUngappedArgs& g, bool use_side, int rs_log2, unsigned blocks,
+                             hipStream_t stream) {
+    general_kernel<P, W, KM><<<blocks, 256, 0, stream>>>(
+        g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, use_side ? g.side : nullptr,
+        use_side ? g.side_cnt : nullptr, g.side_cap, g.side_regions, rs_log2, g.match, g.mismatch, g.out_score,
+        g.out_end, g.err_flag);
+}
+
+template <int KM>
+static bool dispatch_uniform(const OvlUngappedArgs& g, unsigned blocks, hipStream_t s) {
     switch (g.wmax) {
-        case 2: launch_ungapped_t<P, 2, KeyT>(g, blocks, stream); break;
-        case 4: launch_ungapped_t<P, 4, KeyT>(g, blocks, stream); break;
-        case 8: launch_ungapped_t<P, 8, KeyT>(g, blocks, stream); break;
-        default: return hipErrorInvalidValue;
+        case 1: launch_uniform_t<1, KM>(g, blocks, s); return true;
+        case 2: launch_uniform_t<2, KM>(g, blocks, s); return true;
+        case 3: launch_uniform_t<3, KM>(g, blocks, s); return true;
+        case 4: launch_uniform_t<4, KM>(g, blocks, s); return true;
+        case 5: launch_uniform_t<5, KM>(g, blocks, s); return true;
+        case 6: launch_uniform_t<6, KM>(g, blocks, s); return true;
+        case 7: launch_uniform_t<7, KM>(g, blocks, s); return true;
+        case 8: launch_uniform_t<8, KM>(g, blocks, s); return true;
     }
-    return hipGetLastError();
+    return false;
 }
 
+template <int P, int KM>
+static bool dispatch_general_w(const OvlUngappedArgs& g, bool use_side, int rs, unsigned blocks, hipStream_t s) {
+    switch (g.wmax) {
+        case 1: launch_general_t<P, 1, KM>(g, use_side, rs, blocks, s); return true;
+        case 2: launch_general_t<P, 2, KM>(g, use_side, rs, blocks, s); return true;
+        case 3: launch_general_t<P, 3, KM>(g, use_side, rs, blocks, s); return true;
+        case 4: launch_general_t<P, 4, KM>(g, use_side, rs, blocks, s); return true;
+        case 5: launch_general_t<P, 5, KM>(g, use_side, rs, blocks, s); return true;
+        case 6: launch_general_t<P, 6, KM>(g, use_side, rs, blocks, s); return true;
+        case 7: launch_general_t<P, 7, KM>(g, use_side, rs, blocks, s); return true;
+        case 8: launch_general_t<P, 8, KM>(g, use_side, rs, blocks, s); return true;
+    }
+    return false;
+}
+
+template <int KM>
+static bool dispatch_general(const OvlUngappedArgs& g, bool use_side, int rs, unsigned blocks, hipStream_t s) {
+    switch (g.planes) {
+        case 2: return dispatch_general_w<2, KM>(g, use_side, rs, blocks, s);
+        case 4: return dispatch_general_w<4, KM>(g, use_side, rs, blocks, s);
+        case 8: return dispatch_general_w<8, KM>(g, use_side, rs, blocks, s);
+    }
+    return false;
+}
+
+static unsigned grid_for(int64_t pairs, int rs_log2, int64_t max_blocks) {
+    const int64_t ppw = 64 >> rs_log2;
+    int64_t blocks = ((pairs + ppw - 1) / ppw + 3) / 4;  // 4 wavefronts per block
+    if (blocks > max_blocks) blocks = max_blocks;
+    if (blocks < 1) blocks = 1;
+    return (unsigned)blocks;
+}
+
+extern "C" int64_t ovl_uniform_side_layout(int64_t n_pairs, int64_t max_blocks, int32_t* regions, int32_t* cap) {
+    const unsigned blocks = grid_for(n_pairs, 0, max_blocks);
+    const int64_t waves = (int64_t)blocks * 4;
+    const int64_t tiles = (n_pairs + 63) / 64;
+    *regions = (int32_t)waves;
+    *cap = (int32_t)(((tiles + waves - 1) / waves) * 64);
+    return (int64_t)*regions * *cap;
+}
+
+// Uniform path (P = 2 and a uniform read length): uniform_kernel over all pairs,
+// then general_kernel over its side-list regions.  Otherwise general_kernel over all pairs.
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
-    const int64_t n_tiles = (g->n_pairs + g->tile - 1) / g->tile;
-    int64_t blocks = (n_tiles + 3) / 4;  // 4 waves per block
-    if (blocks > g->max_blocks) blocks = g->max_blocks;
-    const unsigned nb = (unsigned)blocks;
-    if (g->key64) {
-        switch (g->planes) {
-            case 2: return launch_ungapped_p<2, uint64_t>(*g, nb, stream);
-            case 4: return launch_ungapped_p<4, uint64_t>(*g, nb, stream);
-            case 8: return launch_ungapped_p<8, uint64_t>(*g, nb, stream);
-        }
+    bool ok;
+    if (g->lw > 0) {
+        const unsigned nb = grid_for(g->n_pairs, 0, g->max_blocks);
+        if ((int64_t)nb * 4 != g->side_regions) return hipErrorInvalidValue;  // layout mismatch
+        ok = g->key64 ? dispatch_uniform<1>(*g, nb, stream) : dispatch_uniform<0>(*g, nb, stream);
+        if (!ok) return hipErrorInvalidValue;
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        // one general wavefront per side region; 4 lanes per pair
+        const unsigned nb2 = (unsigned)((g->side_regions + 3) / 4);
+        ok = g->key64 ? dispatch_general<1>(*g, true, 2, nb2, stream) : dispatch_general<0>(*g, true, 2, nb2, stream);
     } else {
-        switch (g->planes) {
-            case 2: return launch_ungapped_p<2, uint32_t>(*g, nb, stream);
-            case 4: return launch_ungapped_p<4, uint32_t>(*g, nb, stream);
-            case 8: return launch_ungapped_p<8, uint32_t>(*g, nb, stream);
-        }
+        const unsigned nb = grid_for(g->n_pairs, g->rs_log2, g->max_blocks);
+        ok = g->key64 ? dispatch_general<1>(*g, false, g->rs_log2, nb, stream)
+                      : dispatch_general<0>(*g, false, g->rs_log2, nb, stream);
     }
-    return hipErrorInvalidValue;
+    if (!ok) return hipErrorInvalidValue;
+    return hipGetLastError();
 }
 
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {

@@ -140,6 +140,36 @@ class OverlapEngine:
         self.score_device(a.data_ptr(), b.data_ptr(), n, out_score.data_ptr(), out_end.data_ptr(),
                           match, mismatch, indel, band, stream=s.cuda_stream)
 
+    def launcher(self, a, b, out_score, out_end, match: int = 10, mismatch: int = -1,
+                 indel: int = INDEL_DEFAULT, band: int = -1, stream=None):
+        """Pre-bound scoring launch for repeated steps over the same device buffers.
+
+        Converts every argument to its ctypes form once, so each call costs one
+        foreign call (the launch itself) instead of per-call tensor checks.
+        The tensors must stay alive while the launcher is used.
+        """
+        import torch
+        for t in (a, b, out_score, out_end):
+            if t.dtype != torch.int32 or not t.is_cuda or not t.is_contiguous():
+                raise OvlError(-1, "launcher needs contiguous int32 device tensors")
+        n = a.numel()
+        if b.numel() != n or out_score.numel() < n or out_end.numel() < n:
+            raise OvlError(-1, "tensor sizes disagree")
+        s = stream if stream is not None else torch.cuda.current_stream(a.device)
+        fn = self._L.ovl_score_device
+        ctx = self._ctx
+        args = (ctx, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), ctypes.c_int64(n),
+                ctypes.c_int32(match), ctypes.c_int32(mismatch), ctypes.c_int64(indel), ctypes.c_int32(band),
+                ctypes.c_void_p(out_score.data_ptr()), ctypes.c_void_p(out_end.data_ptr()),
+                ctypes.c_void_p(s.cuda_stream or None))
+        check(self._L.ovl_plan(ctx, match, mismatch, indel, band, ctypes.byref(ctypes.c_int32())), ctx)
+
+        def launch() -> None:
+            rc = fn(*args)
+            if rc:
+                check(rc, ctx)
+        return launch
+
     def check_device_errors(self) -> None:
         check(self._L.ovl_check_device_errors(self._ctx), self._ctx)
 

@@ -91,7 +91,7 @@ int ovl_score_host(ovl_ctx* ctx, const int32_t* a_idx, const int32_t* b_idx, int
 
 /*
  * Score against the resident reads with DEVICE pointers, asynchronously on
- * `stream` (a hipStream_t; NULL = the context's stream).  Pairs with an index
+ * `stream` (a hipStream_t; NULL = the default stream, as in the HIP API).  Pairs with an index
  * outside [0, n_reads) get score = end = -1 and set a device error flag that
  * ovl_check_device_errors() reports.
  */

@@ -39,12 +39,24 @@ def _rand(rng, n, alphabet="ACGT"):
 # ----------------------------------------------------------------------------- golden vectors
 
 def test_golden_default_batch(engine, golden_default):
-    reads, a, b = _pairs_to_reads(golden_default["pairs"])
+    # reads <= 256 bases: bit-plane layout -> ungapped kernel
+    pairs = [p for p in golden_default["pairs"] if max(len(p["s"]), len(p["t"])) <= 256]
+    assert len(pairs) > 900
+    reads, a, b = _pairs_to_reads(pairs)
     engine.set_reads(reads)
     assert engine.plan() == "ungapped"
     sc, en = engine.score(a, b)
-    assert sc.tolist() == [p["score"] for p in golden_default["pairs"]]
-    assert en.tolist() == [p["end"] for p in golden_default["pairs"]]
+    assert sc.tolist() == [p["score"] for p in pairs]
+    assert en.tolist() == [p["end"] for p in pairs]
+    # every ungapped template tier (wmax 2 / 4 / 8): read sets capped at 64, 128, 256
+    for cap in (64, 128):
+        sub = [p for p in pairs if max(len(p["s"]), len(p["t"])) <= cap]
+        reads, a, b = _pairs_to_reads(sub)
+        engine.set_reads(reads)
+        assert engine.plan() == "ungapped"
+        sc, en = engine.score(a, b)
+        assert sc.tolist() == [p["score"] for p in sub]
+        assert en.tolist() == [p["end"] for p in sub]
 
 
 def test_golden_default_through_dp_kernel(engine, golden_default):
