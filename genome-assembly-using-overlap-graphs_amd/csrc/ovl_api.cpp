@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -38,6 +39,7 @@ struct ovl_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int32_t cu_count = 256;
+    int32_t split_override = -1;  // OVL_SPLIT env: force log2(lanes|wavefronts per pair), tuning only
     // resident reads
     int32_t n_reads = -1;
     int32_t lmax = 0;
@@ -48,7 +50,6 @@ struct ovl_ctx {
     DevBuf codes, off, len, sfx, pfx, lut;
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
-    DevBuf side, counters;  // side-list regions of non-uniform pairs + per-region counts
 };
 
 namespace {
@@ -146,7 +147,7 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s);
 
-// Kernels index pairs of one launch with int32 (side-list entries); split huge lists.
+// Kernels queue pair indices as int32 (LDS side ring); split huge lists.
 int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                  int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                  hipStream_t s) {
@@ -174,24 +175,21 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         g.n_pairs = n_pairs;
         // split a pair's 32 bit shifts over 1, 2 or 4 lanes until the grid has
         // enough wavefronts to fill every SIMD a few times
+        // lanes per pair of the general kernel: split a pair's bit shifts over 1, 2 or 4
+        // lanes until the grid has enough wavefronts; the uniform kernel keeps one
+        // wavefront per tile (measured: splitting its r range over 2 or 4 wavefronts
+        // does not shorten small lists and costs occupancy on large ones)
         int32_t rs_log2 = 0;
         const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
         while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
+        const bool uniform_path = c->planes == 2;
+        if (uniform_path) rs_log2 = 0;
+        if (c->split_override >= 0) rs_log2 = c->split_override;  // OVL_SPLIT tuning knob (0..2)
         g.rs_log2 = rs_log2;
-        // uniform-length fast path (2 bit planes): reads of length lmax; the rest go
-        // through the side list (capacity n_pairs)
+        // uniform-length fast path (2 bit planes): pairs of two reads of length lmax;
+        // uniform_kernel scores the other pairs through its LDS side ring
         g.lw = c->planes == 2 ? c->lmax : 0;
         g.max_blocks = (int64_t)c->cu_count * 8;
-        if (g.lw > 0) {
-            int32_t regions = 0, cap = 0;
-            const int64_t entries = ovl_uniform_side_layout(n_pairs, g.max_blocks, &regions, &cap);
-            HIPCHK(c, ensure(c->side, sizeof(int4) * (size_t)entries));
-            HIPCHK(c, ensure(c->counters, sizeof(int32_t) * (size_t)regions));
-            g.side = as<int4>(c->side);
-            g.side_cnt = as<int32_t>(c->counters);
-            g.side_cap = cap;
-            g.side_regions = regions;
-        }
         g.match = match;
         g.mismatch = mismatch;
         g.out_score = d_score;
@@ -263,6 +261,10 @@ OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
     HIPCHK(nullptr, hipSetDevice(device));
     ovl_ctx* c = new ovl_ctx();
     c->device = device;
+    if (const char* sp = getenv("OVL_SPLIT")) {
+        const int v = atoi(sp);
+        if (v >= 0 && v <= 2) c->split_override = v;
+    }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         c->cu_count = prop.multiProcessorCount;
@@ -283,7 +285,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->a, &c->b, &c->score, &c->end,
-                      &c->tb, &c->err_flag, &c->side, &c->counters})
+                      &c->tb, &c->err_flag})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

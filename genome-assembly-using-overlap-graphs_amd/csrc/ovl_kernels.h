@@ -20,11 +20,7 @@ struct OvlUngappedArgs {
     int32_t planes;      // 2, 4 or 8 bit planes per base
     int32_t wmax;        // W = 1..8 words of 32 bases (read length <= 32*W)
     int32_t key64;       // 64-bit (score, end) keys (else 32-bit folded keys)
-    int32_t lw;          // uniform read length for uniform_kernel (0: general kernel only)
-    int4* side;          // side-list regions {pair, a, b, 0}: side_regions x side_cap entries
-    int32_t* side_cnt;   // entries per region (written by uniform_kernel every call)
-    int32_t side_cap;
-    int32_t side_regions;
+    int32_t lw;          // dominant read length for uniform_kernel (0: general kernel only)
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
 };
 
@@ -53,6 +49,5 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
                                       int32_t n_reads, int32_t w, int32_t srow, int32_t trow, uint32_t* sfx,
                                       uint32_t* pfx, hipStream_t stream);
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream_t stream);
-// side-list geometry of the uniform path for n_pairs: regions (= wavefronts) and entries per region
-extern "C" int64_t ovl_uniform_side_layout(int64_t n_pairs, int64_t max_blocks, int32_t* regions, int32_t* cap);
+
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);

@@ -246,7 +246,8 @@ __device__ __forceinline__ typename Key<KM>::T sweep_shifts(const uint32_t* Sw, 
 // v_mad_i32_i24 and one v_max.
 template <int W, int KM>
 __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw, const uint32_t* Tw, int32_t lw,
-                                                             int32_t match, int32_t dms) {
+                                                             int32_t match, int32_t dms, uint32_t r_lo,
+                                                             uint32_t r_hi) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int TW = W + 1;
@@ -301,7 +302,7 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
         }
     };
     // r = 0: j = 32q (q >= 1); block W only when lw == 32W
-    {
+    if (r_lo == 0) {
         T rm0 = 0;
         if (rcut == 32) {
             body(0u, 0u, rm0, std::integral_constant<int, W + 1>{});
@@ -309,15 +310,16 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
             body(0u, 0u, rm0, std::integral_constant<int, W>{});
         }
     }
-    T rm = mq;
-    uint32_t r = 1;
+    uint32_t r = r_lo > 1 ? r_lo : 1;
+    T rm = (T)r * mq;
     const uint32_t rc = (uint32_t)(rcut < 31 ? rcut : 31);
-    for (; r <= rc; ++r) {  // blocks 0..W-1
+    const uint32_t ra = rc < r_hi - 1 ? rc : r_hi - 1;
+    for (; r <= ra; ++r) {  // blocks 0..W-1
         const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> (r - 1));
         body(r, vt, rm, std::integral_constant<int, W>{});
         rm += mq;
     }
-    for (; r < 32; ++r) {  // blocks 0..W-2
+    for (; r < r_hi; ++r) {  // blocks 0..W-2
         const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> (r - 1));
         body(r, vt, rm, std::integral_constant<int, W - 1>{});
         rm += mq;
@@ -331,122 +333,159 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     return out;
 }
 
+// One general-path unit: up to 64/RS pairs, RS = 2^rs_log2 lanes per pair (lanes
+// slot, slot + 64/RS, ...; lane group g sweeps r = g, g + RS, ...), any lengths
+// <= 32W, per-lane masks.  Writes (score, end), or (-1, -1) for a bad index.
+template <int P, int W, int KM>
+__device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, int32_t b,
+                                             const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx,
+                                             const int32_t* __restrict__ len, int32_t n_reads, int r0,
+                                             int rs_log2, int32_t match, int32_t mismatch,
+                                             int32_t* __restrict__ out_score, int32_t* __restrict__ out_end,
+                                             uint32_t* __restrict__ err_flag) {
+    constexpr int SROW = (W * P + 3) & ~3;
+    constexpr int TROW = ((W + 1) * P + 3) & ~3;
+    bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
+    if (!ok) { a = 0; b = 0; }
+    int32_t n = len[a], m = len[b];
+    ok = ok && n <= 32 * W && m <= 32 * W;
+    if (mine && !ok && r0 == 0) atomicOr(err_flag, 1u);
+    if (!ok) { n = 0; m = 0; }
+    uint32_t Sw[SROW], Tw[TROW];
+    load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
+    load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+    uint32_t SV[W];  // valid bits of s' word k: positions >= 32W - n
+    const int pad = 32 * W - n;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const int lo = pad - 32 * k;
+        SV[k] = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
+    }
+    const int jmax = wave_max_i32(m);
+    const auto best = sweep_shifts<P, W, KM, false>(Sw, Tw, SV, n, m, jmax, r0, rs_log2, match, mismatch - match);
+    const auto full = group_max(best, 64 >> rs_log2);
+    if (mine && r0 == 0) {
+        int32_t sc, en;
+        Key<KM>::decode(full, sc, en);
+        out_score[p] = ok ? sc : -1;
+        out_end[p] = ok ? en : -1;
+    }
+}
+
 // Uniform-pair kernel (P = 2 bit planes, reads of one length lw = lmax, the
 // common case of simulated reads).  One lane per pair, so every lane of a
-// wavefront sweeps the same bit shift r (scalar).  Pairs that are not
-// (lw, lw) -- e.g. reads truncated at the genome end (generateErrorFreeReads.py
-// :45-46) -- are written to this wavefront's own region of the side list
-// (`cap` entries per wavefront, count in side_cnt[wave]); general_kernel scores
-// them next.  No atomics: the regions are disjoint and every count is rewritten
-// by every call.
-template <int W, int KM>
+// wavefront sweeps the same bit shift r (scalar).  With S = 2^split wavefronts
+// per tile (small candidate lists), wavefront `part` of a tile group sweeps
+// r in [32 part / S, 32 (part+1) / S) and the S partial keys meet in LDS.
+// Pairs that are not (lw, lw) -- e.g. reads truncated at the genome end
+// (generateErrorFreeReads.py:45-46) -- are queued by the part-0 wavefront in its
+// LDS ring and scored 16 at a time by the general path (4 lanes per pair)
+// whenever 16 are waiting, and once more at the end.
+template <int W, int KM, bool SPLIT>
 __global__ __launch_bounds__(256) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
-    int32_t lw, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score, int32_t* __restrict__ out_end,
-    int4* __restrict__ side, int32_t* __restrict__ side_cnt, int32_t cap, uint32_t* __restrict__ err_flag) {
+    int32_t lw, int32_t split, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score,
+    int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    if (!SPLIT) split = 0;
+    using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = ((W + 1) * P + 3) & ~3;
+    constexpr int RING = 128;                      // >= 15 left over + 64 from one tile
+    __shared__ int4 ring_all[4][RING];             // 8 KiB per block of 4 wavefronts
+    __shared__ T keys[SPLIT ? 4 : 1][64];
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    const int wib = threadIdx.x >> 6;              // wavefront in block
+    const int S = 1 << split;
+    const int part = wib & (S - 1);
+    const int grp = wib >> split;
+    const int G = 4 >> split;                      // tile groups per block
+    const uint32_t r_lo = (uint32_t)((32 * part) >> split);
+    const uint32_t r_hi = (uint32_t)((32 * (part + 1)) >> split);
+    int4* ring = ring_all[wib];
     const int64_t n_tiles = (n_pairs + 63) >> 6;
-    int4* region = side + wave * cap;
-    int32_t n_side = 0;
-    for (int64_t tile = wave; tile < n_tiles; tile += n_waves) {
+    int head = 0, tail = 0;                        // wave-uniform ring cursors
+    auto drain = [&](int count) {                  // score ring[head .. head + count), count <= 16
+        const int slot = lane & 15;
+        const bool mine = slot < count;
+        int4 e = make_int4(0, 0, 0, 0);
+        if (mine) e = ring[(head + slot) & (RING - 1)];
+        general_unit<P, W, KM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> 4, 2, match, mismatch,
+                               out_score, out_end, err_flag);
+        head += count;
+    };
+    for (int64_t base = (int64_t)blockIdx.x * G; base < n_tiles; base += (int64_t)gridDim.x * G) {
+        const int64_t tile = base + grp;
         const int64_t p = tile * 64 + lane;
-        const bool mine = p < n_pairs;
+        const bool mine = tile < n_tiles && p < n_pairs;
         int32_t a = mine ? a_idx[p] : 0;
         int32_t b = mine ? b_idx[p] : 0;
         const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
         if (!ok) { a = 0; b = 0; }
         const bool uni = ok && len[a] == lw && len[b] == lw;
-        if (mine && !ok) atomicOr(err_flag, 1u);
-        const bool push = mine && ok && !uni;
-        const uint64_t pm = __ballot(push);
-        if (push) region[n_side + __popcll(pm & ((1ull << lane) - 1ull))] = make_int4((int32_t)p, a, b, 0);
-        n_side += __popcll(pm);
+        if (part == 0) {
+            if (mine && !ok) atomicOr(err_flag, 1u);
+            const bool push = mine && ok && !uni;
+            const uint64_t pm = __ballot(push);
+            if (push)
+                ring[(tail + __popcll(pm & ((1ull << lane) - 1ull))) & (RING - 1)] = make_int4((int32_t)p, a, b, 0);
+            tail += __popcll(pm);
+        }
         uint32_t Sw[SROW], Tw[TROW];
         load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
         load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
-        const auto best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match);
-        if (mine && (uni || !ok)) {
+        T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, r_lo, r_hi);
+        if (SPLIT && S > 1) {
+            keys[wib][lane] = best;
+            __syncthreads();
+            if (part == 0) {
+                for (int k = 1; k < S; ++k) {
+                    const T o = keys[wib + k][lane];
+                    best = o > best ? o : best;
+                }
+            }
+            __syncthreads();
+        }
+        if (part == 0 && mine && (uni || !ok)) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
             out_score[p] = ok ? sc : -1;
             out_end[p] = ok ? en : -1;
         }
+        if (part == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            while (tail - head >= 16) drain(16);
+        }
     }
-    if (lane == 0 && wave < n_waves) side_cnt[wave] = n_side;
+    if (part == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (tail > head) drain(tail - head);
+    }
 }
 
-// General kernel: any lengths <= 32W and P bit planes, per-lane masks.  A pair
-// is owned by RS = 2^rs_log2 lanes (lanes slot, slot + 64/RS, ...); lane group g
-// sweeps the bit shifts r = g, g + RS, ...  With `side` it scores the side-list
-// regions left by uniform_kernel (wavefront w handles regions w, w + n_waves, ...);
-// otherwise pairs 0..n_pairs-1 directly.
+// General kernel: any lengths <= 32W and P bit planes (used when the read set
+// is not 2-plane-encodable or has no single dominant length), RS lanes per pair.
 template <int P, int W, int KM>
 __global__ __launch_bounds__(256) void general_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
-    const int4* __restrict__ side, const int32_t* __restrict__ side_cnt, int32_t cap, int32_t n_regions,
     int32_t rs_log2, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score,
     int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
-    constexpr int SROW = (W * P + 3) & ~3;
-    constexpr int TROW = ((W + 1) * P + 3) & ~3;
     const int lane = threadIdx.x & 63;
     const int ppw = 64 >> rs_log2;
     const int slot = lane & (ppw - 1);
     const int r0 = lane >> (6 - rs_log2);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    // work units: (region, chunk of ppw entries) for the side list, or tiles of ppw pairs
-    const int64_t n_units_direct = (n_pairs + ppw - 1) / ppw;
-    const int64_t n_outer = side ? (int64_t)n_regions : 1;
-    for (int64_t reg = side ? wave : 0; reg < n_outer; reg += side ? n_waves : 1) {
-        const int64_t count = side ? (int64_t)side_cnt[reg] : n_pairs;
-        const int64_t n_units = side ? (count + ppw - 1) / ppw : n_units_direct;
-        for (int64_t u = side ? 0 : wave; u < n_units; u += side ? 1 : n_waves) {
-            const int64_t idx = u * ppw + slot;
-            const bool mine = idx < count;
-            int64_t p = 0;
-            int32_t a = 0, b = 0;
-            if (mine) {
-                if (side) {
-                    const int4 e = side[reg * cap + idx];
-                    p = e.x; a = e.y; b = e.z;
-                } else {
-                    p = idx; a = a_idx[p]; b = b_idx[p];
-                }
-            }
-            bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
-            if (!ok) { a = 0; b = 0; }
-            int32_t n = len[a], m = len[b];
-            ok = ok && n <= 32 * W && m <= 32 * W;
-            if (mine && !ok && r0 == 0) atomicOr(err_flag, 1u);
-            if (!ok) { n = 0; m = 0; }
-            uint32_t Sw[SROW], Tw[TROW];
-            load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
-            load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
-            uint32_t SV[W];  // valid bits of s' word k: positions >= 32W - n
-            const int pad = 32 * W - n;
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-                const int lo = pad - 32 * k;
-                SV[k] = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
-            }
-            const int jmax = wave_max_i32(m);
-            const auto best = sweep_shifts<P, W, KM, false>(Sw, Tw, SV, n, m, jmax, r0, rs_log2, match,
-                                                            mismatch - match);
-            const auto full = group_max(best, ppw);
-            if (mine && r0 == 0) {
-                int32_t sc, en;
-                Key<KM>::decode(full, sc, en);
-                out_score[p] = ok ? sc : -1;
-                out_end[p] = ok ? en : -1;
-            }
-        }
+    const int64_t n_units = (n_pairs + ppw - 1) / ppw;
+    for (int64_t u = wave; u < n_units; u += n_waves) {
+        const int64_t p = u * ppw + slot;
+        const bool mine = p < n_pairs;
+        const int32_t a = mine ? a_idx[p] : 0;
+        const int32_t b = mine ? b_idx[p] : 0;
+        general_unit<P, W, KM>(mine, p, a, b, sfx, pfx, len, n_reads, r0, rs_log2, match, mismatch, out_score,
+                               out_end, err_flag);
     }
 }
 
@@ -594,18 +633,21 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
 
 template <int W, int KM>
 static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    uniform_kernel<W, KM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs,
-                                                      g.lw, g.match, g.mismatch, g.out_score, g.out_end, g.side,
-                                                      g.side_cnt, g.side_cap, g.err_flag);
+    if (g.rs_log2 > 0)
+        uniform_kernel<W, KM, true><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
+                                                                g.n_pairs, g.lw, g.rs_log2, g.match, g.mismatch,
+                                                                g.out_score, g.out_end, g.err_flag);
+    else
+        uniform_kernel<W, KM, false><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
+                                                                 g.n_pairs, g.lw, 0, g.match, g.mismatch,
+                                                                 g.out_score, g.out_end, g.err_flag);
 }
 
 template <int P, int W, int KM>
-static void launch_general_t(const OvlUngappedArgs& g, bool use_side, int rs_log2, unsigned blocks,
-                             hipStream_t stream) {
-    general_kernel<P, W, KM><<<blocks, 256, 0, stream>>>(
-        g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, use_side ? g.side : nullptr,
-        use_side ? g.side_cnt : nullptr, g.side_cap, g.side_regions, rs_log2, g.match, g.mismatch, g.out_score,
-        g.out_end, g.err_flag);
+static void launch_general_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    general_kernel<P, W, KM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
+                                                         g.n_pairs, g.rs_log2, g.match, g.mismatch, g.out_score,
+                                                         g.out_end, g.err_flag);
 }
 
 template <int KM>
@@ -624,26 +666,26 @@ static bool dispatch_uniform(const OvlUngappedArgs& g, unsigned blocks, hipStrea
 }
 
 template <int P, int KM>
-static bool dispatch_general_w(const OvlUngappedArgs& g, bool use_side, int rs, unsigned blocks, hipStream_t s) {
+static bool dispatch_general_w(const OvlUngappedArgs& g, unsigned blocks, hipStream_t s) {
     switch (g.wmax) {
-        case 1: launch_general_t<P, 1, KM>(g, use_side, rs, blocks, s); return true;
-        case 2: launch_general_t<P, 2, KM>(g, use_side, rs, blocks, s); return true;
-        case 3: launch_general_t<P, 3, KM>(g, use_side, rs, blocks, s); return true;
-        case 4: launch_general_t<P, 4, KM>(g, use_side, rs, blocks, s); return true;
-        case 5: launch_general_t<P, 5, KM>(g, use_side, rs, blocks, s); return true;
-        case 6: launch_general_t<P, 6, KM>(g, use_side, rs, blocks, s); return true;
-        case 7: launch_general_t<P, 7, KM>(g, use_side, rs, blocks, s); return true;
-        case 8: launch_general_t<P, 8, KM>(g, use_side, rs, blocks, s); return true;
+        case 1: launch_general_t<P, 1, KM>(g, blocks, s); return true;
+        case 2: launch_general_t<P, 2, KM>(g, blocks, s); return true;
+        case 3: launch_general_t<P, 3, KM>(g, blocks, s); return true;
+        case 4: launch_general_t<P, 4, KM>(g, blocks, s); return true;
+        case 5: launch_general_t<P, 5, KM>(g, blocks, s); return true;
+        case 6: launch_general_t<P, 6, KM>(g, blocks, s); return true;
+        case 7: launch_general_t<P, 7, KM>(g, blocks, s); return true;
+        case 8: launch_general_t<P, 8, KM>(g, blocks, s); return true;
     }
     return false;
 }
 
 template <int KM>
-static bool dispatch_general(const OvlUngappedArgs& g, bool use_side, int rs, unsigned blocks, hipStream_t s) {
+static bool dispatch_general(const OvlUngappedArgs& g, unsigned blocks, hipStream_t s) {
     switch (g.planes) {
-        case 2: return dispatch_general_w<2, KM>(g, use_side, rs, blocks, s);
-        case 4: return dispatch_general_w<4, KM>(g, use_side, rs, blocks, s);
-        case 8: return dispatch_general_w<8, KM>(g, use_side, rs, blocks, s);
+        case 2: return dispatch_general_w<2, KM>(g, blocks, s);
+        case 4: return dispatch_general_w<4, KM>(g, blocks, s);
+        case 8: return dispatch_general_w<8, KM>(g, blocks, s);
     }
     return false;
 }
@@ -656,34 +698,18 @@ static unsigned grid_for(int64_t pairs, int rs_log2, int64_t max_blocks) {
     return (unsigned)blocks;
 }
 
-extern "C" int64_t ovl_uniform_side_layout(int64_t n_pairs, int64_t max_blocks, int32_t* regions, int32_t* cap) {
-    const unsigned blocks = grid_for(n_pairs, 0, max_blocks);
-    const int64_t waves = (int64_t)blocks * 4;
-    const int64_t tiles = (n_pairs + 63) / 64;
-    *regions = (int32_t)waves;
-    *cap = (int32_t)(((tiles + waves - 1) / waves) * 64);
-    return (int64_t)*regions * *cap;
-}
-
-// Uniform path (P = 2 and a uniform read length): uniform_kernel over all pairs,
-// then general_kernel over its side-list regions.  Otherwise general_kernel over all pairs.
+// Uniform path (P = 2 and a dominant read length lw): uniform_kernel, which also
+// scores the other pairs through its LDS side ring.  Otherwise general_kernel.
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->lw > 0) {
-        const unsigned nb = grid_for(g->n_pairs, 0, g->max_blocks);
-        if ((int64_t)nb * 4 != g->side_regions) return hipErrorInvalidValue;  // layout mismatch
+        // rs_log2 here = log2 of wavefronts per tile (split of the r range)
+        const unsigned nb = grid_for(g->n_pairs << g->rs_log2, 0, g->max_blocks);
         ok = g->key64 ? dispatch_uniform<1>(*g, nb, stream) : dispatch_uniform<0>(*g, nb, stream);
-        if (!ok) return hipErrorInvalidValue;
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        // one general wavefront per side region; 4 lanes per pair
-        const unsigned nb2 = (unsigned)((g->side_regions + 3) / 4);
-        ok = g->key64 ? dispatch_general<1>(*g, true, 2, nb2, stream) : dispatch_general<0>(*g, true, 2, nb2, stream);
     } else {
         const unsigned nb = grid_for(g->n_pairs, g->rs_log2, g->max_blocks);
-        ok = g->key64 ? dispatch_general<1>(*g, false, g->rs_log2, nb, stream)
-                      : dispatch_general<0>(*g, false, g->rs_log2, nb, stream);
+        ok = g->key64 ? dispatch_general<1>(*g, nb, stream) : dispatch_general<0>(*g, nb, stream);
     }
     if (!ok) return hipErrorInvalidValue;
     return hipGetLastError();
