@@ -167,15 +167,22 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible devices (flow rehearsal on a 1-GPU box) share them
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = os.environ.get("OVL_BENCH_BACKEND", "nccl")  # nccl = RCCL on ROCm; gloo only for rehearsal
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     w = Workload(args.config, seed=rank, dev=dev)
     elapsed, kernel_ms = timed_steps(w, args.steps, args.warmup, dev, world)
 
-    stats = torch.tensor([elapsed, kernel_ms, float(w.n_pairs)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, kernel_ms, float(w.n_pairs)], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
