@@ -47,7 +47,7 @@ struct ovl_ctx {
     int32_t wmax = 0;  // 0: no bit-plane layout (reads longer than kFastMaxLen)
     int32_t srow = 0;  // sfx row stride (words)
     int32_t trow = 0;  // pfx row stride (words)
-    DevBuf codes, off, len, sfx, pfx, lut;
+    DevBuf codes, off, len, sfx, pfx, lut, full;  // full: bit r set iff len[r] == lmax
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
 };
@@ -189,6 +189,7 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         // uniform-length fast path (2 bit planes): pairs of two reads of length lmax;
         // uniform_kernel scores the other pairs through its LDS side ring
         g.lw = c->planes == 2 ? c->lmax : 0;
+        g.full = as<uint32_t>(c->full);
         g.max_blocks = (int64_t)c->cu_count * 8;
         g.match = match;
         g.mismatch = mismatch;
@@ -284,7 +285,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     if (!c) return OVL_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->a, &c->b, &c->score, &c->end,
+    for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->full, &c->a, &c->b, &c->score, &c->end,
                       &c->tb, &c->err_flag})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -311,6 +312,9 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
         lmax = std::max(lmax, (int32_t)l);
     }
     const int64_t total = n_reads > 0 ? off[n_reads] : 0;
+    std::vector<uint32_t> full(((size_t)std::max(n_reads, 1) + 31) / 32, 0u);
+    for (int32_t r = 0; r < n_reads; ++r)
+        if (len[r] == lmax) full[(size_t)r >> 5] |= 1u << (r & 31);
     if (total > 0 && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
     // alphabet: dense codes in byte order (equality-preserving)
     bool present[256] = {false};
@@ -325,7 +329,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     int32_t wmax = 0;
     if (lmax <= kFastMaxLen) wmax = std::max(1, (lmax + 31) / 32);
     const int32_t srow = wmax ? ((wmax * planes + 3) & ~3) : 0;
-    const int32_t trow = wmax ? (((wmax + 1) * planes + 3) & ~3) : 0;
+    const int32_t trow = wmax ? ((wmax * planes + 3) & ~3) : 0;
 
     c->n_reads = -1;  // invalid until fully built
     DevBuf raw;
@@ -342,6 +346,10 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
         e = hipMemcpyAsync(c->len.p, len.data(), sizeof(int32_t) * len.size(), hipMemcpyHostToDevice, c->stream);
         if (e != hipSuccess) break;
         e = hipMemcpyAsync(c->lut.p, lut, 256, hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) break;
+        e = ensure(c->full, sizeof(uint32_t) * full.size());
+        if (e != hipSuccess) break;
+        e = hipMemcpyAsync(c->full.p, full.data(), sizeof(uint32_t) * full.size(), hipMemcpyHostToDevice, c->stream);
         if (e != hipSuccess) break;
         if (total > 0) {
             e = hipMemcpyAsync(raw.p, src, (size_t)total, hipMemcpyHostToDevice, c->stream);

@@ -21,6 +21,7 @@ struct OvlUngappedArgs {
     int32_t wmax;        // W = 1..8 words of 32 bases (read length <= 32*W)
     int32_t key64;       // 64-bit (score, end) keys (else 32-bit folded keys)
     int32_t lw;          // dominant read length for uniform_kernel (0: general kernel only)
+    const uint32_t* full; // bit r set iff len[r] == lw
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
 };
 

@@ -23,7 +23,7 @@
 // Layouts (per read, W = ceil(lmax/32) words of 32 bases, P planes interleaved per
 // word, rows padded to 16 bytes):
 //   sfx[r][k*P + p], k < W:       read right-aligned: base i at position 32W - n + i
-//   pfx[r][x*P + p], x < W + 1:   read left-aligned: base i at position i; word W is zero
+//   pfx[r][x*P + p], x < W:       read left-aligned: base i at position i (word W is implicitly zero)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -194,7 +194,7 @@ __device__ __forceinline__ typename Key<KM>::T sweep_shifts(const uint32_t* Sw, 
         for (int i = 0; i < TW; ++i) {
 #pragma unroll
             for (int c = 0; c < P; ++c) {
-                const uint32_t hi = Tw[i * P + c];
+                const uint32_t hi = i < W ? Tw[i * P + c] : 0u;  // t word W is zero (m <= 32W)
                 const uint32_t lo = i ? Tw[(i - 1) * P + c] : 0u;
                 U[i][c] = alignbit(hi, lo, r);
             }
@@ -276,7 +276,7 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
             if (i < NQ || (NQ > W && i <= W)) {
 #pragma unroll
                 for (int c = 0; c < P; ++c) {
-                    const uint32_t hi = Tw[i * P + c];
+                    const uint32_t hi = i < W ? Tw[i * P + c] : 0u;  // t word W is zero (m <= 32W)
                     const uint32_t lo = i ? Tw[(i - 1) * P + c] : 0u;
                     U[i][c] = alignbit(hi, lo, r);
                 }
@@ -340,11 +340,11 @@ template <int P, int W, int KM>
 __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, int32_t b,
                                              const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx,
                                              const int32_t* __restrict__ len, int32_t n_reads, int r0,
-                                             int rs_log2, int32_t match, int32_t mismatch,
+                                             int rs_log2, int32_t jbound, int32_t match, int32_t mismatch,
                                              int32_t* __restrict__ out_score, int32_t* __restrict__ out_end,
                                              uint32_t* __restrict__ err_flag) {
     constexpr int SROW = (W * P + 3) & ~3;
-    constexpr int TROW = ((W + 1) * P + 3) & ~3;
+    constexpr int TROW = (W * P + 3) & ~3;
     bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
     if (!ok) { a = 0; b = 0; }
     int32_t n = len[a], m = len[b];
@@ -361,7 +361,8 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
         const int lo = pad - 32 * k;
         SV[k] = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
     }
-    const int jmax = wave_max_i32(m);
+    // wave-uniform bound on end positions: the caller's (lmax) or the wave max of m
+    const int jmax = jbound > 0 ? jbound : wave_max_i32(m);
     const auto best = sweep_shifts<P, W, KM, false>(Sw, Tw, SV, n, m, jmax, r0, rs_log2, match, mismatch - match);
     const auto full = group_max(best, 64 >> rs_log2);
     if (mine && r0 == 0) {
@@ -385,13 +386,13 @@ template <int W, int KM, bool SPLIT>
 __global__ __launch_bounds__(256) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
-    int32_t lw, int32_t split, int32_t match, int32_t mismatch, int32_t* __restrict__ out_score,
-    int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    int32_t lw, const uint32_t* __restrict__ full, int32_t split, int32_t match, int32_t mismatch,
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
     if (!SPLIT) split = 0;
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
-    constexpr int TROW = ((W + 1) * P + 3) & ~3;
+    constexpr int TROW = (W * P + 3) & ~3;
     constexpr int RING = 128;                      // >= 15 left over + 64 from one tile
     __shared__ int4 ring_all[4][RING];             // 8 KiB per block of 4 wavefronts
     __shared__ T keys[SPLIT ? 4 : 1][64];
@@ -406,13 +407,17 @@ __global__ __launch_bounds__(256) void uniform_kernel(
     int4* ring = ring_all[wib];
     const int64_t n_tiles = (n_pairs + 63) >> 6;
     int head = 0, tail = 0;                        // wave-uniform ring cursors
-    auto drain = [&](int count) {                  // score ring[head .. head + count), count <= 16
-        const int slot = lane & 15;
+    // score ring[head .. head + count), count <= 16, with 64/count-ish lanes per pair:
+    // 4 lanes (16 pairs), 8 lanes (<= 8) or 16 lanes (<= 4) to shorten the serial r loop
+    auto drain = [&](int count) {
+        const int rs = count > 8 ? 2 : (count > 4 ? 3 : 4);   // log2(lanes per pair)
+        const int ppw = 64 >> rs;
+        const int slot = lane & (ppw - 1);
         const bool mine = slot < count;
         int4 e = make_int4(0, 0, 0, 0);
         if (mine) e = ring[(head + slot) & (RING - 1)];
-        general_unit<P, W, KM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> 4, 2, match, mismatch,
-                               out_score, out_end, err_flag);
+        general_unit<P, W, KM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
+                               mismatch, out_score, out_end, err_flag);
         head += count;
     };
     for (int64_t base = (int64_t)blockIdx.x * G; base < n_tiles; base += (int64_t)gridDim.x * G) {
@@ -423,7 +428,8 @@ __global__ __launch_bounds__(256) void uniform_kernel(
         int32_t b = mine ? b_idx[p] : 0;
         const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
         if (!ok) { a = 0; b = 0; }
-        const bool uni = ok && len[a] == lw && len[b] == lw;
+        // both reads of length lw? one bit per read (L1-resident bitmap) instead of two len gathers
+        const bool uni = ok && ((full[a >> 5] >> (a & 31)) & (full[b >> 5] >> (b & 31)) & 1u);
         if (part == 0) {
             if (mine && !ok) atomicOr(err_flag, 1u);
             const bool push = mine && ok && !uni;
@@ -435,7 +441,12 @@ __global__ __launch_bounds__(256) void uniform_kernel(
         uint32_t Sw[SROW], Tw[TROW];
         load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
         load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+#ifdef OVL_ABLATE_SWEEP  // diagnostic build only: keep the loads, skip the sweep
+        T best = (T)(Sw[0] ^ Tw[0] ^ Sw[SROW - 1] ^ Tw[TROW - 1]) & 0;
+        asm volatile("" ::"v"(Sw[0]), "v"(Tw[0]), "v"(Sw[SROW - 1]), "v"(Tw[TROW - 1]));
+#else
         T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, r_lo, r_hi);
+#endif
         if (SPLIT && S > 1) {
             keys[wib][lane] = best;
             __syncthreads();
@@ -453,15 +464,19 @@ __global__ __launch_bounds__(256) void uniform_kernel(
             out_score[p] = ok ? sc : -1;
             out_end[p] = ok ? en : -1;
         }
+#ifndef OVL_ABLATE_DRAIN  // diagnostic build only: side pairs left unscored
         if (part == 0) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             while (tail - head >= 16) drain(16);
         }
+#endif
     }
+#ifndef OVL_ABLATE_DRAIN
     if (part == 0) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (tail > head) drain(tail - head);
     }
+#endif
 }
 
 // General kernel: any lengths <= 32W and P bit planes (used when the read set
@@ -484,7 +499,7 @@ __global__ __launch_bounds__(256) void general_kernel(
         const bool mine = p < n_pairs;
         const int32_t a = mine ? a_idx[p] : 0;
         const int32_t b = mine ? b_idx[p] : 0;
-        general_unit<P, W, KM>(mine, p, a, b, sfx, pfx, len, n_reads, r0, rs_log2, match, mismatch, out_score,
+        general_unit<P, W, KM>(mine, p, a, b, sfx, pfx, len, n_reads, r0, rs_log2, 0, match, mismatch, out_score,
                                out_end, err_flag);
     }
 }
@@ -635,11 +650,11 @@ template <int W, int KM>
 static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
     if (g.rs_log2 > 0)
         uniform_kernel<W, KM, true><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
-                                                                g.n_pairs, g.lw, g.rs_log2, g.match, g.mismatch,
-                                                                g.out_score, g.out_end, g.err_flag);
+                                                                g.n_pairs, g.lw, g.full, g.rs_log2, g.match,
+                                                                g.mismatch, g.out_score, g.out_end, g.err_flag);
     else
         uniform_kernel<W, KM, false><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
-                                                                 g.n_pairs, g.lw, 0, g.match, g.mismatch,
+                                                                 g.n_pairs, g.lw, g.full, 0, g.match, g.mismatch,
                                                                  g.out_score, g.out_end, g.err_flag);
 }
 

@@ -130,7 +130,7 @@ def test_golden_graphs(engine, golden_graphs):
 
 # ----------------------------------------------------------------------------- seeded vs oracle
 
-@pytest.mark.parametrize("lmax", [20, 64, 65, 100, 128, 129, 150, 200, 256])
+@pytest.mark.parametrize("lmax", [1, 5, 20, 31, 32, 33, 64, 65, 96, 100, 128, 129, 150, 160, 192, 200, 224, 255, 256])
 def test_random_lengths_vs_oracle(engine, oracle_mod, lmax):
     rng = random.Random(lmax)
     reads = [_rand(rng, rng.randint(1, lmax)) for _ in range(300)]
@@ -298,3 +298,64 @@ def test_full_config_vs_oracle(engine, oracle_mod, cfg):
     ds, de = oracle_mod.batch_dp(reads, a[:2000], b[:2000])
     np.testing.assert_array_equal(sc[:2000], ds)
     np.testing.assert_array_equal(en[:2000], de)
+
+
+@pytest.mark.parametrize("lw", [1, 7, 31, 32, 33, 63, 64, 95, 96, 97, 100, 127, 128, 150, 160, 192, 224, 250, 256])
+@pytest.mark.parametrize("trunc", [0.0, 0.03, 0.5])
+def test_uniform_length_sets_vs_oracle(engine, oracle_mod, lw, trunc):
+    """Read sets of one dominant length (the uniform kernel) with a fraction of truncated reads
+    (the side ring), over every W tier and both sides of the block cut r <= lw - 32(W-1)."""
+    rng = random.Random(lw * 1000 + int(trunc * 100))
+    reads = [_rand(rng, lw) if rng.random() >= trunc else _rand(rng, rng.randint(1, lw)) for _ in range(700)]
+    # related reads so that scores are large and ties frequent
+    base = _rand(rng, 3 * lw)
+    reads += [base[i:i + lw] for i in range(0, 2 * lw, max(1, lw // 7))]
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(9000)], dtype=np.int32)
+    b = np.array([rng.randrange(n) for _ in range(9000)], dtype=np.int32)
+    engine.set_reads(reads)
+    assert engine.plan() == "ungapped"
+    sc, en = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("params", [(1, -1), (3, -2), (127, -1), (10, -120), (2000, -3000)])
+def test_uniform_kernel_key_variants(engine, oracle_mod, params):
+    """Other match/mismatch values: folded 32-bit keys, and 64-bit keys when scores can reach 2^15."""
+    ma, mm = params
+    rng = random.Random(ma * 7 + mm)
+    reads = [_rand(rng, 100) for _ in range(300)] + [_rand(rng, rng.randint(1, 99)) for _ in range(20)]
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(4000)], dtype=np.int32)
+    b = np.array([rng.randrange(n) for _ in range(4000)], dtype=np.int32)
+    engine.set_reads(reads)
+    indel = -(2 ** 40)
+    assert engine.plan(ma, mm, indel) == "ungapped"
+    sc, en = engine.score(a, b, ma, mm, indel)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b, ma, mm, indel)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+def test_split_knob_equivalence(oracle_mod):
+    """OVL_SPLIT (r range over 2 / 4 wavefronts) must not change results."""
+    import os
+    from ovlgraph import OverlapEngine
+    rng = random.Random(42)
+    reads = [_rand(rng, 100) for _ in range(400)] + [_rand(rng, rng.randint(1, 99)) for _ in range(30)]
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(5000)], dtype=np.int32)
+    b = np.array([rng.randrange(n) for _ in range(5000)], dtype=np.int32)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    for split in ("0", "1", "2"):
+        os.environ["OVL_SPLIT"] = split
+        try:
+            with OverlapEngine(0) as eng:
+                eng.set_reads(reads)
+                sc, en = eng.score(a, b)
+        finally:
+            del os.environ["OVL_SPLIT"]
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
