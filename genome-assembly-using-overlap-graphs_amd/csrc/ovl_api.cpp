@@ -39,7 +39,7 @@ struct ovl_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int32_t cu_count = 256;
-    int32_t split_override = -1;  // OVL_SPLIT env: force log2(lanes|wavefronts per pair), tuning only
+    int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
     // resident reads
     int32_t n_reads = -1;
     int32_t lmax = 0;
@@ -129,7 +129,7 @@ int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, 
         const int64_t dms = (int64_t)mismatch - (int64_t)match;
         // (the uniform sweep compares keys without their block constant: |score| + 32*amax
         //  must stay below 2^15 as well)
-        p.key64 = !(amax * (2 * L + 32) < (1 << 15) && iabs64(dms) < 128);
+        p.key64 = !(amax * (2 * L + 32) < (1 << 15) && iabs64(dms) < 128 && iabs64(match) < 128);
     } else {
         if (c->lmax > kDpMaxLen)
             return fail(c, OVL_E_UNSUPPORTED, "gapped DP supports reads up to %d bases (longest is %d)", kDpMaxLen,
@@ -175,16 +175,14 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         g.n_pairs = n_pairs;
         // split a pair's 32 bit shifts over 1, 2 or 4 lanes until the grid has
         // enough wavefronts to fill every SIMD a few times
-        // lanes per pair of the general kernel: split a pair's bit shifts over 1, 2 or 4
-        // lanes until the grid has enough wavefronts; the uniform kernel keeps one
-        // wavefront per tile (measured: splitting its r range over 2 or 4 wavefronts
-        // does not shorten small lists and costs occupancy on large ones)
+        // general kernel: split a pair's bit shifts over 1, 2 or 4 lanes until the grid
+        // has enough wavefronts.  Uniform kernel: latency mode (two wavefronts per tile,
+        // side pairs beside the sweep) when there is about one tile per wavefront slot.
         int32_t rs_log2 = 0;
         const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
         while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
-        const bool uniform_path = c->planes == 2;
-        if (uniform_path) rs_log2 = 0;
-        if (c->split_override >= 0) rs_log2 = c->split_override;  // OVL_SPLIT tuning knob (0..2)
+        if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * 8) ? 1 : 0;
+        if (c->split_override >= 0) rs_log2 = c->split_override;  // OVL_SPLIT tuning knob
         g.rs_log2 = rs_log2;
         // uniform-length fast path (2 bit planes): pairs of two reads of length lmax;
         // uniform_kernel scores the other pairs through its LDS side ring

@@ -33,6 +33,22 @@
 
 namespace ovl {
 
+#ifdef OVL_TRACE  // diagnostic build only (make trace): per-wavefront timestamps of the uniform kernel
+__device__ unsigned long long ovl_trace_buf[65536 * 8];
+#define OVL_TR_CLOCK(k, dep)                                                                           \
+    do {                                                                                               \
+        unsigned long long t_;                                                                         \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)"            \
+                     : "=s"(t_) : "v"(dep) : "memory");                                                \
+        if (lane == 0 && tr_id < 65536) ovl_trace_buf[tr_id * 8 + (k)] = t_;                            \
+    } while (0)
+#define OVL_TR_VAL(k, v) \
+    do { if (lane == 0 && tr_id < 65536) ovl_trace_buf[tr_id * 8 + (k)] = (unsigned long long)(v); } while (0)
+#else
+#define OVL_TR_CLOCK(k, dep) do {} while (0)
+#define OVL_TR_VAL(k, v) do {} while (0)
+#endif
+
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t r) {
     return __builtin_amdgcn_alignbit(hi, lo, r);
 }
@@ -219,6 +235,13 @@ __device__ __forceinline__ typename Key<KM>::T sweep_shifts(const uint32_t* Sw, 
             T key;
             if constexpr (UNI && KM == 0) {
                 key = Key<0>::make_folded(X, d2, kr + 32 * q * m2);
+            } else if constexpr (KM == 0) {
+                // key = L * (match << 16) + X * (dms << 16) - j with two v_mad_i32_i24
+                // (v_mul_lo_u32 is quarter rate); host guarantees |match|, |dms| < 128
+                const int32_t L = n < j ? n : j;
+                const int32_t m16 = (int32_t)((uint32_t)match << 16);
+                const int32_t xs = ((int32_t)X << 8) >> 8, ls = (L << 8) >> 8;
+                key = ls * ((m16 << 8) >> 8) + (xs * ((d2 << 8) >> 8) - j);
             } else {
                 const int32_t L = n < j ? n : j;
                 key = Key<KM>::make(match * L + dms * (int32_t)X, j);
@@ -336,6 +359,26 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
 // One general-path unit: up to 64/RS pairs, RS = 2^rs_log2 lanes per pair (lanes
 // slot, slot + 64/RS, ...; lane group g sweeps r = g, g + RS, ...), any lengths
 // <= 32W, per-lane masks.  Writes (score, end), or (-1, -1) for a bad index.
+// score one pair per group of 2^rs_log2 lanes from its rows already in registers
+// (n, m = lengths; ok = valid pair); returns the pair's best key on every lane of the group
+template <int P, int W, int KM>
+__device__ __forceinline__ typename Key<KM>::T general_core(bool ok, int32_t n, int32_t m, const uint32_t* Sw,
+                                                            const uint32_t* Tw, int r0, int rs_log2, int32_t jbound,
+                                                            int32_t match, int32_t mismatch) {
+    if (!ok) { n = 0; m = 0; }
+    uint32_t SV[W];  // valid bits of s' word k: positions >= 32W - n
+    const int pad = 32 * W - n;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const int lo = pad - 32 * k;
+        SV[k] = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
+    }
+    // wave-uniform bound on end positions: the caller's (lmax) or the wave max of m
+    const int jmax = jbound > 0 ? jbound : wave_max_i32(m);
+    const auto best = sweep_shifts<P, W, KM, false>(Sw, Tw, SV, n, m, jmax, r0, rs_log2, match, mismatch - match);
+    return group_max(best, 64 >> rs_log2);
+}
+
 template <int P, int W, int KM>
 __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, int32_t b,
                                              const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx,
@@ -350,21 +393,10 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
     int32_t n = len[a], m = len[b];
     ok = ok && n <= 32 * W && m <= 32 * W;
     if (mine && !ok && r0 == 0) atomicOr(err_flag, 1u);
-    if (!ok) { n = 0; m = 0; }
     uint32_t Sw[SROW], Tw[TROW];
     load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
     load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
-    uint32_t SV[W];  // valid bits of s' word k: positions >= 32W - n
-    const int pad = 32 * W - n;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-        const int lo = pad - 32 * k;
-        SV[k] = lo <= 0 ? 0xFFFFFFFFu : (lo >= 32 ? 0u : (0xFFFFFFFFu << lo));
-    }
-    // wave-uniform bound on end positions: the caller's (lmax) or the wave max of m
-    const int jmax = jbound > 0 ? jbound : wave_max_i32(m);
-    const auto best = sweep_shifts<P, W, KM, false>(Sw, Tw, SV, n, m, jmax, r0, rs_log2, match, mismatch - match);
-    const auto full = group_max(best, 64 >> rs_log2);
+    const auto full = general_core<P, W, KM>(ok, n, m, Sw, Tw, r0, rs_log2, jbound, match, mismatch);
     if (mine && r0 == 0) {
         int32_t sc, en;
         Key<KM>::decode(full, sc, en);
@@ -375,36 +407,42 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
 
 // Uniform-pair kernel (P = 2 bit planes, reads of one length lw = lmax, the
 // common case of simulated reads).  One lane per pair, so every lane of a
-// wavefront sweeps the same bit shift r (scalar).  With S = 2^split wavefronts
-// per tile (small candidate lists), wavefront `part` of a tile group sweeps
-// r in [32 part / S, 32 (part+1) / S) and the S partial keys meet in LDS.
-// Pairs that are not (lw, lw) -- e.g. reads truncated at the genome end
-// (generateErrorFreeReads.py:45-46) -- are queued by the part-0 wavefront in its
-// LDS ring and scored 16 at a time by the general path (4 lanes per pair)
-// whenever 16 are waiting, and once more at the end.
-template <int W, int KM, bool SPLIT>
-__global__ __launch_bounds__(256) void uniform_kernel(
+// wavefront sweeps the same bit shift r (scalar).  Pairs that are not (lw, lw)
+// -- e.g. reads truncated at the genome end (generateErrorFreeReads.py:45-46) --
+// are "side pairs", scored by the general path with 4, 8 or 16 lanes per pair:
+//  - throughput mode (LAT = false): one wavefront per tile; side pairs are queued
+//    as (p, a, b) in the wavefront's LDS ring and scored whenever 16 are waiting,
+//    and once at the end;
+//  - latency mode (LAT = true, about one tile per wavefront slot): two wavefronts
+//    per tile running concurrently -- role 0 sweeps the uniform pairs, role 1
+//    loads lengths and rows in the round trip after the indices, restages its
+//    side pairs through LDS into the 4/8/16-lane layout and scores them -- so the
+//    side work overlaps the sweep instead of trailing it.
+// waves per SIMD the kernel is compiled for (VGPR budget 512 / occupancy): the
+// most that fits without spilling
+#define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : 4))) \
+                                  : ((W) <= 4 ? 7 : ((W) <= 5 ? 6 : ((W) <= 6 ? 5 : 4))))
+template <int W, int KM, bool LAT>
+__global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
-    int32_t lw, const uint32_t* __restrict__ full, int32_t split, int32_t match, int32_t mismatch,
+    int32_t lw, const uint32_t* __restrict__ full, int32_t match, int32_t mismatch,
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
-    if (!SPLIT) split = 0;
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = (W * P + 3) & ~3;
     constexpr int RING = 128;                      // >= 15 left over + 64 from one tile
-    __shared__ int4 ring_all[4][RING];             // 8 KiB per block of 4 wavefronts
-    __shared__ T keys[SPLIT ? 4 : 1][64];
+    constexpr int ROWQ = (SROW + TROW) / 4;        // uint4 per staged side pair (latency mode)
+    __shared__ int4 ring_all[LAT ? 1 : 4][RING];   // throughput mode: 8 KiB per block
+    __shared__ int4 side_ent[LAT ? 2 : 1][64];     // latency mode: (p, -, n, m) per side pair
+    __shared__ uint4 side_rows[LAT ? 2 * 64 * ROWQ : 1];
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;              // wavefront in block
-    const int S = 1 << split;
-    const int part = wib & (S - 1);
-    const int grp = wib >> split;
-    const int G = 4 >> split;                      // tile groups per block
-    const uint32_t r_lo = (uint32_t)((32 * part) >> split);
-    const uint32_t r_hi = (uint32_t)((32 * (part + 1)) >> split);
-    int4* ring = ring_all[wib];
+    const int role = LAT ? (wib & 1) : 0;          // latency mode: 0 = sweep, 1 = side pairs
+    constexpr int G = LAT ? 2 : 4;                 // tiles per block per iteration
+    const int grp = LAT ? (wib >> 1) : wib;
+    int4* ring = ring_all[LAT ? 0 : wib];
     const int64_t n_tiles = (n_pairs + 63) >> 6;
     int head = 0, tail = 0;                        // wave-uniform ring cursors
     // score ring[head .. head + count), count <= 16, with 64/count-ish lanes per pair:
@@ -420,6 +458,16 @@ __global__ __launch_bounds__(256) void uniform_kernel(
                                mismatch, out_score, out_end, err_flag);
         head += count;
     };
+#ifdef OVL_TRACE
+    const int64_t tr_id = (int64_t)blockIdx.x * 4 + wib;
+    {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(hw), "=s"(xcc));
+        OVL_TR_VAL(5, hw);
+        OVL_TR_VAL(6, xcc | (role << 8));
+    }
+    OVL_TR_CLOCK(0, lane);
+#endif
     for (int64_t base = (int64_t)blockIdx.x * G; base < n_tiles; base += (int64_t)gridDim.x * G) {
         const int64_t tile = base + grp;
         const int64_t p = tile * 64 + lane;
@@ -428,51 +476,105 @@ __global__ __launch_bounds__(256) void uniform_kernel(
         int32_t b = mine ? b_idx[p] : 0;
         const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
         if (!ok) { a = 0; b = 0; }
+        if (LAT && role == 1) {
+            // lengths and rows in the round trip after the indices; side pairs
+            // restaged through LDS and scored 16 at a time
+            const int32_t n = len[a], m = len[b];
+            uint32_t Sw[SROW], Tw[TROW];
+            load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
+            load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+            OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
+            if (mine && !ok) {
+                atomicOr(err_flag, 1u);
+                out_score[p] = -1;
+                out_end[p] = -1;
+            }
+            const bool push = ok && !(n == lw && m == lw);
+            const uint64_t pm = __ballot(push);
+            int4* ent = side_ent[LAT ? grp : 0];
+            uint4* rows = side_rows + (LAT ? grp * 64 * ROWQ : 0);
+            if (push) {
+                const int s = __popcll(pm & ((1ull << lane) - 1ull));
+                ent[s] = make_int4((int32_t)p, 0, n, m);
+#pragma unroll
+                for (int k = 0; k < SROW / 4; ++k)
+                    rows[s * ROWQ + k] = make_uint4(Sw[4 * k], Sw[4 * k + 1], Sw[4 * k + 2], Sw[4 * k + 3]);
+#pragma unroll
+                for (int k = 0; k < TROW / 4; ++k)
+                    rows[s * ROWQ + SROW / 4 + k] = make_uint4(Tw[4 * k], Tw[4 * k + 1], Tw[4 * k + 2], Tw[4 * k + 3]);
+            }
+            const int cnt = __popcll(pm);
+#ifndef OVL_ABLATE_DRAIN  // diagnostic build only: side pairs left unscored
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (int h = 0; h < cnt; h += 16) {
+                const int count = cnt - h < 16 ? cnt - h : 16;
+                const int rs = count > 8 ? 2 : (count > 4 ? 3 : 4);
+                const int slot = lane & ((64 >> rs) - 1);
+                const bool own = slot < count;
+                const int s = own ? h + slot : 0;
+                const int4 en = ent[s];
+                uint32_t Sv[SROW], Tv[TROW];
+#pragma unroll
+                for (int k = 0; k < SROW / 4; ++k) {
+                    const uint4 v = rows[s * ROWQ + k];
+                    Sv[4 * k] = v.x; Sv[4 * k + 1] = v.y; Sv[4 * k + 2] = v.z; Sv[4 * k + 3] = v.w;
+                }
+#pragma unroll
+                for (int k = 0; k < TROW / 4; ++k) {
+                    const uint4 v = rows[s * ROWQ + SROW / 4 + k];
+                    Tv[4 * k] = v.x; Tv[4 * k + 1] = v.y; Tv[4 * k + 2] = v.z; Tv[4 * k + 3] = v.w;
+                }
+                const int r0 = lane >> (6 - rs);
+                const auto full = general_core<P, W, KM>(own, en.z, en.w, Sv, Tv, r0, rs, lw, match, mismatch);
+                if (own && r0 == 0) {
+                    int32_t sc, e2;
+                    Key<KM>::decode(full, sc, e2);
+                    out_score[en.x] = sc;
+                    out_end[en.x] = e2;
+                }
+            }
+#endif
+            OVL_TR_CLOCK(2, cnt);
+            OVL_TR_VAL(7, cnt);
+            continue;
+        }
+        uint32_t Sw[SROW], Tw[TROW];
+        load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
+        load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
         // both reads of length lw? one bit per read (L1-resident bitmap) instead of two len gathers
         const bool uni = ok && ((full[a >> 5] >> (a & 31)) & (full[b >> 5] >> (b & 31)) & 1u);
-        if (part == 0) {
+        OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
+        if constexpr (!LAT) {
             if (mine && !ok) atomicOr(err_flag, 1u);
-            const bool push = mine && ok && !uni;
+            const bool push = ok && !uni;
             const uint64_t pm = __ballot(push);
             if (push)
                 ring[(tail + __popcll(pm & ((1ull << lane) - 1ull))) & (RING - 1)] = make_int4((int32_t)p, a, b, 0);
             tail += __popcll(pm);
         }
-        uint32_t Sw[SROW], Tw[TROW];
-        load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
-        load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
 #ifdef OVL_ABLATE_SWEEP  // diagnostic build only: keep the loads, skip the sweep
         T best = (T)(Sw[0] ^ Tw[0] ^ Sw[SROW - 1] ^ Tw[TROW - 1]) & 0;
         asm volatile("" ::"v"(Sw[0]), "v"(Tw[0]), "v"(Sw[SROW - 1]), "v"(Tw[TROW - 1]));
 #else
-        T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, r_lo, r_hi);
+        T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, 0u, 32u);
 #endif
-        if (SPLIT && S > 1) {
-            keys[wib][lane] = best;
-            __syncthreads();
-            if (part == 0) {
-                for (int k = 1; k < S; ++k) {
-                    const T o = keys[wib + k][lane];
-                    best = o > best ? o : best;
-                }
-            }
-            __syncthreads();
-        }
-        if (part == 0 && mine && (uni || !ok)) {
+        OVL_TR_CLOCK(3, (uint32_t)best);
+        if (mine && (uni || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
             out_score[p] = ok ? sc : -1;
             out_end[p] = ok ? en : -1;
         }
-#ifndef OVL_ABLATE_DRAIN  // diagnostic build only: side pairs left unscored
-        if (part == 0) {
+        OVL_TR_CLOCK(4, (uint32_t)best);
+#ifndef OVL_ABLATE_DRAIN
+        if constexpr (!LAT) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             while (tail - head >= 16) drain(16);
         }
 #endif
     }
 #ifndef OVL_ABLATE_DRAIN
-    if (part == 0) {
+    if constexpr (!LAT) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (tail > head) drain(tail - head);
     }
@@ -648,13 +750,13 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
 
 template <int W, int KM>
 static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    if (g.rs_log2 > 0)
+    if (g.rs_log2 > 0)  // latency mode: two wavefronts per tile
         uniform_kernel<W, KM, true><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
-                                                                g.n_pairs, g.lw, g.full, g.rs_log2, g.match,
-                                                                g.mismatch, g.out_score, g.out_end, g.err_flag);
+                                                                g.n_pairs, g.lw, g.full, g.match, g.mismatch,
+                                                                g.out_score, g.out_end, g.err_flag);
     else
         uniform_kernel<W, KM, false><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
-                                                                 g.n_pairs, g.lw, g.full, 0, g.match, g.mismatch,
+                                                                 g.n_pairs, g.lw, g.full, g.match, g.mismatch,
                                                                  g.out_score, g.out_end, g.err_flag);
 }
 
@@ -719,8 +821,8 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->lw > 0) {
-        // rs_log2 here = log2 of wavefronts per tile (split of the r range)
-        const unsigned nb = grid_for(g->n_pairs << g->rs_log2, 0, g->max_blocks);
+        // rs_log2 > 0 here selects the latency mode
+        const unsigned nb = grid_for(g->n_pairs << (g->rs_log2 > 0 ? 1 : 0), 0, g->max_blocks);
         ok = g->key64 ? dispatch_uniform<1>(*g, nb, stream) : dispatch_uniform<0>(*g, nb, stream);
     } else {
         const unsigned nb = grid_for(g->n_pairs, g->rs_log2, g->max_blocks);
@@ -746,3 +848,9 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
     }
     return hipGetLastError();
 }
+
+#ifdef OVL_TRACE
+extern "C" __attribute__((visibility("default"))) int ovl_debug_trace_read(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ovl::ovl_trace_buf), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -340,14 +340,17 @@ def test_uniform_kernel_key_variants(engine, oracle_mod, params):
 
 
 def test_split_knob_equivalence(oracle_mod):
-    """OVL_SPLIT (r range over 2 / 4 wavefronts) must not change results."""
+    """OVL_SPLIT (0 = one wavefront per tile, >0 = latency mode with a side-pair
+    wavefront beside each sweeping one) must not change results, including a list
+    long enough (6250 tiles) to make latency-mode blocks loop over tiles."""
     import os
     from ovlgraph import OverlapEngine
     rng = random.Random(42)
     reads = [_rand(rng, 100) for _ in range(400)] + [_rand(rng, rng.randint(1, 99)) for _ in range(30)]
     n = len(reads)
-    a = np.array([rng.randrange(n) for _ in range(5000)], dtype=np.int32)
-    b = np.array([rng.randrange(n) for _ in range(5000)], dtype=np.int32)
+    nr = np.random.default_rng(42)
+    a = nr.integers(0, n, 400_000, dtype=np.int32)
+    b = nr.integers(0, n, 400_000, dtype=np.int32)
     rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
     for split in ("0", "1", "2"):
         os.environ["OVL_SPLIT"] = split

@@ -1,4 +1,4 @@
-# A/B of the uniform kernel's r-split (OVL_SPLIT=0,1,2) on cfg2 and target, kernel-only timing from bench.
+# A/B of the uniform kernel launch mode (OVL_SPLIT=0 normal, 1 latency mode; 2 = same as 1) on cfg2 and target, kernel-only timing from bench.
 set -u
 cd "$GRAFT_REPO_ROOT"
 OUT="$GRAFT_REPO_ROOT/gpurun_out/${1:-splitab}"
