@@ -96,7 +96,7 @@ def cpu_baseline(reads, a, b, budget_s: float = 10.0):
 class Workload:
     """One rank's read set + candidate list resident on its GPU."""
 
-    def __init__(self, name: str, seed: int, dev, engine=None):
+    def __init__(self, name: str, seed: int, dev, engine=None, indel: int = None, band: int = -1):
         import torch
         from ovlgraph import OverlapEngine
         from ovlgraph.candidates import dedup_reads, enumerate_candidates
@@ -112,13 +112,22 @@ class Workload:
         t0 = time.perf_counter()
         self.eng.set_reads(self.reads)
         self.t_pack = time.perf_counter() - t0
-        self.kernel = self.eng.plan()
+        from ovlgraph.engine import INDEL_DEFAULT
+        self.indel = INDEL_DEFAULT if indel is None else indel
+        self.band = band
+        self.kernel = self.eng.plan(10, -1, self.indel, band)
         self.n_pairs = int(self.a.shape[0])
         self.da = torch.as_tensor(self.a, device=dev)
         self.db = torch.as_tensor(self.b, device=dev)
         self.ds = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
         self.de = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
-        self.launch = self.eng.launcher(self.da, self.db, self.ds, self.de)
+        self.launch = self.eng.launcher(self.da, self.db, self.ds, self.de, 10, -1, self.indel, band)
+
+    def rebind(self, indel: int, band: int) -> None:
+        """Same resident reads and pairs, other scoring (band sweep)."""
+        self.indel, self.band = indel, band
+        self.kernel = self.eng.plan(10, -1, indel, band)
+        self.launch = self.eng.launcher(self.da, self.db, self.ds, self.de, 10, -1, indel, band)
 
     def algo_bytes(self) -> int:
         lens = np.fromiter((len(r) for r in self.reads), dtype=np.int64, count=len(self.reads))
@@ -150,6 +159,27 @@ def timed_steps(w: Workload, steps: int, warmup: int, dev, world: int):
     return time.perf_counter() - t0, ev0.elapsed_time(ev1) / max(steps, 1)
 
 
+def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
+    """Config 5's band-width sweep: the same resident pairs at each band (-1 = full DP).
+
+    band >= 0 is the build's seed-and-extend knob (ungapped seed j*, DP on
+    |(i - j) - (n - j*)| <= band), not a reference mode; cells_per_pair counts
+    the DP cells inside the band (full: n * m).
+    """
+    lens = np.fromiter((len(r) for r in w.reads), dtype=np.int64, count=len(w.reads))
+    n, m = lens[w.a].astype(np.float64), lens[w.b].astype(np.float64)
+    out = {"indel": indel, "match": 10, "mismatch": -1, "pairs": w.n_pairs, "points": []}
+    for band in bands:
+        w.rebind(indel, band)
+        el, km = timed_steps(w, steps, 1, dev, 1)
+        cells = float((n * m).mean()) if band < 0 else float(np.minimum(n * m, (2 * band + 1) * n).mean())
+        out["points"].append({"band": band, "kernel": w.kernel, "ms_per_step": el / steps * 1e3,
+                              "kernel_ms": km, "pairs_per_s": w.n_pairs * steps / el,
+                              "cells_per_pair_upper": round(cells, 1),
+                              "cells_per_s": w.n_pairs * cells / (km * 1e-3)})
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,6 +189,13 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra single-GPU configs")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--indel", type=int, default=None, help="indel score (default: the reference's -2**31)")
+    ap.add_argument("--band", type=int, default=-1, help="band half-width (-1 = full DP, the reference)")
+    ap.add_argument("--band-sweep", default=None,
+                    help="comma list of bands (-1 = full) timed on the same workload at --sweep-indel "
+                         "(config 5's sweep: 8,16,32,64,-1); reported under band_sweep")
+    ap.add_argument("--sweep-indel", type=int, default=-2)
+    ap.add_argument("--sweep-steps", type=int, default=5)
     args = ap.parse_args()
 
     import torch
@@ -178,7 +215,7 @@ def main() -> None:
         else:
             dist.init_process_group(backend)
 
-    w = Workload(args.config, seed=rank, dev=dev)
+    w = Workload(args.config, seed=rank, dev=dev, indel=args.indel, band=args.band)
     elapsed, kernel_ms = timed_steps(w, args.steps, args.warmup, dev, world)
 
     stats = torch.tensor([elapsed, kernel_ms, float(w.n_pairs)], dtype=torch.float64,
@@ -216,6 +253,7 @@ def main() -> None:
                 "read_length": w.cfg["l"],
                 "parallelism": f"pair-sharded x{world} (one process per GPU, own seeded read set per rank)",
                 "kernel": w.kernel,
+                "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},
             },
             "roofline": {
                 "bound": "hbm",
@@ -229,6 +267,10 @@ def main() -> None:
             },
             "host_setup_s": {"read_sim_and_enumeration": round(w.t_enum, 3), "upload_and_pack": round(w.t_pack, 4)},
         }
+        if world == 1 and args.band_sweep:
+            line["band_sweep"] = band_sweep(w, [int(x) for x in args.band_sweep.split(",")], args.sweep_indel,
+                                            args.sweep_steps, dev)
+            w.rebind(w.indel if args.indel is None else args.indel, args.band)
         if world == 1 and not args.no_extra:
             extra = {}
             for name in ("target", "cfg3"):

@@ -111,13 +111,46 @@ struct Plan {
     int kernel = OVL_KERNEL_NONE;
     bool key64 = false;
     bool wide = true;
+    int32_t band = -1;       // OVL_KERNEL_BANDED: band half-width
+    int seed_kernel = OVL_KERNEL_NONE;  // OVL_KERNEL_BANDED: how the seed end j* is computed
+    bool seed_key64 = false;
+    bool seed_wide = true;
 };
 
+int make_plan_full(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, Plan* out);
+
+// band >= 0: the build's seed-and-extend knob (oracle_overlap_banded), exact
+// (== the reference) whenever gaps cannot win -- the seed cell (n, j*) is
+// always in the band and nothing off the ungapped diagonals can beat it -- and
+// whenever the band covers every diagonal (band >= 2 * lmax).
 int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* out) {
-    if (band >= 0)
-        return fail(c, OVL_E_UNSUPPORTED, "band=%d: only the full DP (band < 0) is implemented in ABI v%d", band,
-                    OVL_ABI_VERSION);
     if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
+    const int64_t L = std::max<int32_t>(c->lmax, 1);
+    if (band < 0 || band >= 2 * L || gaps_cannot_win(match, mismatch, indel, L))
+        return make_plan_full(c, match, mismatch, indel, out);
+    // seed: the ungapped closed form (any kernel that evaluates it exactly)
+    Plan seed;
+    int rc = make_plan_full(c, match, mismatch, INT32_MIN, &seed);
+    if (rc != OVL_OK) return rc;
+    if (!gaps_cannot_win(match, mismatch, INT32_MIN, L))
+        return fail(c, OVL_E_UNSUPPORTED, "banded: the ungapped seed cannot be evaluated exactly at these scores");
+    Plan full;
+    rc = make_plan_full(c, match, mismatch, indel, &full);
+    if (rc != OVL_OK) return rc;
+    if (full.kernel != OVL_KERNEL_DP || full.wide)
+        return fail(c, OVL_E_UNSUPPORTED, "banded: scores too large for int32 cells (|score| * (2*lmax+1) >= 2^31)");
+    Plan p;
+    p.kernel = OVL_KERNEL_BANDED;
+    p.wide = false;
+    p.band = band;
+    p.seed_kernel = seed.kernel;
+    p.seed_key64 = seed.key64;
+    p.seed_wide = seed.wide;
+    *out = p;
+    return OVL_OK;
+}
+
+int make_plan_full(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, Plan* out) {
     const int64_t L = std::max<int32_t>(c->lmax, 1);
     const int64_t amax = std::max(iabs64(match), iabs64(mismatch));
     Plan p;
@@ -164,6 +197,15 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s) {
     if (n_pairs == 0) return OVL_OK;
+    if (pl.kernel == OVL_KERNEL_BANDED) {
+        // seed j* into d_end, then the banded DP reads it and overwrites (score, end)
+        Plan seed;
+        seed.kernel = pl.seed_kernel;
+        seed.key64 = pl.seed_key64;
+        seed.wide = pl.seed_wide;
+        int rc = launch_score_chunk(c, seed, d_a, d_b, n_pairs, match, mismatch, INT32_MIN, d_score, d_end, s);
+        if (rc != OVL_OK) return rc;
+    }
     if (pl.kernel == OVL_KERNEL_UNGAPPED) {
         OvlUngappedArgs g{};
         g.sfx = as<uint32_t>(c->sfx);
@@ -217,6 +259,7 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         g.tb = nullptr;
         g.err_flag = as<uint32_t>(c->err_flag);
         g.wide = pl.wide ? 1 : 0;
+        g.band = pl.kernel == OVL_KERNEL_BANDED ? pl.band : -1;
         HIPCHK(c, ovl_launch_dp(&g, s));
     }
     return OVL_OK;
@@ -511,6 +554,7 @@ OVL_API int ovl_align_one(ovl_ctx* c, int32_t a, int32_t b, int32_t match, int32
     g.tb = traceback ? as<int8_t>(c->tb) : nullptr;
     g.err_flag = as<uint32_t>(c->err_flag);
     g.wide = !(indel > INT32_MIN && M < (int64_t(1) << 31) && (2 * L + 1) * M < (int64_t(1) << 31));
+    g.band = -1;
     HIPCHK(c, ovl_launch_dp(&g, c->stream));
     int32_t res[2];
     HIPCHK(c, hipMemcpyAsync(res, c->score.p, sizeof(res), hipMemcpyDeviceToHost, c->stream));

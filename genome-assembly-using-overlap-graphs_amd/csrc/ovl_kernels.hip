@@ -632,11 +632,18 @@ __device__ __forceinline__ int64_t shr1<int64_t>(int64_t v) {
 // them from the staged LDS row (the previous strip's last row) and t codes.
 // Cell rule of aligners.py:35-48 with Acc-width arithmetic; the stored value
 // is narrowed to int32 as the reference's int32 table does.
-template <typename Acc>
+// BANDED (the build's band knob, oracle_overlap_banded; not a reference mode):
+// out_end[pair] holds the seed end j* on entry (the ungapped closed form's
+// first argmax, written by the launch before); only cells with
+// |(i - j) - d*| <= band, d* = n - j*, are filled, out-of-band predecessors
+// count as -inf, and only strips and anti-diagonal steps that meet the band are
+// swept.  A cell's diagonal predecessor is always in the band; "up" leaves it
+// only at the row's last band cell and "left" only at its first.
+template <typename Acc, bool BANDED>
 __global__ __launch_bounds__(64) void dp_kernel(
     const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx,
-    int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel,
+    int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel, int32_t band,
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, int8_t* __restrict__ tb,
     uint32_t* __restrict__ err_flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -659,23 +666,41 @@ __global__ __launch_bounds__(64) void dp_kernel(
         const int32_t m = len[b];
         const uint8_t* s = codes + off[a];
         const uint8_t* t = codes + off[b];
+        // band: seed diagonal d* and the rows [rlo, rhi] that hold band cells
+        const int32_t dstar = BANDED ? n - out_end[pair] : 0;
+        const int32_t W = BANDED ? band : 0;
+        const int32_t rlo = BANDED ? (dstar - W + 1 > 1 ? dstar - W + 1 : 1) : 1;
         __syncthreads();  // previous pair's LDS readers are done
         for (int j = lane; j <= m; j += 64) row0[j] = 0;
         for (int j = lane; j < m; j += 64) tcodes[j] = t[j];
         __syncthreads();
         int32_t* rin = row0;
         int32_t* rout = row1;
-        int32_t best = 0, bend = 0;  // tracked by the lane that owns row n
+        // tracked by the lane that owns row n; dp[n][0] = 0 is the j = 0 candidate
+        // (in banded mode only when (n, 0) is in the band)
+        int32_t best = (!BANDED || n - dstar - W <= 0) ? 0 : INT32_MIN, bend = 0;
         const int nstrips = (n + 63) >> 6;
-        for (int st = 0; st < nstrips; ++st) {
+        const int st0 = BANDED ? (rlo - 1) >> 6 : 0;
+        for (int st = st0; st < nstrips; ++st) {
             const int32_t i = 64 * st + 1 + lane;
             const bool row_ok = i <= n;
             const uint32_t sc = row_ok ? (uint32_t)s[i - 1] : 0xFFFFFFFFu;
+            // anti-diagonal steps: lane L is on column j = tau - L + 1
+            int tau_lo = 0, tau_hi = m + 62;
+            if (BANDED) {
+                const int lmax = (n - 64 * st - 1) < 63 ? (n - 64 * st - 1) : 63;
+                const int lo = 64 * st - dstar - W;
+                const int hi = 64 * st + 2 * lmax - dstar + W;
+                tau_lo = lo > 0 ? lo : 0;
+                tau_hi = hi < tau_hi ? hi : tau_hi;
+            }
+            const int32_t jlo = i - dstar - W, jhi = i - dstar + W;  // unclamped band edges of row i
             int32_t cur = 0;      // dp[i][j-1] (starts as dp[i][0] = 0)
-            int32_t uprev = 0;    // dp[i-1][j-1]
+            // dp[i-1][j-1]; lane 0 starts mid-row in banded mode
+            int32_t uprev = (BANDED && lane == 0) ? rin[tau_lo] : 0;
             uint32_t tch = 0;
             const bool last_strip_row = (lane == 63) && (st + 1 < nstrips);
-            for (int tau = 0; tau < m + 63; ++tau) {
+            for (int tau = tau_lo; tau <= tau_hi; ++tau) {
                 const int32_t j = tau - lane + 1;
                 // lane 0's inputs come from LDS (uniform address: broadcast)
                 const int32_t jj = tau + 1 <= m ? tau + 1 : m;
@@ -684,17 +709,20 @@ __global__ __launch_bounds__(64) void dp_kernel(
                 int32_t upin = shr1<int32_t>(cur);
                 uint32_t tin = (uint32_t)shr1<int32_t>((int32_t)tch);
                 if (lane == 0) { upin = lds_up; tin = lds_t; }
-                if (row_ok && j >= 1 && j <= m) {
+                const bool in_band = !BANDED || (j >= jlo && j <= jhi);
+                if (row_ok && j >= 1 && j <= m && in_band) {
                     const Acc diag = (Acc)uprev + (sc == tin ? (Acc)match : (Acc)mismatch);
                     const Acc up = (Acc)upin + (Acc)indel;
                     const Acc left = (Acc)cur + (Acc)indel;
+                    const bool up_ok = !BANDED || j != jhi;
+                    const bool left_ok = !BANDED || j != jlo;
                     int8_t dir;
                     Acc v;
-                    if (diag >= up && diag >= left) { v = diag; dir = 0; }
-                    else if (up >= left)            { v = up;   dir = 1; }
-                    else                            { v = left; dir = 2; }
+                    if ((!up_ok || diag >= up) && (!left_ok || diag >= left)) { v = diag; dir = 0; }
+                    else if (up_ok && (!left_ok || up >= left))               { v = up;   dir = 1; }
+                    else                                                      { v = left; dir = 2; }
                     cur = (int32_t)v;
-                    if (tb) tb[(int64_t)i * (m + 1) + j] = dir;
+                    if (!BANDED && tb) tb[(int64_t)i * (m + 1) + j] = dir;
                     if (i == n && cur > best) { best = cur; bend = j; }
                     if (last_strip_row) rout[j] = cur;
                 }
@@ -706,10 +734,11 @@ __global__ __launch_bounds__(64) void dp_kernel(
             __syncthreads();
             int32_t* tmp = rin; rin = rout; rout = tmp;
         }
-        // row n lives in lane (n-1) % 64 of the last strip; dp[n][0] = 0 is the j = 0 candidate.
+        // row n lives in lane (n-1) % 64 of the last strip
         const int owner = (n - 1) & 63;
         const int32_t bs = __shfl(best, owner, 64);
         const int32_t be = __shfl(bend, owner, 64);
+        __syncthreads();  // every lane has read out_end[pair] (banded seed) before it is overwritten
         if (lane == 0) {
             out_score[pair] = n > 0 && m > 0 ? bs : 0;
             out_end[pair] = n > 0 && m > 0 ? be : 0;
@@ -832,19 +861,27 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     return hipGetLastError();
 }
 
+template <typename Acc, bool BANDED>
+static void launch_dp_t(const OvlDpArgs* g, unsigned blocks, size_t lds, hipStream_t stream) {
+    dp_kernel<Acc, BANDED><<<blocks, 64, lds, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
+                                                         g->n_pairs, g->mcap, g->match, g->mismatch, g->indel,
+                                                         g->band, g->out_score, g->out_end, g->tb, g->err_flag);
+}
+
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     int64_t blocks = g->n_pairs;
     if (blocks > 16384) blocks = 16384;
     const size_t lds = (size_t)2 * (g->mcap + 1) * sizeof(int32_t) + (size_t)g->mcap + 16;
-    if (g->wide) {
-        dp_kernel<int64_t><<<(unsigned)blocks, 64, lds, stream>>>(
-            g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
-            g->mismatch, g->indel, g->out_score, g->out_end, g->tb, g->err_flag);
+    const unsigned nb = (unsigned)blocks;
+    if (g->band >= 0) {
+        // banded mode runs only where values fit int32 (the host checks) and never writes tb
+        if (g->wide || g->tb) return hipErrorInvalidValue;
+        launch_dp_t<int32_t, true>(g, nb, lds, stream);
+    } else if (g->wide) {
+        launch_dp_t<int64_t, false>(g, nb, lds, stream);
     } else {
-        dp_kernel<int32_t><<<(unsigned)blocks, 64, lds, stream>>>(
-            g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
-            g->mismatch, g->indel, g->out_score, g->out_end, g->tb, g->err_flag);
+        launch_dp_t<int32_t, false>(g, nb, lds, stream);
     }
     return hipGetLastError();
 }

@@ -16,14 +16,14 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "build", "libovl.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OVL_OK = 0
 ERRORS = {
     -1: "OVL_E_ARG", -2: "OVL_E_HIP", -3: "OVL_E_OOM", -4: "OVL_E_UNSUPPORTED",
     -5: "OVL_E_RANGE", -6: "OVL_E_STATE", -7: "OVL_E_INDEX",
 }
-KERNELS = {0: "none", 1: "ungapped", 2: "dp"}
+KERNELS = {0: "none", 1: "ungapped", 2: "dp", 3: "banded"}
 
 # name -> (restype, argtypes); mirrors include/ovl.h exactly
 _P = ctypes.c_void_p

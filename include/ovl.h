@@ -28,14 +28,14 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 1
+#define OVL_ABI_VERSION 2
 
 enum {
     OVL_OK = 0,
     OVL_E_ARG = -1,          /* bad argument (null pointer, negative size, bad offsets) */
     OVL_E_HIP = -2,          /* HIP runtime error */
     OVL_E_OOM = -3,          /* device allocation failed */
-    OVL_E_UNSUPPORTED = -4,  /* band >= 0 (not in this ABI version), read too long, >256 symbols */
+    OVL_E_UNSUPPORTED = -4,  /* read too long, >256 symbols, band at scores too large for int32 cells */
     OVL_E_RANGE = -5,        /* scoring magnitudes would overflow the int32 DP table */
     OVL_E_STATE = -6,        /* no resident reads (ovl_set_reads not called) */
     OVL_E_INDEX = -7         /* a pair index is outside [0, n_reads) */
@@ -44,7 +44,8 @@ enum {
 enum {
     OVL_KERNEL_NONE = 0,
     OVL_KERNEL_UNGAPPED = 1, /* 2-bit (or 4/8-bit) bit-plane popcount kernel; exact when gaps cannot win */
-    OVL_KERNEL_DP = 2        /* anti-diagonal wavefront DP, int64-exact, any scoring */
+    OVL_KERNEL_DP = 2,       /* anti-diagonal wavefront DP, int64-exact, any scoring */
+    OVL_KERNEL_BANDED = 3    /* ungapped seed + banded DP around its diagonal (band >= 0, gaps can win) */
 };
 
 typedef struct ovl_ctx ovl_ctx;
@@ -66,7 +67,14 @@ const char* ovl_last_error(const ovl_ctx* ctx);
  * One-shot batch scoring: uploads and packs the reads, scores
  * n_pairs candidates (a_idx[p], b_idx[p]) and writes out_score[p], out_end[p].
  * Replaces the loop body of overlapGraphs.py:50-53 for a whole candidate list.
- * band < 0 means the full DP (the only mode of this ABI version).
+ *
+ * band < 0: the full DP of aligners.py:27-57 (reference semantics, bit-exact).
+ * band >= 0: the build's seed-and-extend knob (not a reference mode): seed
+ *   j* = the ungapped first argmax, diagonal d* = n - j*; the aligners.py:33-48
+ *   recurrence on cells with |(i - j) - d*| <= band only, out-of-band
+ *   predecessors = -inf; last-row strict '>' first argmax over in-band cells.
+ *   Identical to band < 0 whenever gaps cannot win (e.g. the default
+ *   indel = -2^31) and when band >= 2 * (longest read).
  */
 int ovl_score_pairs(ovl_ctx* ctx, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
                     const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,

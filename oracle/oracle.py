@@ -127,6 +127,8 @@ def lib():
         L.oracle_batch_dp.restype = ctypes.c_int
         L.oracle_batch_ungapped.argtypes = [P, P, i32, P, P, i64, i64, i64, P, P, i32]
         L.oracle_batch_ungapped.restype = ctypes.c_int
+        L.oracle_batch_banded.argtypes = [P, P, i32, P, P, i64, i64, i64, i64, i32, P, P, i32]
+        L.oracle_batch_banded.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -185,6 +187,58 @@ def batch_ungapped(reads: Sequence[str], a_idx, b_idx, match=10, mismatch=-1,
     if rc != 0:
         raise RuntimeError(f"oracle_batch_ungapped failed rc={rc}")
     return sc, en
+
+
+def batch_banded(reads: Sequence[str], a_idx, b_idx, match=10, mismatch=-1, indel=-2, band=8,
+                 threads: int = 0, encoded=None) -> Tuple[np.ndarray, np.ndarray]:
+    """The build's banded seed-and-extend knob (oracle_overlap_banded; not a reference mode)."""
+    seqs, offs = encoded if encoded is not None else encode(reads)
+    a = np.ascontiguousarray(a_idx, dtype=np.int32)
+    b = np.ascontiguousarray(b_idx, dtype=np.int32)
+    sc = np.zeros(a.shape[0], np.int32)
+    en = np.zeros(a.shape[0], np.int32)
+    if seqs.size == 0:
+        seqs = np.zeros(1, np.uint8)
+    rc = lib().oracle_batch_banded(_ptr(seqs), _ptr(offs), len(offs) - 1, _ptr(a), _ptr(b), a.shape[0],
+                                   match, mismatch, indel, band, _ptr(sc), _ptr(en), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle_batch_banded failed rc={rc}")
+    return sc, en
+
+
+def banded_py(s: str, t: str, match: int = 10, mismatch: int = -1, indel: int = -2,
+              band: int = 8) -> Tuple[int, int]:
+    """Pure-Python statement of the banded knob (small cases; cross-checks the C version).
+
+    Seed j* = ungapped first argmax, d* = n - j*; the aligners.py:33-48 recurrence
+    on cells with |(i - j) - d*| <= band, out-of-band predecessors = -inf; last-row
+    strict '>' first argmax over in-band cells.
+    """
+    n, m = len(s), len(t)
+    _, jstar = ungapped(s, t, match, mismatch)
+    d = n - jstar
+    NEG = None
+    dp = [[0] * (m + 1) for _ in range(n + 1)]
+    inb = lambda i, j: abs((i - j) - d) <= band  # noqa: E731
+    for i in range(1, n + 1):
+        for j in range(1, m + 1):
+            if not inb(i, j):
+                dp[i][j] = NEG
+                continue
+            cand_d = dp[i - 1][j - 1] + (match if s[i - 1] == t[j - 1] else mismatch)
+            up = dp[i - 1][j] + indel if inb(i - 1, j) else NEG
+            left = dp[i][j - 1] + indel if inb(i, j - 1) else NEG
+            if (up is NEG or cand_d >= up) and (left is NEG or cand_d >= left):
+                dp[i][j] = cand_d
+            elif up is not NEG and (left is NEG or up >= left):
+                dp[i][j] = up
+            else:
+                dp[i][j] = left
+    best, end = None, -1
+    for j in range(m + 1):
+        if inb(n, j) and (best is None or dp[n][j] > best):
+            best, end = dp[n][j], j
+    return int(best), end
 
 
 def dp_one(s: str, t: str, match=10, mismatch=-1, indel=INT32_MIN, want_tb=False):

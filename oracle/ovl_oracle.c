@@ -95,9 +95,59 @@ void oracle_overlap_ungapped(const uint8_t* s, int32_t n, const uint8_t* t, int3
     *out_end = end;
 }
 
+/* Banded seed-and-extend variant (the build's band knob; NOT a reference mode,
+ * parity with the reference only at full width).  Seed: the ungapped closed
+ * form's first argmax j* (diagonal d* = n - j*).  Extend: the aligners.py:33-48
+ * recurrence restricted to cells with |(i - j) - d*| <= band; predecessors
+ * outside the band count as -inf (never chosen); row 0 / column 0 cells inside
+ * the band are 0.  Score: last-row cells inside the band, strict '>' first argmax.
+ * Requires values to fit int32 (no wrap): callers check that. */
+int oracle_overlap_banded(const uint8_t* s, int32_t n, const uint8_t* t, int32_t m,
+                          int64_t match, int64_t mismatch, int64_t indel, int32_t band,
+                          int32_t* out_score, int32_t* out_end)
+{
+    int32_t seed_score, jstar;
+    oracle_overlap_ungapped(s, n, t, m, match, mismatch, &seed_score, &jstar);
+    const int64_t dstar = (int64_t)n - jstar;
+    const size_t W = (size_t)m + 1;
+    const size_t cells = ((size_t)n + 1) * W;
+    int64_t* dp = (int64_t*)calloc(cells, sizeof(int64_t));
+    if (!dp) return -1;
+    for (int32_t i = 1; i <= n; ++i) {
+        const int64_t* prev = dp + (size_t)(i - 1) * W;
+        int64_t* cur = dp + (size_t)i * W;
+        const int64_t jlo = (int64_t)i - dstar - band;   /* unclamped band edges of row i */
+        const int64_t jhi = (int64_t)i - dstar + band;
+        const uint8_t si = s[i - 1];
+        for (int32_t j = 1; j <= m; ++j) {
+            if (j < jlo || j > jhi) continue;
+            const int64_t diag = prev[j - 1] + (si == t[j - 1] ? match : mismatch);
+            const int up_ok = j != jhi;    /* (i-1, j) is inside the band */
+            const int left_ok = j != jlo;  /* (i, j-1) is inside the band (or column 0) */
+            const int64_t up = prev[j] + indel;
+            const int64_t left = cur[j - 1] + indel;
+            if ((!up_ok || diag >= up) && (!left_ok || diag >= left)) cur[j] = diag;
+            else if (up_ok && (!left_ok || up >= left))               cur[j] = up;
+            else                                                      cur[j] = left;
+        }
+    }
+    int64_t best = 0;
+    int32_t end = -1;
+    const int64_t* last = dp + (size_t)n * W;
+    for (int32_t j = 0; j <= m; ++j) {
+        const int64_t k = (int64_t)n - j - dstar;
+        if (k < -band || k > band) continue;
+        if (end < 0 || last[j] > best) { best = last[j]; end = j; }
+    }
+    *out_score = (int32_t)best;
+    *out_end = end;
+    free(dp);
+    return 0;
+}
+
 static int batch_common(int mode, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
                         const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
-                        int64_t match, int64_t mismatch, int64_t indel,
+                        int64_t match, int64_t mismatch, int64_t indel, int32_t band,
                         int32_t* out_score, int32_t* out_end, int32_t threads)
 {
     for (int64_t p = 0; p < n_pairs; ++p) {
@@ -116,6 +166,8 @@ static int batch_common(int mode, const uint8_t* seqs, const int64_t* offsets, i
         const int32_t m = (int32_t)(offsets[b + 1] - offsets[b]);
         if (mode == 0) {
             err |= oracle_overlap_dp(s, n, t, m, match, mismatch, indel, out_score + p, out_end + p, NULL);
+        } else if (mode == 2) {
+            err |= oracle_overlap_banded(s, n, t, m, match, mismatch, indel, band, out_score + p, out_end + p);
         } else {
             oracle_overlap_ungapped(s, n, t, m, match, mismatch, out_score + p, out_end + p);
         }
@@ -130,7 +182,7 @@ int oracle_batch_dp(const uint8_t* seqs, const int64_t* offsets, int32_t n_reads
                     int64_t match, int64_t mismatch, int64_t indel,
                     int32_t* out_score, int32_t* out_end, int32_t threads)
 {
-    return batch_common(0, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, indel,
+    return batch_common(0, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, indel, -1,
                         out_score, out_end, threads);
 }
 
@@ -139,6 +191,15 @@ int oracle_batch_ungapped(const uint8_t* seqs, const int64_t* offsets, int32_t n
                           int64_t match, int64_t mismatch,
                           int32_t* out_score, int32_t* out_end, int32_t threads)
 {
-    return batch_common(1, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, 0,
+    return batch_common(1, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, 0, -1,
+                        out_score, out_end, threads);
+}
+
+int oracle_batch_banded(const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                        const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                        int64_t match, int64_t mismatch, int64_t indel, int32_t band,
+                        int32_t* out_score, int32_t* out_end, int32_t threads)
+{
+    return batch_common(2, seqs, offsets, n_reads, a_idx, b_idx, n_pairs, match, mismatch, indel, band,
                         out_score, out_end, threads);
 }

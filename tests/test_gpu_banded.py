@@ -1,0 +1,99 @@
+"""GPU banded seed-and-extend knob (band >= 0) vs its oracle, bit-exact.
+
+The band is the build's perf knob for the config-5 sweep, not a
+reference mode: parity with the reference holds at full width and at the
+default indel; narrower bands are checked against oracle_overlap_banded.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from test_oracle_banded import _indel_reads
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from ovlgraph import OverlapEngine
+    eng = OverlapEngine(0)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="module")
+def reads_pairs():
+    rng = random.Random(23)
+    # lengths up to 250: several 64-row strips, band edges inside and outside the table
+    reads = _indel_reads(rng, 300, 250) + _indel_reads(rng, 100, 40)
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(4000)], np.int32)
+    b = np.array([rng.randrange(n) for _ in range(4000)], np.int32)
+    return reads, a, b
+
+
+@pytest.mark.parametrize("band", [0, 1, 2, 5, 8, 16, 31, 32, 63, 64, 65, 100, 200])
+def test_banded_vs_oracle(engine, oracle_mod, reads_pairs, band):
+    reads, a, b = reads_pairs
+    engine.set_reads(reads)
+    assert engine.plan(10, -1, -2, band) == "banded"
+    sc, en = engine.score(a, b, 10, -1, -2, band)
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("params", [(1, -1, -1), (2, -3, -5), (5, -4, -1), (10, -1, -30)])
+@pytest.mark.parametrize("band", [3, 24])
+def test_banded_params_vs_oracle(engine, oracle_mod, reads_pairs, params, band):
+    reads, a, b = reads_pairs
+    engine.set_reads(reads)
+    sc, en = engine.score(a, b, *params, band)
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, *params, band)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+def test_band_at_default_indel_is_exact(engine, oracle_mod, reads_pairs):
+    reads, a, b = reads_pairs
+    engine.set_reads(reads)
+    assert engine.plan(band=4) == engine.plan()
+    sc, en = engine.score(a, b, band=4)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+def test_full_width_band_is_the_reference_dp(engine, oracle_mod, reads_pairs):
+    reads, a, b = reads_pairs
+    engine.set_reads(reads)
+    lmax = max(len(r) for r in reads)
+    assert engine.plan(10, -1, -2, 2 * lmax) == "dp"
+    sc, en = engine.score(a, b, 10, -1, -2, 2 * lmax)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b, 10, -1, -2)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+def test_banded_cfg5_sample(engine, oracle_mod):
+    """Config 5 reads (PhiX, l=250, p=0.05): a strided 20k-pair sample at the sweep's bands."""
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("cfg5"))
+    a, b = enumerate_candidates(reads, 5)
+    idx = np.linspace(0, a.shape[0] - 1, 20000).astype(np.int64)
+    a, b = a[idx], b[idx]
+    engine.set_reads(reads)
+    for band in (8, 64):
+        sc, en = engine.score(a, b, 10, -1, -2, band)
+        rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
+
+
+def test_banded_unsupported_magnitudes(engine):
+    from ovlgraph import OvlError
+    engine.set_reads(["ACGTACGT", "CGTACGTA"])
+    with pytest.raises(OvlError, match="OVL_E_UNSUPPORTED"):
+        engine.score([0], [1], 2 ** 28, -1, -1, 4)

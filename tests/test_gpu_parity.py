@@ -236,7 +236,7 @@ def test_errors(engine):
     with pytest.raises(OvlError, match="OVL_E_INDEX"):
         engine.score([0, 2], [1, 0])
     with pytest.raises(OvlError, match="OVL_E_UNSUPPORTED"):
-        engine.score([0], [1], band=8)
+        engine.score([0], [1], 2 ** 28, -1, -1, 3)   # banded, scores too large for int32 cells
     with pytest.raises(OvlError, match="OVL_E_ARG"):
         engine.score([0, 1], [1])
 
