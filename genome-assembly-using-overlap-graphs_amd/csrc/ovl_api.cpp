@@ -50,6 +50,9 @@ struct ovl_ctx {
     DevBuf codes, off, len, sfx, pfx, lut, full;  // full: bit r set iff len[r] == lmax
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
+    // device candidate enumeration (ovl_candidates): per-read keys / groups and the pair list
+    DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
+    int64_t cand_n = -1;  // -1: no candidate list for the resident reads
 };
 
 namespace {
@@ -327,7 +330,8 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->full, &c->a, &c->b, &c->score, &c->end,
-                      &c->tb, &c->err_flag})
+                      &c->tb, &c->err_flag, &c->k_pre, &c->k_suf, &c->k_sorted, &c->k_iota, &c->k_order, &c->k_lo,
+                      &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -373,6 +377,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     const int32_t trow = wmax ? ((wmax * planes + 3) & ~3) : 0;
 
     c->n_reads = -1;  // invalid until fully built
+    c->cand_n = -1;
     DevBuf raw;
     HIPCHK(c, ensure(c->off, sizeof(int64_t) * off.size()));
     HIPCHK(c, ensure(c->len, sizeof(int32_t) * len.size()));
@@ -562,5 +567,107 @@ OVL_API int ovl_align_one(ovl_ctx* c, int32_t a, int32_t b, int32_t match, int32
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *out_score = res[0];
     *out_end = res[1];
+    return OVL_OK;
+}
+
+// ----------------------------------------------------------------------------- candidate enumeration
+
+OVL_API int ovl_candidates(ovl_ctx* c, int32_t k, int64_t* out_n_pairs) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!out_n_pairs) return fail(c, OVL_E_ARG, "out_n_pairs is NULL");
+    if (k < 0) return fail(c, OVL_E_ARG, "k-mer length must be non-negative (k=%d)", k);
+    if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
+    const int32_t bits = c->planes;  // symbol codes are dense: < 2^planes
+    if (k > 0 && (int64_t)k * bits > 58)
+        return fail(c, OVL_E_UNSUPPORTED, "k=%d with %d-bit symbols does not fit a 64-bit key (k * bits <= 58)", k,
+                    bits);
+    HIPCHK(c, hipSetDevice(c->device));
+    c->cand_n = -1;
+    const int32_t n = c->n_reads;
+    const size_t nr = (size_t)std::max(n, 1);
+    const int all = k == 0 ? 1 : 0;
+    hipStream_t s = c->stream;
+    HIPCHK(c, ensure(c->k_lo, nr * sizeof(int64_t)));
+    HIPCHK(c, ensure(c->k_hi, nr * sizeof(int64_t)));
+    HIPCHK(c, ensure(c->k_cnt, nr * sizeof(int64_t)));
+    HIPCHK(c, ensure(c->k_offs, nr * sizeof(int64_t)));
+    size_t temp = 0;
+    HIPCHK(c, ovl_cand_temp_bytes(n, &temp));
+    HIPCHK(c, ensure(c->k_temp, temp));
+    if (!all) {
+        HIPCHK(c, ensure(c->k_pre, nr * sizeof(uint64_t)));
+        HIPCHK(c, ensure(c->k_suf, nr * sizeof(uint64_t)));
+        HIPCHK(c, ensure(c->k_sorted, nr * sizeof(uint64_t)));
+        HIPCHK(c, ensure(c->k_iota, nr * sizeof(int32_t)));
+        HIPCHK(c, ensure(c->k_order, nr * sizeof(int32_t)));
+        HIPCHK(c, ovl_cand_keys(as<uint8_t>(c->codes), as<int64_t>(c->off), as<int32_t>(c->len), n, k, bits,
+                                as<uint64_t>(c->k_pre), as<uint64_t>(c->k_suf), as<int32_t>(c->k_iota), s));
+        HIPCHK(c, ovl_cand_sort(c->k_temp.p, c->k_temp.bytes, as<uint64_t>(c->k_pre), as<uint64_t>(c->k_sorted),
+                                as<int32_t>(c->k_iota), as<int32_t>(c->k_order), n, s));
+    }
+    HIPCHK(c, ovl_cand_count(as<uint64_t>(c->k_sorted), as<uint64_t>(c->k_pre), as<uint64_t>(c->k_suf), n, all,
+                             as<int64_t>(c->k_lo), as<int64_t>(c->k_hi), as<int64_t>(c->k_cnt), s));
+    HIPCHK(c, ovl_cand_scan(c->k_temp.p, c->k_temp.bytes, as<int64_t>(c->k_cnt), as<int64_t>(c->k_offs), n, s));
+    int64_t tail[2] = {0, 0};
+    if (n > 0) {
+        HIPCHK(c, hipMemcpyAsync(&tail[0], as<int64_t>(c->k_offs) + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(&tail[1], as<int64_t>(c->k_cnt) + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, hipStreamSynchronize(s));
+    const int64_t total = tail[0] + tail[1];
+    HIPCHK(c, ensure(c->cand_a, (size_t)total * sizeof(int32_t)));
+    HIPCHK(c, ensure(c->cand_b, (size_t)total * sizeof(int32_t)));
+    if (total > 0)
+        HIPCHK(c, ovl_cand_emit(as<int32_t>(c->k_order), as<int64_t>(c->k_lo), as<int64_t>(c->k_hi),
+                                as<int64_t>(c->k_offs), n, all, as<int32_t>(c->cand_a), as<int32_t>(c->cand_b), s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->cand_n = total;
+    *out_n_pairs = total;
+    return OVL_OK;
+}
+
+OVL_API int ovl_candidates_copy(ovl_ctx* c, int32_t* a_idx, int32_t* b_idx) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (c->cand_n < 0) return fail(c, OVL_E_STATE, "no candidate list: call ovl_candidates first");
+    if (c->cand_n == 0) return OVL_OK;
+    if (!a_idx || !b_idx) return fail(c, OVL_E_ARG, "NULL host pointer");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t bytes = (size_t)c->cand_n * sizeof(int32_t);
+    HIPCHK(c, hipMemcpyAsync(a_idx, c->cand_a.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(b_idx, c->cand_b.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return OVL_OK;
+}
+
+OVL_API int ovl_candidates_device(const ovl_ctx* c, const int32_t** d_a_idx, const int32_t** d_b_idx,
+                                  int64_t* n_pairs) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (c->cand_n < 0) return fail(c, OVL_E_STATE, "no candidate list: call ovl_candidates first");
+    if (d_a_idx) *d_a_idx = reinterpret_cast<const int32_t*>(c->cand_a.p);
+    if (d_b_idx) *d_b_idx = reinterpret_cast<const int32_t*>(c->cand_b.p);
+    if (n_pairs) *n_pairs = c->cand_n;
+    return OVL_OK;
+}
+
+OVL_API int ovl_score_candidates(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                                 int32_t* out_score, int32_t* out_end) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (c->cand_n < 0) return fail(c, OVL_E_STATE, "no candidate list: call ovl_candidates first");
+    Plan p;
+    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    if (rc != OVL_OK) return rc;
+    const int64_t n = c->cand_n;
+    if (n == 0) return OVL_OK;
+    if (!out_score || !out_end) return fail(c, OVL_E_ARG, "NULL host pointer");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t bytes = sizeof(int32_t) * (size_t)n;
+    HIPCHK(c, ensure(c->score, bytes));
+    HIPCHK(c, ensure(c->end, bytes));
+    rc = launch_score(c, p, as<int32_t>(c->cand_a), as<int32_t>(c->cand_b), n, match, mismatch, indel,
+                      as<int32_t>(c->score), as<int32_t>(c->end), c->stream);
+    if (rc != OVL_OK) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_score, c->score.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out_end, c->end.p, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return OVL_OK;
 }

@@ -53,3 +53,19 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream_t stream);
 
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);
+
+// candidate enumeration (ovl_candidates.hip)
+extern "C" hipError_t ovl_cand_keys(const uint8_t* codes, const int64_t* off, const int32_t* len, int32_t n_reads,
+                                    int32_t k, int32_t bits, uint64_t* pre_key, uint64_t* suf_key, int32_t* iota,
+                                    hipStream_t stream);
+extern "C" hipError_t ovl_cand_temp_bytes(int32_t n_reads, size_t* bytes);
+extern "C" hipError_t ovl_cand_sort(void* temp, size_t temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                                    const int32_t* vals_in, int32_t* vals_out, int32_t n_reads, hipStream_t stream);
+extern "C" hipError_t ovl_cand_count(const uint64_t* sorted, const uint64_t* pre_key, const uint64_t* suf_key,
+                                     int32_t n_reads, int32_t all_pairs, int64_t* lo, int64_t* hi, int64_t* cnt,
+                                     hipStream_t stream);
+extern "C" hipError_t ovl_cand_scan(void* temp, size_t temp_bytes, const int64_t* cnt, int64_t* offs, int32_t n_reads,
+                                    hipStream_t stream);
+extern "C" hipError_t ovl_cand_emit(const int32_t* order, const int64_t* lo, const int64_t* hi, const int64_t* offs,
+                                    int32_t n_reads, int32_t all_pairs, int32_t* out_a, int32_t* out_b,
+                                    hipStream_t stream);

@@ -45,6 +45,10 @@ SIGNATURES = {
     "ovl_score_device": (ctypes.c_int, [_P, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P, _P]),
     "ovl_check_device_errors": (ctypes.c_int, [_P]),
     "ovl_align_one": (ctypes.c_int, [_P, _i32, _i32, _i32, _i32, _i64, _pi32, _pi32, _P]),
+    "ovl_candidates": (ctypes.c_int, [_P, _i32, _pi64]),
+    "ovl_candidates_copy": (ctypes.c_int, [_P, _P, _P]),
+    "ovl_candidates_device": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _pi64]),
+    "ovl_score_candidates": (ctypes.c_int, [_P, _i32, _i32, _i64, _i32, _P, _P]),
 }
 
 

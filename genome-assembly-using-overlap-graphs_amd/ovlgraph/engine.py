@@ -104,6 +104,45 @@ class OverlapEngine:
         check(self._L.ovl_plan(self._ctx, match, mismatch, indel, band, ctypes.byref(k)), self._ctx)
         return _lib.KERNELS[k.value]
 
+    # ---------------------------------------------------------------- candidates
+    def candidates(self, k: int = 5) -> Tuple[np.ndarray, np.ndarray]:
+        """k-mer candidate pairs over the resident (distinct) reads, enumerated on the GPU.
+
+        Same list and order as ``candidates.enumerate_candidates`` (overlapGraphs.py:30-52);
+        the list also stays resident for ``score_candidates``.
+        """
+        n = self.enumerate_candidates(k)
+        a = np.empty(n, dtype=np.int32)
+        b = np.empty(n, dtype=np.int32)
+        if n:
+            check(self._L.ovl_candidates_copy(self._ctx, _ptr(a), _ptr(b)), self._ctx)
+        return a, b
+
+    def enumerate_candidates(self, k: int = 5) -> int:
+        """Enumerate the candidate list on the device (kept resident); returns its length."""
+        if k < 0:
+            raise AssertionError("k-mer length must be non-negative")
+        n = ctypes.c_int64()
+        check(self._L.ovl_candidates(self._ctx, int(k), ctypes.byref(n)), self._ctx)
+        return int(n.value)
+
+    def candidates_device(self) -> Tuple[int, int, int]:
+        """(device ptr of a_idx, device ptr of b_idx, n_pairs) of the resident candidate list."""
+        pa, pb, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check(self._L.ovl_candidates_device(self._ctx, ctypes.byref(pa), ctypes.byref(pb), ctypes.byref(n)),
+              self._ctx)
+        return pa.value or 0, pb.value or 0, int(n.value)
+
+    def score_candidates(self, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
+                         band: int = -1) -> Tuple[np.ndarray, np.ndarray]:
+        """Score the resident candidate list (no pair upload) -> (score, end) host arrays."""
+        n = self.candidates_device()[2]
+        sc = np.empty(n, dtype=np.int32)
+        en = np.empty(n, dtype=np.int32)
+        check(self._L.ovl_score_candidates(self._ctx, match, mismatch, indel, band, _ptr(sc), _ptr(en)),
+              self._ctx)
+        return sc, en
+
     # ---------------------------------------------------------------- scoring
     def score(self, a_idx, b_idx, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
               band: int = -1) -> Tuple[np.ndarray, np.ndarray]:

@@ -5,9 +5,11 @@ same ``(nx.DiGraph, read_copies)``: node names ``f"{read}_{copy}"`` inserted in
 ``read_copies`` order (:22-28), edges inserted per candidate pair in the
 reference's enumeration order and then per (copy_a, copy_b) (:43-60), with the
 attributes ``weight`` (score) and ``end_position`` as Python ints.  The only
-change is *how* the scores are computed: the k-mer candidate list is
-enumerated in Python (``candidates.enumerate_candidates``) and scored in one
-batched GPU call instead of one ``overlap_alignment`` call per pair (:53).
+change is *how* the list is built and scored: the k-mer candidate list is
+enumerated on the GPU (``OverlapEngine.candidates``; the host restatement
+``candidates.enumerate_candidates`` when asked, or when the keys do not fit the
+device's 64-bit keys) and scored in one batched GPU call instead of one
+``overlap_alignment`` call per pair (:53).
 
 Also provided: ``construct_overlap_graph_string`` (:196-232) and
 ``construct_string_graph`` (:332-351), which score all ordered pairs / all
@@ -24,8 +26,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import networkx as nx
 import numpy as np
 
+from ._lib import OvlError
 from .candidates import dedup_reads, enumerate_candidates
 from .engine import INDEL_DEFAULT, OverlapEngine, default_engine
+
+CANDIDATE_MODES = ("auto", "device", "host")
 
 
 def _score(distinct: Sequence[str], a: np.ndarray, b: np.ndarray, engine: Optional[OverlapEngine],
@@ -74,12 +79,41 @@ def assemble_graph(distinct: Sequence[str], counts: Sequence[int], a, b, score, 
     return G
 
 
-def construct_overlap_graph_nx_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None):
+def candidates_and_scores(distinct: Sequence[str], k: int, engine: Optional[OverlapEngine] = None, scorer=None,
+                          candidates: str = "auto"):
+    """Candidate pairs (overlapGraphs.py:30-52) and their (score, end) (:53), in reference order.
+
+    ``candidates``: "device" enumerates on the GPU (list kept resident and scored
+    without a host round trip), "host" uses ``enumerate_candidates``, "auto" is
+    "device" unless the k-mer keys do not fit the device path (OVL_E_UNSUPPORTED).
+    A custom ``scorer`` (e.g. the sharded path) always gets host-enumerated pairs.
+    """
+    if candidates not in CANDIDATE_MODES:
+        raise ValueError(f"candidates must be one of {CANDIDATE_MODES}")
+    if scorer is not None or candidates == "host":
+        a, b = enumerate_candidates(distinct, k)
+        sc, en = _score(distinct, a, b, engine, scorer)
+        return a, b, sc, en
+    eng = engine or default_engine()
+    eng.set_reads(distinct)
+    try:
+        a, b = eng.candidates(k)
+    except OvlError as e:
+        if e.code != -4 or candidates == "device":
+            raise
+        a, b = enumerate_candidates(distinct, k)
+        sc, en = _score(distinct, a, b, eng, None)
+        return a, b, sc, en
+    sc, en = eng.score_candidates(10, -1, INDEL_DEFAULT)
+    return a, b, sc.tolist(), en.tolist()
+
+
+def construct_overlap_graph_nx_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
+                                 candidates: str = "auto"):
     """Overlap graph over k-mer-filtered candidates (overlapGraphs.py:5-61)."""
     assert k >= 0, "k-mer length must be non-negative"
     distinct, counts = dedup_reads(reads)
-    a, b = enumerate_candidates(distinct, k)
-    sc, en = _score(distinct, a, b, engine, scorer)
+    a, b, sc, en = candidates_and_scores(distinct, k, engine, scorer, candidates)
     G = assemble_graph(distinct, counts, a, b, sc, en)
     return G, dict(zip(distinct, counts))
 
@@ -87,11 +121,11 @@ def construct_overlap_graph_nx_k(reads, k=5, engine: Optional[OverlapEngine] = N
 build_overlap_graph = construct_overlap_graph_nx_k
 
 
-def construct_overlap_graph_string(reads, engine: Optional[OverlapEngine] = None, scorer=None):
+def construct_overlap_graph_string(reads, engine: Optional[OverlapEngine] = None, scorer=None,
+                                   candidates: str = "auto"):
     """All ordered distinct pairs, edges where score > 0 (overlapGraphs.py:196-232)."""
     distinct, counts = dedup_reads(reads)
-    a, b = enumerate_candidates(distinct, 0)
-    sc, en = _score(distinct, a, b, engine, scorer)
+    a, b, sc, en = candidates_and_scores(distinct, 0, engine, scorer, candidates)
     G = assemble_graph(distinct, counts, a, b, sc, en, min_score=0)
     return G, dict(zip(distinct, counts))
 

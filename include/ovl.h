@@ -118,6 +118,29 @@ int ovl_check_device_errors(ovl_ctx* ctx);
 int ovl_align_one(ovl_ctx* ctx, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
                   int32_t* out_score, int32_t* out_end, int8_t* traceback);
 
+/*
+ * k-mer candidate enumeration on the device over the resident reads, which must
+ * be the distinct reads in read_copies order (overlapGraphs.py:18-20).  Produces
+ * exactly the pair list the reference scores, in its order (overlapGraphs.py:30-52):
+ * for each read a in order, every read b != a whose prefix read[:k] equals a's
+ * suffix read[-k:] (whole reads when shorter than k), b in read order; k == 0:
+ * every b != a.  The list stays in the context (until the next ovl_candidates or
+ * ovl_set_reads); *out_n_pairs receives its length.  OVL_E_UNSUPPORTED when
+ * k * (bits per symbol: 2, 4 or 8) > 58.  Replaces the Python loops of
+ * overlapGraphs.py:30-52 (which the host path, ovlgraph/candidates.py, restates).
+ */
+int ovl_candidates(ovl_ctx* ctx, int32_t k, int64_t* out_n_pairs);
+
+/* Copy the context's candidate list to host arrays of *out_n_pairs entries each. */
+int ovl_candidates_copy(ovl_ctx* ctx, int32_t* a_idx, int32_t* b_idx);
+
+/* Device pointers (and length) of the context's candidate list, for ovl_score_device. */
+int ovl_candidates_device(const ovl_ctx* ctx, const int32_t** d_a_idx, const int32_t** d_b_idx, int64_t* n_pairs);
+
+/* Score the context's candidate list (no pair upload); host outputs; synchronous. */
+int ovl_score_candidates(ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                         int32_t* out_score, int32_t* out_end);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,7 @@ def test_assert_k_nonnegative():
 
 
 def test_no_candidates_needs_no_gpu():
-    G, copies = og.construct_overlap_graph_nx_k(["AAAA", "CCCC", "AAAA"], k=2)
+    # host enumeration finds no pair -> nothing is scored -> no device needed
+    G, copies = og.construct_overlap_graph_nx_k(["AAAA", "CCCC", "AAAA"], k=2, candidates="host")
     assert list(G.nodes()) == ["AAAA_0", "AAAA_1", "CCCC_0"]
     assert G.number_of_edges() == 0 and copies == {"AAAA": 2, "CCCC": 1}
