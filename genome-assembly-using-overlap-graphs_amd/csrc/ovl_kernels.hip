@@ -290,8 +290,8 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     }
     const int32_t d16 = (int32_t)((uint32_t)dms << 16);
     const int32_t dv = __builtin_amdgcn_readfirstlane(d16);
-    // one r iteration over blocks [0, NQ) (NQ compile-time), r scalar
-    auto body = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag) {
+    // keys of one r over blocks [0, NQ) (NQ compile-time), r scalar
+    auto keys = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag, T (&kq)[W + 1]) {
         constexpr int NQ = decltype(nq_tag)::value;
         uint32_t U[TW][P];
 #pragma unroll
@@ -315,13 +315,30 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
                 if (i == 0) mm &= vt;
                 X += (uint32_t)__builtin_popcount(mm);
             }
-            T key;
             if constexpr (KM == 0) {
-                key = ((int32_t)X * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24
+                kq[q] = ((int32_t)X * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24
             } else {
-                key = (int64_t)dms * 4294967296ll * (int64_t)X + rm;
+                kq[q] = (int64_t)dms * 4294967296ll * (int64_t)X + rm;
             }
-            best[q] = key > best[q] ? key : best[q];
+        }
+    };
+    auto body = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        T kq[W + 1];
+        keys(r, vt, rm, nq_tag, kq);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) best[q] = kq[q] > best[q] ? kq[q] : best[q];
+    };
+    // two consecutive r per step: per block one 3-way max (v_max3_i32) for both keys
+    auto body2 = [&](uint32_t r, T rm, auto nq_tag) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        T k0[W + 1], k1[W + 1];
+        keys(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, nq_tag, k0);
+        keys(r + 1, (uint32_t)((int32_t)0x80000000 >> r), rm + mq, nq_tag, k1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const T m01 = k0[q] > k1[q] ? k0[q] : k1[q];
+            best[q] = m01 > best[q] ? m01 : best[q];
         }
     };
     // r = 0: j = 32q (q >= 1); block W only when lw == 32W
@@ -337,14 +354,31 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     T rm = (T)r * mq;
     const uint32_t rc = (uint32_t)(rcut < 31 ? rcut : 31);
     const uint32_t ra = rc < r_hi - 1 ? rc : r_hi - 1;
-    for (; r <= ra; ++r) {  // blocks 0..W-1
-        const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> (r - 1));
-        body(r, vt, rm, std::integral_constant<int, W>{});
+    // (int64 keys have no 3-way max and no registers to spare: one r per step)
+    for (; KM == 0 && r + 1 <= ra; r += 2) {  // blocks 0..W-1, two r per step
+        body2(r, rm, std::integral_constant<int, W>{});
+        rm += 2 * mq;
+    }
+    for (; KM != 0 && r < ra; ++r) {
+        body(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, std::integral_constant<int, W>{});
         rm += mq;
     }
-    for (; r < r_hi; ++r) {  // blocks 0..W-2
-        const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> (r - 1));
-        body(r, vt, rm, std::integral_constant<int, W - 1>{});
+    if (r <= ra) {
+        body(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, std::integral_constant<int, W>{});
+        ++r;
+        rm += mq;
+    }
+    for (; KM == 0 && r + 1 < r_hi; r += 2) {  // blocks 0..W-2, two r per step
+        body2(r, rm, std::integral_constant<int, W - 1>{});
+        rm += 2 * mq;
+    }
+    for (; KM != 0 && r + 1 < r_hi; ++r) {
+        body(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, std::integral_constant<int, W - 1>{});
+        rm += mq;
+    }
+    if (r < r_hi) {
+        body(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, std::integral_constant<int, W - 1>{});
+        ++r;
         rm += mq;
     }
     T out = 0;
@@ -446,9 +480,9 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const int64_t n_tiles = (n_pairs + 63) >> 6;
     int head = 0, tail = 0;                        // wave-uniform ring cursors
     // score ring[head .. head + count), count <= 16, with 64/count-ish lanes per pair:
-    // 4 lanes (16 pairs), 8 lanes (<= 8) or 16 lanes (<= 4) to shorten the serial r loop
+    // 4 lanes (16 pairs), 8 lanes (<= 8), 16 lanes (<= 4) or 32 lanes (<= 2): shortest serial r loop
     auto drain = [&](int count) {
-        const int rs = count > 8 ? 2 : (count > 4 ? 3 : 4);   // log2(lanes per pair)
+        const int rs = count > 8 ? 2 : (count > 4 ? 3 : (count > 2 ? 4 : 5));   // log2(lanes per pair)
         const int ppw = 64 >> rs;
         const int slot = lane & (ppw - 1);
         const bool mine = slot < count;
@@ -508,7 +542,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             for (int h = 0; h < cnt; h += 16) {
                 const int count = cnt - h < 16 ? cnt - h : 16;
-                const int rs = count > 8 ? 2 : (count > 4 ? 3 : 4);
+                const int rs = count > 8 ? 2 : (count > 4 ? 3 : (count > 2 ? 4 : 5));
                 const int slot = lane & ((64 >> rs) - 1);
                 const bool own = slot < count;
                 const int s = own ? h + slot : 0;
