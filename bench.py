@@ -43,19 +43,48 @@ def algorithmic_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> int:
     return int(q[a].sum() + q[b].sum() + 16 * a.shape[0])
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch from the committed PMC summary (profiles/*pmc*.json) for this workload."""
+def load_profile(workload: str):
+    """The committed PMC summary (profiles/*pmc*.json, newest round first) for this workload, or {}."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
-        return None
+        return {}
     for name in sorted(os.listdir(pdir), reverse=True):
         if "pmc" in name and name.endswith(".json"):
             try:
                 d = json.load(open(os.path.join(pdir, name)))
             except Exception:
                 continue
-            if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
-                return int(d["hbm_bytes_per_launch"])
+            if d.get("workload") == workload:
+                return d
+    return {}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed PMC summary for this workload."""
+    d = load_profile(workload)
+    return int(d["hbm_bytes_per_launch"]) if d.get("hbm_bytes_per_launch") else None
+
+
+# VALU issue model (profiles/r01_valu_rates.txt, tools/valu_rates.hip): a wave64 integer VALU instruction
+# occupies its SIMD ~2.6 (xor/or/and/add/sub/bitop3/lshr) or ~4.3 (bcnt/alignbit/mad24/max/min/cndmask...)
+# shader cycles; the uniform sweep's loop mix (tools/isa_mix.py) averages 3.66.  Peak = every SIMD issuing.
+VALU_CYCLES_PER_INST = 3.66
+SIMD_COUNT = 1024
+SHADER_CLOCK_HZ = 2.4e9
+
+
+def valu_roofline(workload: str, kernel_ms: float):
+    """Second bound next to HBM: VALU issue (the one this kernel is actually limited by)."""
+    d = load_profile(workload)
+    n = d.get("SQ_INSTS_VALU_per_launch")
+    if not n or kernel_ms <= 0:
+        return None
+    achieved = n / (kernel_ms * 1e-3)  # wave64 VALU instructions per second
+    peak = SIMD_COUNT * SHADER_CLOCK_HZ / VALU_CYCLES_PER_INST
+    return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "wave64 VALU instructions/s",
+            "frac": achieved / peak, "valu_instructions_per_launch": n,
+            "model": f"{VALU_CYCLES_PER_INST} SIMD cycles per instruction (measured mix), {SIMD_COUNT} SIMDs "
+                     f"x {SHADER_CLOCK_HZ / 1e9} GHz; instruction count from the committed PMC profile"}
     return None
 
 
@@ -78,16 +107,21 @@ def cpu_baseline(reads, a, b, budget_s: float = 10.0):
     n_fit = int(budget_s / max(per_pair, 1e-9))
     if n_fit < a.shape[0]:
         idx = np.linspace(0, a.shape[0] - 1, max(n_fit, cal)).astype(np.int64)
-        sa, sb, reps = a[idx], b[idx], 1
+        sa, sb = a[idx], b[idx]
         what = f"{idx.shape[0]} of {a.shape[0]} candidate pairs (evenly strided)"
     else:
         sa, sb = a, b
-        reps = max(1, int(n_fit // a.shape[0]))
-        what = f"all {a.shape[0]} candidate pairs x {reps} passes"
+        what = f"all {a.shape[0]} candidate pairs"
+    # whole passes until the budget is spent (at least one)
+    reps = 0
     t0 = time.perf_counter()
-    for _ in range(reps):
+    while True:
         oracle.batch_dp(reads, sa, sb, threads=threads, encoded=enc)
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
     dt = time.perf_counter() - t0
+    what += f" x {reps} passes"
     return {"value": sa.shape[0] * reps / dt, "unit": "overlap-pairs/s", "cores": threads, "kind": "port",
             "sample": f"{what} through oracle/ovl_oracle.c oracle_batch_dp (full int32 DP + int8 traceback "
                       f"per pair, as aligners.py:27-57; OpenMP {threads} threads), {dt:.1f} s"}
@@ -159,6 +193,25 @@ def timed_steps(w: Workload, steps: int, warmup: int, dev, world: int):
     return time.perf_counter() - t0, ev0.elapsed_time(ev1) / max(steps, 1)
 
 
+def candidate_timing(w: Workload, reps: int = 5):
+    """Candidate enumeration (overlapGraphs.py:30-52) for this workload: the device path
+    (ovl_candidates: keys, radix sort, lookup, scan, ordered emit; synchronous, list left
+    in HBM) vs the host restatement (candidates.enumerate_candidates, numpy)."""
+    from ovlgraph.candidates import enumerate_candidates
+    k = w.cfg["k"]
+    n = w.eng.enumerate_candidates(k)  # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        n = w.eng.enumerate_candidates(k)
+    dev_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    a, _ = enumerate_candidates(w.reads, k)
+    host_s = time.perf_counter() - t0
+    return {"k": k, "pairs": int(n), "same_count_as_host": int(n) == int(a.shape[0]),
+            "device_ms": dev_s * 1e3, "host_ms": host_s * 1e3,
+            "device_pairs_per_s": n / dev_s if dev_s > 0 else None}
+
+
 def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
     """Config 5's band-width sweep: the same resident pairs at each band (-1 = full DP).
 
@@ -188,7 +241,7 @@ def main() -> None:
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOAD_DESC))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra single-GPU configs")
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-baseline work (>= 10)")
     ap.add_argument("--indel", type=int, default=None, help="indel score (default: the reference's -2**31)")
     ap.add_argument("--band", type=int, default=-1, help="band half-width (-1 = full DP, the reference)")
     ap.add_argument("--band-sweep", default=None,
@@ -265,8 +318,11 @@ def main() -> None:
                 "kernel_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": algo,
             },
+            "valu_roofline": valu_roofline(args.config, kernel_ms),
             "host_setup_s": {"read_sim_and_enumeration": round(w.t_enum, 3), "upload_and_pack": round(w.t_pack, 4)},
         }
+        if world == 1:
+            line["candidates"] = candidate_timing(w)
         if world == 1 and args.band_sweep:
             line["band_sweep"] = band_sweep(w, [int(x) for x in args.band_sweep.split(",")], args.sweep_indel,
                                             args.sweep_steps, dev)

@@ -1,6 +1,6 @@
 """Turn a tools/gpu_profile.sh run into committed artefacts under profiles/.
 
-    python tools/make_profile_summary.py gpurun_out/<tag> <round> <config> [kernel]
+    python tools/make_profile_summary.py gpurun_out/<tag> <round> <config> [kernel] [valu-pmc-dir]
 
 Writes profiles/<round>_<config>_kernel_stats.csv (rocprofv3 --stats), and
 profiles/<round>_<config>_pmc.json with the dominant kernel's per-launch HBM
@@ -30,6 +30,7 @@ def mean_counter(path, kernel, name):
 def main():
     run, rnd, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
     kernel = sys.argv[4] if len(sys.argv) > 4 else "uniform_kernel"
+    valu_dir = sys.argv[5] if len(sys.argv) > 5 else None
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     pdir = os.path.join(root, "profiles")
     os.makedirs(pdir, exist_ok=True)
@@ -52,6 +53,16 @@ def main():
         "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md HBM, gfx950); "
                       "uncalibrated for gather loads",
     }
+    if valu_dir:
+        # SQ counters from tools/gpu_pmc.sh passes (p1, p2, ...): VALU / SALU / LDS / VMEM instructions per launch
+        for name in ("SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE", "SQ_BUSY_CYCLES", "SQ_INSTS_SALU",
+                     "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
+            vals = []
+            for d in sorted(glob.glob(os.path.join(valu_dir, "p*"))):
+                v, n = mean_counter(d, kernel, name)
+                if v is not None:
+                    vals.append(v)
+            out[name + "_per_launch"] = vals[0] if vals else None
     json.dump(out, open(os.path.join(pdir, f"{rnd}_{cfg}_pmc.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
