@@ -212,6 +212,29 @@ def candidate_timing(w: Workload, reps: int = 5):
             "device_pairs_per_s": n / dev_s if dev_s > 0 else None}
 
 
+def end_to_end(w: Workload, seed: int = 0):
+    """``construct_overlap_graph_nx_k`` for this workload, split into its stages (not the metric):
+    dedup + device enumeration + scoring with results on the host, then the DiGraph via the
+    direct builder and, for comparison, via networkx ``add_edges_from`` (the reference's way)."""
+    from ovlgraph import overlapGraphs as og
+    from ovlgraph.reads import config_reads
+    raw = config_reads(w.name, seed=seed)
+    t0 = time.perf_counter()
+    edges = og.overlap_edges_k(raw, w.cfg["k"], engine=w.eng)
+    t1 = time.perf_counter()
+    G = edges.to_digraph()
+    t2 = time.perf_counter()
+    G2 = og.assemble_graph(edges.reads, edges.counts, edges.a, edges.b, edges.score, edges.end)
+    t3 = time.perf_counter()
+    n_e = G.number_of_edges()
+    assert n_e == G2.number_of_edges()
+    del G, G2
+    return {"reads": len(raw), "pairs": len(edges), "edges": n_e,
+            "dedup_enumerate_score_s": round(t1 - t0, 4), "digraph_direct_s": round(t2 - t1, 4),
+            "digraph_networkx_s": round(t3 - t2, 4),
+            "end_to_end_s": round(t2 - t0, 4)}
+
+
 def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
     """Config 5's band-width sweep: the same resident pairs at each band (-1 = full DP).
 
@@ -323,6 +346,8 @@ def main() -> None:
         }
         if world == 1:
             line["candidates"] = candidate_timing(w)
+            if not args.no_extra:
+                line["end_to_end"] = end_to_end(w)
         if world == 1 and args.band_sweep:
             line["band_sweep"] = band_sweep(w, [int(x) for x in args.band_sweep.split(",")], args.sweep_indel,
                                             args.sweep_steps, dev)

@@ -21,6 +21,7 @@ out of scope.
 """
 from __future__ import annotations
 
+import gc
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import networkx as nx
@@ -52,7 +53,9 @@ def _node_names(distinct: Sequence[str], counts: Sequence[int]) -> List[List[str
 
 def assemble_graph(distinct: Sequence[str], counts: Sequence[int], a, b, score, end,
                    min_score: Optional[int] = None) -> nx.DiGraph:
-    """Build the DiGraph from scored candidates in reference insertion order.
+    """Build the DiGraph from scored candidates in reference insertion order, through
+    networkx's own ``add_edges_from`` (the plain statement; ``assemble_graph_direct``
+    builds the identical graph faster and is what the builders use).
 
     Nodes: every copy of every distinct read (overlapGraphs.py:25-28).
     Edges: for each pair p in order, for each copy of a, for each copy of b
@@ -108,14 +111,147 @@ def candidates_and_scores(distinct: Sequence[str], k: int, engine: Optional[Over
     return a, b, sc.tolist(), en.tolist()
 
 
-def construct_overlap_graph_nx_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
-                                 candidates: str = "auto"):
-    """Overlap graph over k-mer-filtered candidates (overlapGraphs.py:5-61)."""
+def assemble_graph_direct(distinct: Sequence[str], counts: Sequence[int], a, b, score, end,
+                          min_score: Optional[int] = None) -> nx.DiGraph:
+    """``assemble_graph`` without networkx's per-edge ``add_edge`` overhead.
+
+    Builds the DiGraph's own node / successor / predecessor dicts in bulk, in the
+    reference's insertion order (overlapGraphs.py:25-28 nodes; :55-60 edges per pair,
+    per copy of a, per copy of b), with one attribute dict per edge shared by its
+    successor and predecessor entries -- the structure ``add_edge`` builds, so every
+    networkx view (edges, successors, predecessors, data) reads identically:
+
+    * pairs x copies are expanded into edge arrays (u, v node ids) with numpy;
+    * successor dicts: edges stably sorted by u keep the global order per u;
+    * predecessor dicts: edges stably sorted by v keep the global order per v.
+    """
+    # millions of new dicts: the cyclic GC would re-traverse them at every generation-2 pass
+    # (they hold no cycles), so it is paused for the bulk build
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        return _assemble_direct(distinct, counts, a, b, score, end, min_score)
+    finally:
+        if gc_was:
+            gc.enable()
+
+
+def _assemble_direct(distinct, counts, a, b, score, end, min_score):
+    names = _node_names(distinct, counts)
+    order = [n for group in names for n in group]
+    cnt = np.fromiter((len(g) for g in names), dtype=np.int64, count=len(names))
+    first = np.zeros(len(names) + 1, dtype=np.int64)
+    np.cumsum(cnt, out=first[1:])
+    a_arr = np.asarray(a, dtype=np.int64)
+    b_arr = np.asarray(b, dtype=np.int64)
+    s_arr = np.asarray(score)
+    e_arr = np.asarray(end)
+    if min_score is not None and a_arr.shape[0]:
+        keep = s_arr > min_score
+        a_arr, b_arr, s_arr, e_arr = a_arr[keep], b_arr[keep], s_arr[keep], e_arr[keep]
+    # edges of pair p: k = 0 .. ca*cb-1 -> (copy of a = k // cb, copy of b = k % cb)
+    per = cnt[a_arr] * cnt[b_arr]
+    n_e = int(per.sum())
+    pid = np.repeat(np.arange(a_arr.shape[0], dtype=np.int64), per)
+    start = np.zeros(a_arr.shape[0], dtype=np.int64)
+    if a_arr.shape[0]:
+        np.cumsum(per[:-1], out=start[1:])
+    k = np.arange(n_e, dtype=np.int64) - start[pid]
+    cb = cnt[b_arr][pid]
+    u = first[a_arr][pid] + k // cb
+    v = first[b_arr][pid] + k % cb
+    dicts = [{"weight": sc, "end_position": en}
+             for sc, en in zip(s_arr[pid].tolist(), e_arr[pid].tolist())]
+    n_nodes = len(order)
+
+    def grouped(key, other):
+        # per node (in node order) the dict other-name -> edge dict, edges in global order
+        perm = np.argsort(key, kind="stable")
+        bounds = np.searchsorted(key[perm], np.arange(n_nodes + 1, dtype=np.int64))
+        names_sorted = [order[x] for x in other[perm].tolist()]
+        dicts_sorted = [dicts[x] for x in perm.tolist()]
+        bl = bounds.tolist()
+        return {order[n]: dict(zip(names_sorted[bl[n]:bl[n + 1]], dicts_sorted[bl[n]:bl[n + 1]]))
+                for n in range(n_nodes)}
+
+    G = nx.DiGraph()
+    G._node = {n: {} for n in order}
+    G._succ = grouped(u, v)   # descriptor: sets _adj and _succ, resets cached views
+    G._pred = grouped(v, u)
+    nx._clear_cache(G)
+    return G
+
+
+class OverlapEdges:
+    """Columnar overlap edges: the scored candidate list before networkx.
+
+    ``reads`` / ``counts`` are ``read_copies`` (overlapGraphs.py:18-20) as two lists;
+    ``a``, ``b``, ``score``, ``end`` are int32 arrays in the reference's pair order
+    (overlapGraphs.py:43-53).  Every pair stands for ``counts[a] * counts[b]`` edges
+    (one per copy pair, :55-60).  ``to_digraph()`` materialises the reference's DiGraph.
+    """
+
+    def __init__(self, reads, counts, a, b, score, end, min_score: Optional[int] = None):
+        self.reads = list(reads)
+        self.counts = list(counts)
+        self.a = np.asarray(a, dtype=np.int32)
+        self.b = np.asarray(b, dtype=np.int32)
+        self.score = np.asarray(score, dtype=np.int32)
+        self.end = np.asarray(end, dtype=np.int32)
+        self.min_score = min_score  # edges kept only when score > min_score (overlapGraphs.py:225)
+
+    def __len__(self) -> int:
+        return int(self.a.shape[0])
+
+    def read_copies(self) -> Dict[str, int]:
+        return dict(zip(self.reads, self.counts))
+
+    def node_names(self) -> List[str]:
+        return [n for group in _node_names(self.reads, self.counts) for n in group]
+
+    def kept(self) -> np.ndarray:
+        return np.ones(len(self), bool) if self.min_score is None else self.score > self.min_score
+
+    def n_edges(self) -> int:
+        c = np.asarray(self.counts, dtype=np.int64)
+        k = self.kept()
+        return int((c[self.a[k]] * c[self.b[k]]).sum()) if len(self) else 0
+
+    def edge_arrays(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        """(u, v, weight, end_position) per edge, u/v indexing ``node_names()``, in insertion order."""
+        c = np.asarray(self.counts, dtype=np.int64)
+        first = np.zeros(c.shape[0] + 1, dtype=np.int64)
+        np.cumsum(c, out=first[1:])
+        k = self.kept()
+        a, b = self.a[k].astype(np.int64), self.b[k].astype(np.int64)
+        per = c[a] * c[b]
+        pid = np.repeat(np.arange(a.shape[0], dtype=np.int64), per)
+        start = np.zeros(a.shape[0], dtype=np.int64)
+        if a.shape[0]:
+            np.cumsum(per[:-1], out=start[1:])
+        q = np.arange(pid.shape[0], dtype=np.int64) - start[pid]
+        cb = c[b][pid]
+        return (first[a][pid] + q // cb, first[b][pid] + q % cb, self.score[k][pid], self.end[k][pid])
+
+    def to_digraph(self) -> nx.DiGraph:
+        return assemble_graph_direct(self.reads, self.counts, self.a, self.b, self.score, self.end,
+                                     self.min_score)
+
+
+def overlap_edges_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
+                    candidates: str = "auto") -> OverlapEdges:
+    """Scored k-mer candidates of ``construct_overlap_graph_nx_k`` as columns (no networkx)."""
     assert k >= 0, "k-mer length must be non-negative"
     distinct, counts = dedup_reads(reads)
     a, b, sc, en = candidates_and_scores(distinct, k, engine, scorer, candidates)
-    G = assemble_graph(distinct, counts, a, b, sc, en)
-    return G, dict(zip(distinct, counts))
+    return OverlapEdges(distinct, counts, a, b, sc, en)
+
+
+def construct_overlap_graph_nx_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
+                                 candidates: str = "auto"):
+    """Overlap graph over k-mer-filtered candidates (overlapGraphs.py:5-61)."""
+    edges = overlap_edges_k(reads, k, engine, scorer, candidates)
+    return edges.to_digraph(), edges.read_copies()
 
 
 build_overlap_graph = construct_overlap_graph_nx_k
@@ -126,8 +262,8 @@ def construct_overlap_graph_string(reads, engine: Optional[OverlapEngine] = None
     """All ordered distinct pairs, edges where score > 0 (overlapGraphs.py:196-232)."""
     distinct, counts = dedup_reads(reads)
     a, b, sc, en = candidates_and_scores(distinct, 0, engine, scorer, candidates)
-    G = assemble_graph(distinct, counts, a, b, sc, en, min_score=0)
-    return G, dict(zip(distinct, counts))
+    edges = OverlapEdges(distinct, counts, a, b, sc, en, min_score=0)
+    return edges.to_digraph(), edges.read_copies()
 
 
 def construct_string_graph(reads, engine: Optional[OverlapEngine] = None, scorer=None):

@@ -114,3 +114,21 @@ def test_golden_graphs_both_candidate_paths(engine, golden_graphs, mode):
             continue
         G, copies = og.construct_overlap_graph_nx_k(rec["reads"], engine=engine, candidates=mode, **rec["kwargs"])
         assert_graph_matches_record(G, rec, copies)
+
+
+def test_cfg4_full_pipeline_vs_oracle(engine, oracle_mod):
+    """Config 4 (random 1 Mbp genome, 200k reads, ~38 M pairs): device enumeration == host
+    enumeration, and every resident candidate scored == the oracle."""
+    from ovlgraph.candidates import enumerate_candidates
+    from ovlgraph.reads import config_reads
+    distinct = _distinct(config_reads("cfg4"))
+    engine.set_reads(distinct)
+    a, b = engine.candidates(5)
+    ra, rb = enumerate_candidates(distinct, 5)
+    np.testing.assert_array_equal(a, ra)
+    np.testing.assert_array_equal(b, rb)
+    assert a.shape[0] > 30_000_000
+    sc, en = engine.score_candidates()
+    rs, re_ = oracle_mod.batch_ungapped(distinct, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
