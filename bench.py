@@ -235,6 +235,36 @@ def end_to_end(w: Workload, seed: int = 0):
             "end_to_end_s": round(t2 - t0, 4)}
 
 
+def local_alignment_timing(eng, reps: int = 5):
+    """local_alignment (aligners.py:85-167, §8f rank 3) of a 4,000-base contig against the whole PhiX
+    genome: GPU with and without the traceback walk, beside the oracle's C port on one core."""
+    import random
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from ovlgraph.reads import read_genome_from_fasta
+    genome = read_genome_from_fasta()
+    rng = random.Random(11)
+    st = rng.randint(0, len(genome) - 4000)
+    contig = "".join(rng.choice("ACGT") if rng.random() < 0.02 else ch for ch in genome[st:st + 4000])
+    eng.local_align(contig, genome)  # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = eng.local_align(contig, genome)
+    tb_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.local_align(contig, genome, traceback=False)
+    sc_s = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    exp = oracle.local_alignment(contig, genome)
+    cpu_s = time.perf_counter() - t0
+    cells = len(contig) * len(genome)
+    return {"query": len(contig), "reference": len(genome), "cells": cells, "score": res[0],
+            "matches_oracle": res[0] == exp[3] and res[2] == exp[5],
+            "gpu_ms_with_traceback": tb_s * 1e3, "gpu_ms_score_only": sc_s * 1e3,
+            "gpu_cells_per_s_score_only": cells / sc_s, "cpu_port_ms_1core": cpu_s * 1e3}
+
+
 def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
     """Config 5's band-width sweep: the same resident pairs at each band (-1 = full DP).
 
@@ -348,6 +378,7 @@ def main() -> None:
             line["candidates"] = candidate_timing(w)
             if not args.no_extra:
                 line["end_to_end"] = end_to_end(w)
+                line["local_alignment"] = local_alignment_timing(w.eng)
         if world == 1 and args.band_sweep:
             line["band_sweep"] = band_sweep(w, [int(x) for x in args.band_sweep.split(",")], args.sweep_indel,
                                             args.sweep_steps, dev)

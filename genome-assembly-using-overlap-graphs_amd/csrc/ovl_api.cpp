@@ -55,6 +55,8 @@ struct ovl_ctx {
     // device candidate enumeration (ovl_candidates): per-read keys / groups and the pair list
     DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
     int64_t cand_n = -1;  // -1: no candidate list for the resident reads
+    // local alignment (ovl_local_align): query / reference bytes, carried rows, progress, traceback
+    DevBuf l_q, l_r, l_row, l_prog, l_tb, l_best;
 };
 
 namespace {
@@ -336,7 +338,8 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->full, &c->a, &c->b, &c->score, &c->end,
                       &c->tb, &c->err_flag, &c->k_pre, &c->k_suf, &c->k_sorted, &c->k_iota, &c->k_order, &c->k_lo,
-                      &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b})
+                      &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b, &c->l_q, &c->l_r, &c->l_row,
+                      &c->l_prog, &c->l_tb, &c->l_best})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -674,5 +677,98 @@ OVL_API int ovl_score_candidates(ovl_ctx* c, int32_t match, int32_t mismatch, in
     HIPCHK(c, hipMemcpyAsync(out_score, c->score.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(out_end, c->end.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return OVL_OK;
+}
+
+// ----------------------------------------------------------------------------- local alignment
+
+OVL_API int ovl_local_align(ovl_ctx* c, const uint8_t* query, int32_t n, const uint8_t* ref, int32_t m,
+                            int32_t match, int32_t mismatch, int64_t indel, int32_t* out_score, int32_t* out_end_i,
+                            int32_t* out_end_j, int32_t* out_start_i, int32_t* out_start_j, int8_t* ops,
+                            int64_t ops_cap, int64_t* out_n_ops) {
+    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n < 0 || m < 0) return fail(c, OVL_E_ARG, "negative length");
+    if ((n > 0 && !query) || (m > 0 && !ref)) return fail(c, OVL_E_ARG, "NULL sequence");
+    if (!out_score || !out_end_i || !out_end_j || !out_start_i || !out_start_j || !out_n_ops)
+        return fail(c, OVL_E_ARG, "NULL output pointer");
+    if (ops && ops_cap < 0) return fail(c, OVL_E_ARG, "ops_cap < 0");
+    // best-cell key: 24-bit score, 20-bit row and column
+    const int64_t mn = std::min(n, m);
+    const int64_t top = std::max<int64_t>(0, match) * mn;
+    if (n > 0xFFFFF || m > 0xFFFFF || top >= (int64_t(1) << 24))
+        return fail(c, OVL_E_UNSUPPORTED, "local alignment: lengths < 2^20 and match * min(n, m) < 2^24 required");
+    *out_score = 0; *out_end_i = 0; *out_end_j = 0; *out_start_i = 0; *out_start_j = 0; *out_n_ops = 0;
+    if (n == 0 || m == 0) return OVL_OK;
+    const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
+    const int wide = (M >= (int64_t(1) << 30) || top + M >= (int64_t(1) << 31)) ? 1 : 0;
+    const int32_t n_strips = (n + 63) / 64;
+    const int64_t steps = (int64_t)m + 63;
+    const size_t tb_bytes = (size_t)n_strips * (size_t)steps * 64;
+    if (ops && tb_bytes > (size_t(8) << 30))
+        return fail(c, OVL_E_UNSUPPORTED, "local alignment traceback table would exceed 8 GiB");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    HIPCHK(c, ensure(c->l_q, (size_t)n));
+    HIPCHK(c, ensure(c->l_r, (size_t)m));
+    HIPCHK(c, ensure(c->l_row, (size_t)n_strips * ((size_t)m + 1) * sizeof(int32_t)));
+    HIPCHK(c, ensure(c->l_prog, (size_t)n_strips * sizeof(int32_t)));
+    HIPCHK(c, ensure(c->l_best, 16));
+    if (ops) HIPCHK(c, ensure(c->l_tb, tb_bytes));
+    HIPCHK(c, hipMemcpyAsync(c->l_q.p, query, (size_t)n, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->l_r.p, ref, (size_t)m, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemsetAsync(c->l_prog.p, 0, (size_t)n_strips * sizeof(int32_t), s));
+    HIPCHK(c, hipMemsetAsync(c->l_best.p, 0, 16, s));
+    HIPCHK(c, hipMemsetAsync(c->err_flag.p, 0, sizeof(uint32_t), s));
+    // strips round-robin over at most 8 one-wavefront blocks per CU: far below residency, so every
+    // strip's producer is a resident wavefront (the hand-off polls would otherwise never end)
+    const int32_t blocks = std::min<int32_t>(n_strips, c->cu_count * 8);
+    HIPCHK(c, ovl_launch_local(as<uint8_t>(c->l_q), n, as<uint8_t>(c->l_r), m, match, mismatch, indel, wide,
+                               as<int32_t>(c->l_row), as<int32_t>(c->l_prog), ops ? as<int8_t>(c->l_tb) : nullptr,
+                               as<unsigned long long>(c->l_best), as<uint32_t>(c->err_flag), blocks, s));
+    unsigned long long key = 0;
+    uint32_t flag = 0;
+    HIPCHK(c, hipMemcpyAsync(&key, c->l_best.p, sizeof(key), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&flag, c->err_flag.p, sizeof(flag), hipMemcpyDeviceToHost, s));
+    std::vector<int8_t> tb;
+    if (ops) {
+        tb.resize(tb_bytes);
+        HIPCHK(c, hipMemcpyAsync(tb.data(), c->l_tb.p, tb_bytes, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (flag) {
+        HIPCHK(c, hipMemset(c->err_flag.p, 0, sizeof(uint32_t)));
+        return fail(c, OVL_E_HIP, "local alignment: a row hand-off timed out (flag %u)", flag);
+    }
+    int32_t bi = 0, bj = 0, score = 0;
+    if (key) {
+        score = (int32_t)(key >> 40);
+        bi = (int32_t)(0xFFFFFu - (uint32_t)((key >> 20) & 0xFFFFF));
+        bj = (int32_t)(0xFFFFFu - (uint32_t)(key & 0xFFFFF));
+    }
+    *out_score = score;
+    *out_end_i = bi;
+    *out_end_j = bj;
+    int32_t i = bi, j = bj;
+    int64_t k = 0;
+    if (ops) {
+        // aligners.py:133-153: walk while i > 0, j > 0 and dp[i][j] > 0
+        while (i > 0 && j > 0) {
+            const int32_t st = (i - 1) >> 6, L = (i - 1) & 63;
+            const int8_t code = tb[((size_t)st * (size_t)steps + (size_t)(j + L - 1)) * 64 + (size_t)L];
+            if (!(code & 4)) break;
+            const int8_t op = code & 3;
+            if (op == 1) { --i; --j; }
+            else if (op == 2) { --i; }
+            else if (op == 3) { --j; }
+            else break;
+            if (k < ops_cap) ops[k] = op;
+            ++k;
+        }
+    }
+    *out_start_i = i;
+    *out_start_j = j;
+    *out_n_ops = k;
+    if (ops && k > ops_cap) return fail(c, OVL_E_RANGE, "ops_cap %lld < walk length %lld", (long long)ops_cap,
+                                        (long long)k);
     return OVL_OK;
 }

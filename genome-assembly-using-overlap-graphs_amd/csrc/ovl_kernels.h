@@ -69,3 +69,9 @@ extern "C" hipError_t ovl_cand_scan(void* temp, size_t temp_bytes, const int64_t
 extern "C" hipError_t ovl_cand_emit(const int32_t* order, const int64_t* lo, const int64_t* hi, const int64_t* offs,
                                     int32_t n_reads, int32_t all_pairs, int32_t* out_a, int32_t* out_b,
                                     hipStream_t stream);
+
+// local alignment (ovl_local.hip)
+extern "C" hipError_t ovl_launch_local(const uint8_t* q, int32_t n, const uint8_t* r, int32_t m, int64_t match,
+                                       int64_t mismatch, int64_t indel, int32_t wide, int32_t* rowbuf,
+                                       int32_t* progress, int8_t* tb, unsigned long long* best, uint32_t* err_flag,
+                                       int32_t blocks, hipStream_t stream);

@@ -49,6 +49,8 @@ SIGNATURES = {
     "ovl_candidates_copy": (ctypes.c_int, [_P, _P, _P]),
     "ovl_candidates_device": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _pi64]),
     "ovl_score_candidates": (ctypes.c_int, [_P, _i32, _i32, _i64, _i32, _P, _P]),
+    "ovl_local_align": (ctypes.c_int, [_P, _P, _i32, _P, _i32, _i32, _i32, _i64, _pi32, _pi32, _pi32, _pi32,
+                                       _pi32, _P, _i64, _pi64]),
 }
 
 

@@ -143,6 +143,28 @@ class OverlapEngine:
               self._ctx)
         return sc, en
 
+    # ---------------------------------------------------------------- local alignment
+    def local_align(self, query: str, reference: str, match: int = 10, mismatch: int = -1, indel: int = -1,
+                    traceback: bool = True):
+        """local_alignment's DP (aligners.py:105-160) on the GPU for one (possibly large) pair.
+
+        Returns (score, end_i, end_j, start_i, start_j, ops) with ops the walk's codes
+        (1 diag, 2 up, 3 left) in walk order (None without traceback).
+        """
+        buf, offs = encode_reads([query, reference])
+        n, m = len(query), len(reference)
+        qb = np.ascontiguousarray(buf[:n]) if n else np.zeros(1, np.uint8)
+        rb = np.ascontiguousarray(buf[n:n + m]) if m else np.zeros(1, np.uint8)
+        outs = [ctypes.c_int32() for _ in range(5)]
+        k = ctypes.c_int64()
+        cap = n + m + 1
+        ops = np.zeros(cap, dtype=np.int8) if traceback else None
+        check(self._L.ovl_local_align(self._ctx, _ptr(qb), n, _ptr(rb), m, int(match), int(mismatch), int(indel),
+                                      *[ctypes.byref(o) for o in outs], _ptr(ops) if traceback else None,
+                                      cap if traceback else 0, ctypes.byref(k)), self._ctx)
+        sc, ei, ej, si, sj = (o.value for o in outs)
+        return sc, ei, ej, si, sj, (ops[: k.value] if traceback else None)
+
     # ---------------------------------------------------------------- scoring
     def score(self, a_idx, b_idx, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
               band: int = -1) -> Tuple[np.ndarray, np.ndarray]:

@@ -141,6 +141,20 @@ int ovl_candidates_device(const ovl_ctx* ctx, const int32_t** d_a_idx, const int
 int ovl_score_candidates(ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
                          int32_t* out_score, int32_t* out_end);
 
+/*
+ * local_alignment (aligners.py:85-167) of query[0..n) against reference[0..m) on the whole GPU:
+ * Smith-Waterman with the reference's tie order and int64-exact arithmetic; bytes are compared
+ * for equality only.  Outputs: the best score and its cell (end_i, end_j) -- the first strict
+ * maximum in fill order; with ops != NULL also the traceback walk of aligners.py:133-153 from
+ * that cell: ops[k] in walk order (1 diag, 2 up, 3 left), *n_ops its length (OVL_E_RANGE when
+ * > ops_cap; n + m always suffices) and the cell where it stopped (start_i, start_j; start_j is
+ * the reference's start position, aligners.py:156).  Needs n, m < 2^20 and match*min(n,m) < 2^24.
+ */
+int ovl_local_align(ovl_ctx* ctx, const uint8_t* query, int32_t n, const uint8_t* reference, int32_t m,
+                    int32_t match, int32_t mismatch, int64_t indel, int32_t* out_score, int32_t* out_end_i,
+                    int32_t* out_end_j, int32_t* out_start_i, int32_t* out_start_j, int8_t* ops,
+                    int64_t ops_cap, int64_t* out_n_ops);
+
 #ifdef __cplusplus
 }
 #endif

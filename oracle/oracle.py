@@ -129,6 +129,8 @@ def lib():
         L.oracle_batch_ungapped.restype = ctypes.c_int
         L.oracle_batch_banded.argtypes = [P, P, i32, P, P, i64, i64, i64, i64, i32, P, P, i32]
         L.oracle_batch_banded.restype = ctypes.c_int
+        L.oracle_local_align.argtypes = [P, i32, P, i32, i64, i64, i64, P, P, P, P, P, P, i64, P]
+        L.oracle_local_align.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -239,6 +241,56 @@ def banded_py(s: str, t: str, match: int = 10, mismatch: int = -1, indel: int = 
         if inb(n, j) and (best is None or dp[n][j] > best):
             best, end = dp[n][j], j
     return int(best), end
+
+
+def local_strings(query: str, reference: str, bi: int, bj: int, ops) -> Tuple[str, str, str, int, int]:
+    """Rebuild aligners.py:133-160's strings from a walk: ops (1 diag, 2 up, 3 left) from (bi, bj)."""
+    aq, ar = [], []
+    i, j = bi, bj
+    for c in ops:
+        if c == 1:
+            aq.append(query[i - 1]); ar.append(reference[j - 1]); i -= 1; j -= 1
+        elif c == 2:
+            aq.append(query[i - 1]); ar.append("-"); i -= 1
+        else:
+            aq.append("-"); ar.append(reference[j - 1]); j -= 1
+    aligned_query = "".join(reversed(aq))
+    aligned_reference = "".join(reversed(ar))
+    to_print = (f"\nTarget:   {aligned_reference}\n          {'|' * len(aligned_reference)}\nQuery:    "
+                f"{aligned_query}")
+    return to_print, aligned_reference, aligned_query, i, j
+
+
+def local_alignment(query: str, reference: str, match_score: int = 10, mismatch: int = -1,
+                    indel: int = -1):
+    """aligners.py:85-167 through the C restatement: the reference's 6-tuple."""
+    buf, _ = encode([query, reference])
+    n, m = len(query), len(reference)
+    qb = np.ascontiguousarray(buf[:n]) if n else np.zeros(1, np.uint8)
+    rb = np.ascontiguousarray(buf[n:]) if m else np.zeros(1, np.uint8)
+    out = [np.zeros(1, np.int32) for _ in range(5)]
+    cap = n + m + 1
+    ops = np.zeros(cap, np.int8)
+    k = np.zeros(1, np.int64)
+    rc = lib().oracle_local_align(_ptr(qb), n, _ptr(rb), m, match_score, mismatch, indel,
+                                  *[_ptr(o) for o in out], _ptr(ops), cap, _ptr(k))
+    if rc != 0:
+        raise RuntimeError("oracle_local_align failed")
+    score, bi, bj = int(out[0][0]), int(out[1][0]), int(out[2][0])
+    to_print, a_r, a_q, _, start = local_strings(query, reference, bi, bj, ops[: int(k[0])].tolist())
+    assert start == int(out[4][0])
+    return to_print, a_r, a_q, score, start, bj
+
+
+def align_read_or_contig_to_reference(read_or_contig: str, reference_genome: str, read_length: int,
+                                      match_score: int = 10, mismatch: int = -1, indel: int = -1):
+    """aligners.py:170-202: a shorter item is aligned to the reference's tail only."""
+    L = len(read_or_contig)
+    if L < read_length:
+        tp, a_r, a_q, sc, st, en = local_alignment(read_or_contig, reference_genome[-L:],
+                                                   match_score, mismatch, indel)
+        return tp, a_r, a_q, sc, len(reference_genome) - L + st, len(reference_genome) - L + en
+    return local_alignment(read_or_contig, reference_genome, match_score, mismatch, indel)
 
 
 def dp_one(s: str, t: str, match=10, mismatch=-1, indel=INT32_MIN, want_tb=False):

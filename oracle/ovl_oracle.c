@@ -145,6 +145,62 @@ int oracle_overlap_banded(const uint8_t* s, int32_t n, const uint8_t* t, int32_t
     return 0;
 }
 
+/* local_alignment, aligners.py:85-167 (Smith-Waterman with the reference's tie order):
+ * cell = diag if diag>=up && diag>=left && diag>=0 (code 1), elif up>=left && up>=0 (2),
+ * elif left>=0 (3), else 0 (code 0); int64 arithmetic, int32 stores.  Best cell: the
+ * first strict '>' maximum in the i-major / j-minor fill order, from 0 (:128-130).
+ * Walk (:133-153) from (best_i, best_j) while i > 0 && j > 0 && dp > 0, by code; ops
+ * (nullable, up to cap entries) receives the codes in walk order; *start_j is the
+ * column where the walk stopped (start position, :156).  Returns 0 or -1 (alloc). */
+int oracle_local_align(const uint8_t* q, int32_t n, const uint8_t* r, int32_t m,
+                       int64_t match, int64_t mismatch, int64_t indel,
+                       int32_t* out_score, int32_t* out_bi, int32_t* out_bj, int32_t* out_start_i,
+                       int32_t* out_start_j, int8_t* ops, int64_t cap, int64_t* n_ops)
+{
+    const size_t W = (size_t)m + 1;
+    const size_t cells = ((size_t)n + 1) * W;
+    int32_t* dp = (int32_t*)calloc(cells, sizeof(int32_t));
+    int8_t* tb = (int8_t*)calloc(cells, 1);
+    if (!dp || !tb) { free(dp); free(tb); return -1; }
+    int64_t best = 0;
+    int32_t bi = 0, bj = 0;
+    for (int32_t i = 1; i <= n; ++i) {
+        const int32_t* prev = dp + (size_t)(i - 1) * W;
+        int32_t* cur = dp + (size_t)i * W;
+        int8_t* trow = tb + (size_t)i * W;
+        for (int32_t j = 1; j <= m; ++j) {
+            const int64_t diag = (int64_t)prev[j - 1] + (q[i - 1] == r[j - 1] ? match : mismatch);
+            const int64_t up = (int64_t)prev[j] + indel;
+            const int64_t left = (int64_t)cur[j - 1] + indel;
+            if (diag >= up && diag >= left && diag >= 0) { cur[j] = (int32_t)diag; trow[j] = 1; }
+            else if (up >= left && up >= 0)              { cur[j] = (int32_t)up;   trow[j] = 2; }
+            else if (left >= 0)                          { cur[j] = (int32_t)left; trow[j] = 3; }
+            else                                         { cur[j] = 0; }
+            if ((int64_t)cur[j] > best) { best = cur[j]; bi = i; bj = j; }
+        }
+    }
+    int32_t i = bi, j = bj;
+    int64_t k = 0;
+    while (i > 0 && j > 0 && dp[(size_t)i * W + j] > 0) {
+        const int8_t c = tb[(size_t)i * W + j];
+        if (c == 1)      { --i; --j; }
+        else if (c == 2) { --i; }
+        else if (c == 3) { --j; }
+        else break;
+        if (ops && k < cap) ops[k] = c;
+        ++k;
+    }
+    *out_score = (int32_t)best;
+    *out_bi = bi;
+    *out_bj = bj;
+    *out_start_i = i;
+    *out_start_j = j;
+    *n_ops = k;
+    free(dp);
+    free(tb);
+    return 0;
+}
+
 static int batch_common(int mode, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
                         const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
                         int64_t match, int64_t mismatch, int64_t indel, int32_t band,

@@ -89,3 +89,18 @@ def test_int32_wrap_semantics(oracle_mod):
     py = oracle_mod.overlap_alignment(s, t, big, -1, -(2 ** 40))
     c = oracle_mod.dp_one(s, t, big, -1, -(2 ** 40))
     assert (py[3], py[4]) == c
+
+
+def test_local_alignment_oracle_matches_golden(oracle_mod):
+    """oracle_local_align (C) + string rebuild == the reference's local_alignment and
+    align_read_or_contig_to_reference outputs (tests/golden/local_alignment.json)."""
+    from conftest import load_golden
+    d = load_golden("local_alignment.json")
+    for rec in d["pairs"]:
+        got = oracle_mod.local_alignment(rec["query"], rec["reference"], rec["match"], rec["mismatch"], rec["indel"])
+        assert got == (rec["to_print"], rec["aligned_reference"], rec["aligned_query"], rec["score"], rec["start"],
+                       rec["end"])
+    for rec in d["align_to_reference"]:
+        got = oracle_mod.align_read_or_contig_to_reference(rec["item"], rec["reference"], rec["read_length"])
+        assert got == (rec["to_print"], rec["aligned_reference"], rec["aligned_query"], rec["score"], rec["start"],
+                       rec["end"])
