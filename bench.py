@@ -188,9 +188,10 @@ def timed_steps(w: Workload, steps: int, warmup: int, dev, world: int):
         w.launch()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()  # this rank's own end; the caller takes the max over ranks
     if world > 1:
         dist.barrier()
-    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / max(steps, 1)
+    return t1 - t0, ev0.elapsed_time(ev1) / max(steps, 1)
 
 
 def candidate_timing(w: Workload, reps: int = 5):
@@ -289,7 +290,7 @@ def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOAD_DESC))
     ap.add_argument("--no-cpu-baseline", action="store_true")
