@@ -780,6 +780,149 @@ __global__ __launch_bounds__(64) void dp_kernel(
     }
 }
 
+// Banded knob, row form (used when 2*band+1 <= 192, lmax <= 1024 and magnitudes are small):
+// lanes own band diagonals t = j - (i - d* - band) in [0, 2*band] and the sweep walks rows.
+// diag = same lane of the previous row, up = lane t+1 of the previous row (wave_shl:1; out of the
+// band at t = 2*band), and the row's left dependency H[t] = max(C[t], H[t-1] + indel) becomes an
+// inclusive prefix maximum of C[t] - t*indel (DPP row_shr 1/2/4/8, row_bcast 15/31), segmented per
+// pair: SEG = 16, 32 or 64 lanes (4, 2 or 1 pairs per wavefront), or NC = 2/3 chunks of 64 lanes
+// carried left to right.  Same values as dp_kernel<int32_t, true> (only values matter: no traceback
+// in band mode).  Column 0 is the boundary (value 0) inside the band; j < 0 and j > m are not cells.
+constexpr int32_t kBandNeg = -(1 << 30);  // "-inf": host keeps (4*lmax + 2) * |score| < 2^29
+
+template <int SEG>
+__device__ __forceinline__ int32_t seg_scan_max(int32_t v) {
+    // inclusive prefix max inside aligned SEG-lane segments (identity kBandNeg)
+    v = max(v, __builtin_amdgcn_update_dpp(kBandNeg, v, 0x111, 0xF, 0xF, false));  // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(kBandNeg, v, 0x112, 0xF, 0xF, false));  // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(kBandNeg, v, 0x114, 0xF, 0xF, false));  // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(kBandNeg, v, 0x118, 0xF, 0xF, false));  // row_shr:8
+    if constexpr (SEG >= 32) v = max(v, __builtin_amdgcn_update_dpp(kBandNeg, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    if constexpr (SEG >= 64) v = max(v, __builtin_amdgcn_update_dpp(kBandNeg, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return v;
+}
+
+template <int SEG, int NC>
+__global__ __launch_bounds__(256) void band_row_kernel(
+    const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
+    int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
+    int32_t lcap, int32_t match, int32_t mismatch, int32_t indel, int32_t band, int32_t* __restrict__ out_score,
+    int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    constexpr int PPW = 64 / SEG;  // pairs per wavefront
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+    const int seg = lane / SEG;      // pair slot in the wavefront
+    const int t0 = lane % SEG;       // band lane inside the segment (chunk 0)
+    uint8_t* sq = smem + (size_t)(wib * PPW + seg) * 2 * lcap;  // this pair's s, then t
+    uint8_t* st = sq + lcap;
+    const int64_t n_slots = (n_pairs + PPW - 1) / PPW;
+    const int64_t wave0 = (int64_t)blockIdx.x * 4 + wib;
+    for (int64_t slot = wave0; slot < n_slots; slot += (int64_t)gridDim.x * 4) {
+        const int64_t p = slot * PPW + seg;
+        const bool mine = p < n_pairs;
+        int32_t a = mine ? a_idx[p] : 0, b = mine ? b_idx[p] : 0;
+        bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
+        if (!ok) { a = 0; b = 0; }
+        const int32_t n = ok ? len[a] : 0, m = ok ? len[b] : 0;
+        ok = ok && n <= lcap && m <= lcap;
+        if (mine && !ok && t0 == 0) {
+            atomicOr(err_flag, 1u);
+            out_score[p] = -1;
+            out_end[p] = -1;
+        }
+        const int32_t jstar = ok ? out_end[p] : 0;  // seed from the ungapped launch
+        const int32_t dstar = n - jstar;
+        // stage s and t of this pair in LDS (the segment's lanes copy them)
+        if (ok) {
+            const uint8_t* gs = codes + off[a];
+            const uint8_t* gt = codes + off[b];
+            for (int q = t0; q < n; q += SEG) sq[q] = gs[q];
+            for (int q = t0; q < m; q += SEG) st[q] = gt[q];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // rows: from r0 (first row with a cell of column >= 1 in the band) to n
+        const int32_t r0 = dstar - band + 1 > 1 ? dstar - band + 1 : 1;
+        int32_t rows = ok && n > 0 && m > 0 ? n - r0 + 1 : 0;
+        // previous row (r0 - 1) in band lanes: row 0 is all zero, otherwise only column 0 is a value
+        int32_t hp[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const int32_t t = t0 + 64 * c;
+            const int32_t j = (r0 - 1) - dstar - band + t;
+            hp[c] = (t <= 2 * band && (j == 0 || (r0 == 1 && j >= 0 && j <= m))) ? 0 : kBandNeg;
+        }
+        // segments of a wavefront run different pairs: iterate to the longest
+        int32_t rows_max = rows;
+#pragma unroll
+        for (int o = SEG; o < 64; o <<= 1) rows_max = max(rows_max, __shfl_xor(rows_max, o, 64));
+        int64_t bestkey = INT64_MIN;
+        for (int32_t k = 0; k < rows_max; ++k) {
+            const int32_t i = r0 + k;
+            const bool live = k < rows;
+            const int32_t jlo = i - dstar - band;
+            const uint32_t sc = live ? (uint32_t)sq[i - 1] : 0xFFFFu;
+            int32_t h[NC];
+            int32_t carry = kBandNeg;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int32_t t = t0 + 64 * c;
+                const int32_t j = jlo + t;
+                const bool cell = live && t <= 2 * band && j >= 1 && j <= m;
+                const uint32_t tc = cell ? (uint32_t)st[j - 1] : 0xFFFFFu;
+                // up: lane t+1 of the previous row (wave_shl:1; chunk c+1's lane 0 for lane 63)
+                int32_t upv = __builtin_amdgcn_update_dpp(kBandNeg, hp[c], 0x130, 0xF, 0xF, false);
+                if constexpr (NC > 1) {
+                    if (c + 1 < NC) {
+                        const int32_t nxt = __builtin_amdgcn_readlane(hp[c + 1 < NC ? c + 1 : c], 0);
+                        if (lane == 63) upv = nxt;
+                    }
+                }
+                const bool up_ok = t < 2 * band;
+                const int32_t dv = hp[c] + (sc == tc ? match : mismatch);
+                int32_t cv = up_ok ? max(dv, upv + indel) : dv;
+                cv = cell ? cv : ((live && j == 0 && t <= 2 * band) ? 0 : kBandNeg);
+                const int32_t tind = t * indel;
+                int32_t g = seg_scan_max<SEG>(cv - tind);
+                if constexpr (NC > 1) {
+                    g = max(g, carry);
+                    carry = __builtin_amdgcn_readlane(g, 63);
+                }
+                int32_t hv = g + tind;
+                hv = (cell || (live && j == 0 && t <= 2 * band)) ? hv : kBandNeg;
+                h[c] = hv;
+                if (live && i == n && t <= 2 * band && j >= 0 && j <= m) {
+                    // last row: strict '>' first argmax = max value, then smallest j
+                    const int64_t key = (int64_t)hv * 2048 + (2047 - j);
+                    bestkey = key > bestkey ? key : bestkey;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NC; ++c) hp[c] = h[c];
+        }
+        // reduce the segment's keys
+#pragma unroll
+        for (int o = 1; o < SEG; o <<= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)bestkey, o, 64);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)bestkey >> 32), o, 64);
+            const int64_t ok2 = (int64_t)(((uint64_t)hi << 32) | lo);
+            bestkey = ok2 > bestkey ? ok2 : bestkey;
+        }
+        if (mine && ok && t0 == 0) {
+            int32_t sc_out = 0, en_out = 0;
+            if (n > 0 && m > 0 && bestkey != INT64_MIN) {
+                // floor division of the packed key (value may be negative)
+                const int64_t v = bestkey >= 0 ? bestkey / 2048 : -((-bestkey + 2047) / 2048);
+                sc_out = (int32_t)v;
+                en_out = 2047 - (int32_t)(bestkey - v * 2048);
+            }
+            out_score[p] = sc_out;
+            out_end[p] = en_out;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // LDS reuse by the next slot
+    }
+}
+
 }  // namespace ovl
 
 // ----------------------------------------------------------------------------- launchers
@@ -902,6 +1045,18 @@ static void launch_dp_t(const OvlDpArgs* g, unsigned blocks, size_t lds, hipStre
                                                          g->band, g->out_score, g->out_end, g->tb, g->err_flag);
 }
 
+template <int SEG, int NC>
+static void launch_band_row_t(const OvlDpArgs* g, hipStream_t stream) {
+    constexpr int PPW = 64 / SEG;
+    const int64_t slots = (g->n_pairs + PPW - 1) / PPW;
+    int64_t blocks = (slots + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    const size_t lds = (size_t)4 * PPW * 2 * g->mcap;
+    band_row_kernel<SEG, NC><<<(unsigned)blocks, 256, lds, stream>>>(
+        g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, (int32_t)g->match,
+        (int32_t)g->mismatch, (int32_t)g->indel, g->band, g->out_score, g->out_end, g->err_flag);
+}
+
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     int64_t blocks = g->n_pairs;
@@ -911,6 +1066,15 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
     if (g->band >= 0) {
         // banded mode runs only where values fit int32 (the host checks) and never writes tb
         if (g->wide || g->tb) return hipErrorInvalidValue;
+        const int lanes = 2 * g->band + 1;
+        if (g->band_rows && lanes <= 192) {
+            if (lanes <= 16) launch_band_row_t<16, 1>(g, stream);
+            else if (lanes <= 32) launch_band_row_t<32, 1>(g, stream);
+            else if (lanes <= 64) launch_band_row_t<64, 1>(g, stream);
+            else if (lanes <= 128) launch_band_row_t<64, 2>(g, stream);
+            else launch_band_row_t<64, 3>(g, stream);
+            return hipGetLastError();
+        }
         launch_dp_t<int32_t, true>(g, nb, lds, stream);
     } else if (g->wide) {
         launch_dp_t<int64_t, false>(g, nb, lds, stream);

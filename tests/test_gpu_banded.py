@@ -97,3 +97,23 @@ def test_banded_unsupported_magnitudes(engine):
     engine.set_reads(["ACGTACGT", "CGTACGTA"])
     with pytest.raises(OvlError, match="OVL_E_UNSUPPORTED"):
         engine.score([0], [1], 2 ** 28, -1, -1, 4)
+
+
+@pytest.mark.parametrize("band", [0, 3, 8, 31, 63, 64, 95, 96])
+def test_strip_and_row_forms_agree_with_oracle(oracle_mod, reads_pairs, band):
+    """The band knob has two kernels (row form by default, strip form for wide bands / long reads /
+    large magnitudes); OVL_BAND_STRIP=1 forces the strip form: both must equal the oracle."""
+    import os
+    from ovlgraph import OverlapEngine
+    reads, a, b = reads_pairs
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
+    for strip in ("0", "1"):
+        os.environ["OVL_BAND_STRIP"] = strip
+        try:
+            with OverlapEngine(0) as eng:
+                eng.set_reads(reads)
+                sc, en = eng.score(a, b, 10, -1, -2, band)
+        finally:
+            del os.environ["OVL_BAND_STRIP"]
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
