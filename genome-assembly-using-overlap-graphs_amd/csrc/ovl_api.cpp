@@ -57,7 +57,8 @@ struct ovl_ctx {
     DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
     int64_t cand_n = -1;  // -1: no candidate list for the resident reads
     // local alignment (ovl_local_align): query / reference bytes, carried rows, progress, traceback
-    DevBuf l_q, l_r, l_row, l_prog, l_tb, l_best;
+    DevBuf l_q, l_r, l_row, l_tb, l_best;
+    uint32_t l_epoch = 0;  // tags this launch's row hand-off words (l_row is zeroed when allocated)
 };
 
 namespace {
@@ -349,7 +350,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->full, &c->a, &c->b, &c->score, &c->end,
                       &c->tb, &c->err_flag, &c->k_pre, &c->k_suf, &c->k_sorted, &c->k_iota, &c->k_order, &c->k_lo,
                       &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b, &c->l_q, &c->l_r, &c->l_row,
-                      &c->l_prog, &c->l_tb, &c->l_best})
+                      &c->l_tb, &c->l_best})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -712,29 +713,38 @@ OVL_API int ovl_local_align(ovl_ctx* c, const uint8_t* query, int32_t n, const u
     const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
     const int wide = (M >= (int64_t(1) << 30) || top + M >= (int64_t(1) << 31)) ? 1 : 0;
     const int32_t n_strips = (n + 63) / 64;
-    const int64_t steps = (int64_t)m + 63;
+    const int64_t n_chunks = ((int64_t)m + 126) / 64;  // 64-step chunks covering tau = 0 .. m + 62
+    const int64_t steps = n_chunks * 64;                // traceback pitch per strip
     const size_t tb_bytes = (size_t)n_strips * (size_t)steps * 64;
+    const size_t row_bytes = (size_t)n_strips * (size_t)(steps + 64) * sizeof(uint64_t);
     if (ops && tb_bytes > (size_t(8) << 30))
         return fail(c, OVL_E_UNSUPPORTED, "local alignment traceback table would exceed 8 GiB");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t s = c->stream;
     HIPCHK(c, ensure(c->l_q, (size_t)n));
     HIPCHK(c, ensure(c->l_r, (size_t)m));
-    HIPCHK(c, ensure(c->l_row, (size_t)n_strips * ((size_t)m + 1) * sizeof(int32_t)));
-    HIPCHK(c, ensure(c->l_prog, (size_t)n_strips * sizeof(int32_t)));
+    if (c->l_row.bytes < row_bytes) {
+        // fresh words must not carry a live epoch: zero on (re)allocation, epochs start at 1
+        HIPCHK(c, ensure(c->l_row, row_bytes));
+        HIPCHK(c, hipMemsetAsync(c->l_row.p, 0, c->l_row.bytes, s));
+        c->l_epoch = 0;
+    }
+    if (++c->l_epoch == 0) {  // 2^32 launches: start over from zeroed words
+        HIPCHK(c, hipMemsetAsync(c->l_row.p, 0, c->l_row.bytes, s));
+        c->l_epoch = 1;
+    }
     HIPCHK(c, ensure(c->l_best, 16));
     if (ops) HIPCHK(c, ensure(c->l_tb, tb_bytes));
     HIPCHK(c, hipMemcpyAsync(c->l_q.p, query, (size_t)n, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->l_r.p, ref, (size_t)m, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemsetAsync(c->l_prog.p, 0, (size_t)n_strips * sizeof(int32_t), s));
     HIPCHK(c, hipMemsetAsync(c->l_best.p, 0, 16, s));
     HIPCHK(c, hipMemsetAsync(c->err_flag.p, 0, sizeof(uint32_t), s));
     // strips round-robin over at most 8 one-wavefront blocks per CU: far below residency, so every
     // strip's producer is a resident wavefront (the hand-off polls would otherwise never end)
     const int32_t blocks = std::min<int32_t>(n_strips, c->cu_count * 8);
     HIPCHK(c, ovl_launch_local(as<uint8_t>(c->l_q), n, as<uint8_t>(c->l_r), m, match, mismatch, indel, wide,
-                               as<int32_t>(c->l_row), as<int32_t>(c->l_prog), ops ? as<int8_t>(c->l_tb) : nullptr,
-                               as<unsigned long long>(c->l_best), as<uint32_t>(c->err_flag), blocks, s));
+                               as<uint64_t>(c->l_row), ops ? as<int8_t>(c->l_tb) : nullptr,
+                               as<unsigned long long>(c->l_best), as<uint32_t>(c->err_flag), blocks, c->l_epoch, s));
     unsigned long long key = 0;
     uint32_t flag = 0;
     HIPCHK(c, hipMemcpyAsync(&key, c->l_best.p, sizeof(key), hipMemcpyDeviceToHost, s));

@@ -72,7 +72,9 @@ extern "C" hipError_t ovl_cand_emit(const int32_t* order, const int64_t* lo, con
                                     hipStream_t stream);
 
 // local alignment (ovl_local.hip)
+// rowbuf: n_strips x (64 * n_chunks + 64) words {value, epoch}, n_chunks = (m + 126) / 64; tb (nullable):
+// n_strips x 64 * n_chunks x 64 bytes, [strip][tau][lane]
 extern "C" hipError_t ovl_launch_local(const uint8_t* q, int32_t n, const uint8_t* r, int32_t m, int64_t match,
-                                       int64_t mismatch, int64_t indel, int32_t wide, int32_t* rowbuf,
-                                       int32_t* progress, int8_t* tb, unsigned long long* best, uint32_t* err_flag,
-                                       int32_t blocks, hipStream_t stream);
+                                       int64_t mismatch, int64_t indel, int32_t wide, uint64_t* rowbuf, int8_t* tb,
+                                       unsigned long long* best, uint32_t* err_flag, int32_t blocks, uint32_t epoch,
+                                       hipStream_t stream);
