@@ -41,6 +41,7 @@ struct ovl_ctx {
     int32_t cu_count = 256;
     int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
     int32_t band_rows_ok = 1;     // OVL_BAND_STRIP=1 env: force the strip form of the band knob (tests)
+    int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
     int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
                                   // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
     // resident reads
@@ -268,6 +269,7 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         g.err_flag = as<uint32_t>(c->err_flag);
         g.wide = pl.wide ? 1 : 0;
         g.band = pl.kernel == OVL_KERNEL_BANDED ? pl.band : -1;
+        g.classic = c->dp_classic;
         if (g.band >= 0) {
             // row form: band lanes <= 192, LDS-staged reads <= 1024, and a "-inf" that stays below
             // every value (|values| <= (2*lmax + 1) * M and the scan adds up to 2*band*|indel|)
@@ -324,6 +326,7 @@ OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
         if (v >= 0 && v <= 2) c->split_override = v;
     }
     if (const char* e = getenv("OVL_BAND_STRIP")) c->band_rows_ok = atoi(e) ? 0 : 1;
+    if (const char* e = getenv("OVL_DP_CLASSIC")) c->dp_classic = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 1024) c->blocks_per_cu = v;

@@ -44,6 +44,7 @@ struct OvlDpArgs {
     int32_t wide;        // int64 arithmetic (else int32, when magnitudes allow)
     int32_t band;        // < 0: full DP; >= 0: banded around the seed diagonal n - out_end[pair]
     int32_t band_rows;   // banded: use the row form (lanes on band diagonals) -- host checks its limits
+    int32_t classic;     // full DP without traceback: use dp_kernel instead of dp_fast_kernel (tests)
 };
 
 extern "C" hipError_t ovl_launch_map_codes(const uint8_t* raw, const uint8_t* lut, uint8_t* codes, int64_t n,

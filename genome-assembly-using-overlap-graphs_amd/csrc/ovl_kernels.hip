@@ -780,6 +780,142 @@ __global__ __launch_bounds__(64) void dp_kernel(
     }
 }
 
+// Full DP, scores only (no traceback, no band): the scoring path for gapped parameters.
+// Same strips and anti-diagonals as dp_kernel, restructured for issue: 64-step chunks with the step
+// loop unrolled at compile time and branch-free; lane 0's inputs (the previous strip's last row and
+// t) come from one LDS read per chunk and readlane per step; lane 63's values for the next strip are
+// staged with v_writelane (inline-constant lane) and written once per chunk.  A cell's value is
+// max(diag, up, left) whatever the tie order (aligners.py:40-48 keeps the maximum), and the int32
+// store wraps like the reference's table.
+template <int L>
+__device__ __forceinline__ int32_t writelane_c(int32_t vec, int32_t s) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(vec) : "s"(s), "n"(L));
+    return vec;
+}
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void unroll_steps(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        unroll_steps<B + 1, E>(f);
+    }
+}
+
+template <typename Acc>
+__global__ __launch_bounds__(64) void dp_fast_kernel(
+    const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
+    int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx,
+    int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel,
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // rows hold columns 0 .. 64*nch + 64 (hand-off chunks of 64 columns); t codes padded likewise
+    const int32_t pitch = ((mcap + 126) / 64) * 64 + 64;
+    int32_t* row0 = reinterpret_cast<int32_t*>(smem);
+    int32_t* row1 = row0 + pitch;
+    uint8_t* tcodes = reinterpret_cast<uint8_t*>(row1 + pitch);
+    const int lane = threadIdx.x;
+    for (int64_t pair = blockIdx.x; pair < n_pairs; pair += gridDim.x) {
+        const int32_t a = a_idx[pair];
+        const int32_t b = b_idx[pair];
+        if (a < 0 || a >= n_reads || b < 0 || b >= n_reads || len[b] > mcap) {
+            if (lane == 0) {
+                atomicOr(err_flag, 1u);
+                out_score[pair] = -1;
+                out_end[pair] = -1;
+            }
+            continue;
+        }
+        const int32_t n = len[a];
+        const int32_t m = len[b];
+        const uint8_t* s = codes + off[a];
+        const uint8_t* t = codes + off[b];
+        const int32_t nch = (m + 126) / 64;  // chunks covering tau = 0 .. m + 62
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // previous pair's LDS readers are done
+        for (int j = lane; j < pitch; j += 64) row0[j] = 0;
+        for (int j = lane; j < 64 * nch; j += 64) tcodes[j] = j < m ? t[j] : 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        int32_t* rin = row0;
+        int32_t* rout = row1;
+        int32_t best = 0, bend = 0;  // tracked by the lane that owns row n; dp[n][0] = 0 is the j = 0 candidate
+        const int nstrips = (n + 63) >> 6;
+        for (int st = 0; st < nstrips; ++st) {
+            const int32_t i = 64 * st + 1 + lane;
+            const bool last_row = i == n;
+            // rows past n (last strip only) compute unread values: no row mask is needed
+            const uint32_t sc = i <= n ? (uint32_t)s[i - 1] : 0xFFFFFFFFu;
+            const bool last = st + 1 == nstrips;  // last strip: track row n; else carry the last row
+            int32_t cur = 0, uprev = 0, tch = 0;
+            int32_t out_a = 0, out_b = 0;
+            // one chunk of 64 steps; EDGE: chunk 0 (lanes still left of column 1 keep dp[i][0] = 0);
+            // LAST: best tracking of row n (cells up to column m) instead of the carry staging.
+            // Columns past m compute values nobody reads.
+            auto chunk = [&](int32_t c, auto edge_tag, auto last_tag) {
+                constexpr bool EDGE = decltype(edge_tag)::value;
+                constexpr bool LAST = decltype(last_tag)::value;
+                int32_t v_rin = rin[64 * c + 1 + lane];        // lane u: dp[64 st][64c+1+u]
+                int32_t v_t = (int32_t)tcodes[64 * c + lane];  // lane u: t[64c+u]
+                // the column as a running register: per-step lane masks built from constants would be
+                // hoisted as 64 loop invariants (SGPR pairs spilled to VGPR lanes)
+                int32_t jv = 64 * c - lane + 1;
+                unroll_steps<0, 64>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    const int32_t j = jv;
+                    // lane 0 takes its inputs from the chunk registers' lane 0, then they rotate down
+                    const int32_t upin = __builtin_amdgcn_update_dpp(v_rin, cur, 0x138, 0xF, 0xF, false);
+                    const int32_t tin = __builtin_amdgcn_update_dpp(v_t, tch, 0x138, 0xF, 0xF, false);
+                    v_rin = __builtin_amdgcn_mov_dpp(v_rin, 0x130, 0xF, 0xF, true);  // wave_shl:1, lane 63 <- 0
+                    v_t = __builtin_amdgcn_mov_dpp(v_t, 0x130, 0xF, 0xF, true);
+                    const Acc diag = (Acc)uprev + ((uint32_t)tin == sc ? (Acc)match : (Acc)mismatch);
+                    const Acc up = (Acc)upin + (Acc)indel;
+                    const Acc left = (Acc)cur + (Acc)indel;
+                    const Acc mx = diag > up ? diag : up;
+                    const int32_t nv = (int32_t)(mx > left ? mx : left);
+                    if constexpr (EDGE) cur = j >= 1 ? nv : cur;
+                    else cur = nv;
+                    if constexpr (LAST) {
+                        const bool better = last_row && j >= 1 && j <= m && nv > best;
+                        best = better ? nv : best;
+                        bend = better ? j : bend;
+                    } else {
+                        const int32_t v63 = __builtin_amdgcn_readlane(cur, 63);
+                        if constexpr (u <= 62) out_a = writelane_c<u + 1>(out_a, v63);
+                        else out_b = writelane_c<0>(out_b, v63);
+                    }
+                    uprev = upin;
+                    tch = tin;
+                    jv += 1;
+                    asm volatile("" : "+v"(jv), "+v"(v_rin), "+v"(v_t));
+                });
+                if constexpr (!LAST) {
+                    if (c >= 1) rout[64 * (c - 1) + 1 + lane] = out_a;  // columns 64(c-1)+1 .. 64c
+                    out_a = out_b;
+                }
+            };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            if (last) {
+                chunk(0, T_{}, T_{});
+                for (int32_t c = 1; c < nch; ++c) chunk(c, F_{}, T_{});
+            } else {
+                chunk(0, T_{}, F_{});
+                for (int32_t c = 1; c < nch; ++c) chunk(c, F_{}, F_{});
+                rout[64 * (nch - 1) + 1 + lane] = out_a;
+                if (lane == 0) rout[0] = 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            int32_t* tmp = rin; rin = rout; rout = tmp;
+        }
+        // row n lives in lane (n-1) % 64 of the last strip
+        const int owner = (n - 1) & 63;
+        const int32_t bs = __shfl(best, owner, 64);
+        const int32_t be = __shfl(bend, owner, 64);
+        if (lane == 0) {
+            out_score[pair] = n > 0 && m > 0 ? bs : 0;
+            out_end[pair] = n > 0 && m > 0 ? be : 0;
+        }
+    }
+}
+
 // Banded knob, row form (used when 2*band+1 <= 192, lmax <= 1024 and magnitudes are small):
 // lanes own band diagonals t = j - (i - d* - band) in [0, 2*band] and the sweep walks rows.
 // diag = same lane of the previous row, up = lane t+1 of the previous row (wave_shl:1; out of the
@@ -1076,6 +1212,18 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
             return hipGetLastError();
         }
         launch_dp_t<int32_t, true>(g, nb, lds, stream);
+    } else if (!g->tb && !g->classic) {
+        // scores only: the chunked kernel (LDS: two padded rows + padded t)
+        const int32_t pitch = ((g->mcap + 126) / 64) * 64 + 64;
+        const size_t lds2 = (size_t)2 * pitch * sizeof(int32_t) + (size_t)pitch;
+        if (g->wide)
+            dp_fast_kernel<int64_t><<<nb, 64, lds2, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
+                                                              g->n_pairs, g->mcap, g->match, g->mismatch, g->indel,
+                                                              g->out_score, g->out_end, g->err_flag);
+        else
+            dp_fast_kernel<int32_t><<<nb, 64, lds2, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
+                                                              g->n_pairs, g->mcap, g->match, g->mismatch, g->indel,
+                                                              g->out_score, g->out_end, g->err_flag);
     } else if (g->wide) {
         launch_dp_t<int64_t, false>(g, nb, lds, stream);
     } else {

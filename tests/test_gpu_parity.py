@@ -362,3 +362,29 @@ def test_split_knob_equivalence(oracle_mod):
             del os.environ["OVL_SPLIT"]
         np.testing.assert_array_equal(sc, rs)
         np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (2 ** 28, -(2 ** 28), -(2 ** 27))])
+def test_dp_fast_and_classic_agree_with_oracle(oracle_mod, params):
+    """Scores-only full DP runs dp_fast_kernel (chunked, unrolled); OVL_DP_CLASSIC=1 forces dp_kernel.
+    Lengths cross 64-row strips and 64-column chunks on both axes; the last set wraps int32 stores."""
+    import os
+    from ovlgraph import OverlapEngine
+    rng = random.Random(sum(abs(x) for x in params) % 1000 + 5)
+    lens = [1, 2, 62, 63, 64, 65, 127, 128, 129, 191, 200, 257, 300]
+    reads = [_rand(rng, rng.choice(lens)) for _ in range(120)] + [_rand(rng, rng.randint(1, 320)) for _ in range(80)]
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(900)], dtype=np.int32)
+    b = np.array([rng.randrange(n) for _ in range(900)], dtype=np.int32)
+    rs, re_ = oracle_mod.batch_dp(reads, a, b, *params)
+    for classic in ("0", "1"):
+        os.environ["OVL_DP_CLASSIC"] = classic
+        try:
+            with OverlapEngine(0) as eng:
+                eng.set_reads(reads)
+                assert eng.plan(*params) == "dp"
+                sc, en = eng.score(a, b, *params)
+        finally:
+            del os.environ["OVL_DP_CLASSIC"]
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
