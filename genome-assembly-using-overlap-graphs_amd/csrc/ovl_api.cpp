@@ -40,7 +40,7 @@ struct ovl_ctx {
     std::string err;
     int32_t cu_count = 256;
     int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
-    int32_t band_rows_ok = 1;     // OVL_BAND_STRIP=1 env: force the strip form of the band knob (tests)
+    int32_t band_form = -1;       // OVL_BAND_FORM env (diag|rows|fast|strip): band knob kernel (tests)
     int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
     int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
                                   // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
@@ -271,12 +271,20 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         g.band = pl.kernel == OVL_KERNEL_BANDED ? pl.band : -1;
         g.classic = c->dp_classic;
         if (g.band >= 0) {
-            // row form: band lanes <= 192, LDS-staged reads <= 1024, and a "-inf" that stays below
-            // every value (|values| <= (2*lmax + 1) * M and the scan adds up to 2*band*|indel|)
+            // "-inf" (kBandNeg) must stay below every value: |values| <= (2*lmax + 1) * M and the row
+            // form's scan adds up to 2*band*|indel|
             const int64_t Mx = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
             const int64_t L = std::max<int32_t>(c->lmax, 1);
-            g.band_rows = (c->band_rows_ok && 2 * (int64_t)g.band + 1 <= 192 && c->lmax <= 1024 &&
-                           (4 * L + 2) * Mx < (int64_t(1) << 29)) ? 1 : 0;
+            const bool neg_ok = (4 * L + 2) * Mx < (int64_t(1) << 29);
+            const int64_t lanes = 2 * (int64_t)g.band + 1;
+            const bool diag_ok = neg_ok && ovl_band_diag_slots(g.band, c->lmax, nullptr) > 0;
+            const bool rows_ok = neg_ok && lanes <= 192 && c->lmax <= 1024;
+            switch (c->band_form) {
+                case OVL_BAND_FORM_ROWS: g.band_form = rows_ok ? OVL_BAND_FORM_ROWS : OVL_BAND_FORM_STRIP; break;
+                case OVL_BAND_FORM_FAST: g.band_form = OVL_BAND_FORM_FAST; break;
+                case OVL_BAND_FORM_STRIP: g.band_form = OVL_BAND_FORM_STRIP; break;
+                default: g.band_form = diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST; break;
+            }
         }
         HIPCHK(c, ovl_launch_dp(&g, s));
     }
@@ -325,7 +333,12 @@ OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
         const int v = atoi(sp);
         if (v >= 0 && v <= 2) c->split_override = v;
     }
-    if (const char* e = getenv("OVL_BAND_STRIP")) c->band_rows_ok = atoi(e) ? 0 : 1;
+    if (const char* e = getenv("OVL_BAND_FORM")) {
+        if (!strcmp(e, "diag")) c->band_form = OVL_BAND_FORM_DIAG;
+        else if (!strcmp(e, "rows")) c->band_form = OVL_BAND_FORM_ROWS;
+        else if (!strcmp(e, "fast")) c->band_form = OVL_BAND_FORM_FAST;
+        else if (!strcmp(e, "strip")) c->band_form = OVL_BAND_FORM_STRIP;
+    }
     if (const char* e = getenv("OVL_DP_CLASSIC")) c->dp_classic = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
         const int v = atoi(e);

@@ -25,6 +25,14 @@ struct OvlUngappedArgs {
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
 };
 
+// kernels of the band knob (ovl_launch_dp); OVL_BAND_FORM env picks one for tests
+enum {
+    OVL_BAND_FORM_STRIP = 0,  // dp_kernel<int32_t, true>: any length, one row per lane, masks per cell
+    OVL_BAND_FORM_ROWS = 1,   // band_row_kernel: lanes on band diagonals, a row per step (<= 192 lanes)
+    OVL_BAND_FORM_FAST = 2,   // dp_fast_kernel<int32_t, true>: chunked strips with band masks
+    OVL_BAND_FORM_DIAG = 3,   // band_diag_kernel: lanes on band diagonals, an anti-diagonal per step
+};
+
 struct OvlDpArgs {
     const uint8_t* codes;
     const int64_t* off;
@@ -43,7 +51,7 @@ struct OvlDpArgs {
     uint32_t* err_flag;
     int32_t wide;        // int64 arithmetic (else int32, when magnitudes allow)
     int32_t band;        // < 0: full DP; >= 0: banded around the seed diagonal n - out_end[pair]
-    int32_t band_rows;   // banded: use the row form (lanes on band diagonals) -- host checks its limits
+    int32_t band_form;   // banded: OVL_BAND_FORM_* -- the host checks each form's limits
     int32_t classic;     // full DP without traceback: use dp_kernel instead of dp_fast_kernel (tests)
 };
 
@@ -55,6 +63,7 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream_t stream);
 
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);
+extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out);
 
 // candidate enumeration (ovl_candidates.hip)
 extern "C" hipError_t ovl_cand_keys(const uint8_t* codes, const int64_t* off, const int32_t* len, int32_t n_reads,

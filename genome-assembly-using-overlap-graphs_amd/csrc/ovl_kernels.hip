@@ -801,11 +801,11 @@ __device__ __forceinline__ void unroll_steps(F&& f) {
     }
 }
 
-template <typename Acc>
+template <typename Acc, bool BANDED>
 __global__ __launch_bounds__(64) void dp_fast_kernel(
     const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx,
-    int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel,
+    int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel, int32_t band,
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // rows hold columns 0 .. 64*nch + 64 (hand-off chunks of 64 columns); t codes padded likewise
@@ -830,25 +830,49 @@ __global__ __launch_bounds__(64) void dp_fast_kernel(
         const uint8_t* s = codes + off[a];
         const uint8_t* t = codes + off[b];
         const int32_t nch = (m + 126) / 64;  // chunks covering tau = 0 .. m + 62
+        // band: seed diagonal d* (out_end holds the ungapped seed end j*) and the first row with
+        // a band cell of column >= 1; the band of row i is columns [i - d* - W, i - d* + W]
+        const int32_t W = BANDED ? band : 0;
+        const int32_t dstar = BANDED ? n - out_end[pair] : 0;
+        const int32_t rlo = BANDED ? (dstar - W + 1 > 1 ? dstar - W + 1 : 1) : 1;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // previous pair's LDS readers are done
         for (int j = lane; j < pitch; j += 64) row0[j] = 0;
         for (int j = lane; j < 64 * nch; j += 64) tcodes[j] = j < m ? t[j] : 0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         int32_t* rin = row0;
         int32_t* rout = row1;
-        int32_t best = 0, bend = 0;  // tracked by the lane that owns row n; dp[n][0] = 0 is the j = 0 candidate
+        // tracked by the lane that owns row n; dp[n][0] = 0 is the j = 0 candidate when in the band
+        int32_t best = (!BANDED || n - dstar - W <= 0) ? 0 : INT32_MIN, bend = 0;
         const int nstrips = (n + 63) >> 6;
-        for (int st = 0; st < nstrips; ++st) {
+        const int st0 = BANDED ? (rlo - 1) >> 6 : 0;
+        for (int st = st0; st < nstrips; ++st) {
             const int32_t i = 64 * st + 1 + lane;
             const bool last_row = i == n;
             // rows past n (last strip only) compute unread values: no row mask is needed
             const uint32_t sc = i <= n ? (uint32_t)s[i - 1] : 0xFFFFFFFFu;
             const bool last = st + 1 == nstrips;  // last strip: track row n; else carry the last row
+            const int32_t jlo = i - dstar - W, jhi = i - dstar + W;  // this lane's band (BANDED)
+            // chunks whose steps meet the band (all chunks when not banded)
+            int32_t c_lo = 0, c_hi = nch - 1;
+            if constexpr (BANDED) {
+                const int lmax = (n - 64 * st - 1) < 63 ? (n - 64 * st - 1) : 63;
+                const int32_t tlo = 64 * st - dstar - W;                 // lane 0's first band step
+                const int32_t thi = 64 * st + 2 * lmax - dstar + W;      // last lane's last band step
+                c_lo = tlo > 0 ? tlo / 64 : 0;
+                c_hi = thi / 64 < nch - 1 ? thi / 64 : nch - 1;
+                if (c_hi < c_lo) c_hi = c_lo;
+            }
+            // state entering chunk c_lo: lane L used t[64 c_lo - 1 - L] at the step before, lane 0's
+            // diagonal is dp[64 st][64 c_lo]; other lanes' carried values only meet masked cells
             int32_t cur = 0, uprev = 0, tch = 0;
+            if (BANDED && c_lo > 0) {
+                const int32_t tp = 64 * c_lo - 1 - lane;
+                tch = tp >= 0 && tp < m ? (int32_t)tcodes[tp] : 0;
+                uprev = lane == 0 ? rin[64 * c_lo] : 0;
+            }
             int32_t out_a = 0, out_b = 0;
             // one chunk of 64 steps; EDGE: chunk 0 (lanes still left of column 1 keep dp[i][0] = 0);
-            // LAST: best tracking of row n (cells up to column m) instead of the carry staging.
-            // Columns past m compute values nobody reads.
+            // LAST: best tracking of row n instead of the carry staging.
             auto chunk = [&](int32_t c, auto edge_tag, auto last_tag) {
                 constexpr bool EDGE = decltype(edge_tag)::value;
                 constexpr bool LAST = decltype(last_tag)::value;
@@ -866,14 +890,22 @@ __global__ __launch_bounds__(64) void dp_fast_kernel(
                     v_rin = __builtin_amdgcn_mov_dpp(v_rin, 0x130, 0xF, 0xF, true);  // wave_shl:1, lane 63 <- 0
                     v_t = __builtin_amdgcn_mov_dpp(v_t, 0x130, 0xF, 0xF, true);
                     const Acc diag = (Acc)uprev + ((uint32_t)tin == sc ? (Acc)match : (Acc)mismatch);
-                    const Acc up = (Acc)upin + (Acc)indel;
-                    const Acc left = (Acc)cur + (Acc)indel;
+                    Acc up = (Acc)upin + (Acc)indel;
+                    Acc left = (Acc)cur + (Acc)indel;
+                    if constexpr (BANDED) {
+                        // out-of-band predecessors: "up" leaves the band only at the row's last band
+                        // cell, "left" only at its first; diag is always in the band, so substituting
+                        // it leaves the maximum exact
+                        up = j != jhi ? up : diag;
+                        left = j != jlo ? left : diag;
+                    }
                     const Acc mx = diag > up ? diag : up;
                     const int32_t nv = (int32_t)(mx > left ? mx : left);
                     if constexpr (EDGE) cur = j >= 1 ? nv : cur;
                     else cur = nv;
                     if constexpr (LAST) {
-                        const bool better = last_row && j >= 1 && j <= m && nv > best;
+                        bool better = last_row && j >= 1 && j <= m && nv > best;
+                        if constexpr (BANDED) better = better && j >= jlo && j <= jhi;
                         best = better ? nv : best;
                         bend = better ? j : bend;
                     } else {
@@ -894,12 +926,12 @@ __global__ __launch_bounds__(64) void dp_fast_kernel(
             using T_ = std::true_type;
             using F_ = std::false_type;
             if (last) {
-                chunk(0, T_{}, T_{});
-                for (int32_t c = 1; c < nch; ++c) chunk(c, F_{}, T_{});
+                if (c_lo == 0) chunk(0, T_{}, T_{});
+                for (int32_t c = c_lo > 1 ? c_lo : 1; c <= c_hi; ++c) chunk(c, F_{}, T_{});
             } else {
-                chunk(0, T_{}, F_{});
-                for (int32_t c = 1; c < nch; ++c) chunk(c, F_{}, F_{});
-                rout[64 * (nch - 1) + 1 + lane] = out_a;
+                if (c_lo == 0) chunk(0, T_{}, F_{});
+                for (int32_t c = c_lo > 1 ? c_lo : 1; c <= c_hi; ++c) chunk(c, F_{}, F_{});
+                rout[64 * c_hi + 1 + lane] = out_a;  // the last processed hand-off chunk's first column
                 if (lane == 0) rout[0] = 0;
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1174,6 +1206,217 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     return hipGetLastError();
 }
 
+// Banded knob, anti-diagonal form (default for bands up to 255 when values fit int32).
+//
+// Lanes sit on band diagonals and a step is one anti-diagonal a = i + j: every cell of the band
+// depends only on anti-diagonals a-1 (up: diagonal d-1, left: diagonal d+1) and a-2 (diag: own
+// diagonal), so no in-step scan is needed.  A cell of diagonal d exists on every second
+// anti-diagonal; each lane therefore holds D consecutive diagonals (slots k = 0..D-1, relative
+// band index r = D*lane + k) and updates the even slots on even steps and the odd slots on odd
+// ones, which keeps every lane busy on every step.  A segment of P = ceil((2W+1)/D) lanes holds
+// one pair; 64/P segments share a wavefront.  The slot holding r = 2W is KW = 2W - D(P-1) of the
+// segment's last lane; the slots above it are padding.  Band-edge predecessors ("up" of r = 0,
+// "left" of r = 2W) are -inf (kBandNeg), as in oracle_overlap_banded; cells left of column 1 or
+// above row 1 are the table's zero boundary.
+//
+// Values are kept as w = dp + indel, so both gap moves are read as stored and a cell is
+// w' = max3(w_diag + (score - indel), w_up, w_left) + indel (5 VALU per cell with the compare).
+// The s and t codes of each segment's pair are staged in LDS; slot k of lane l at iteration kap
+// (steps 2kap, 2kap+1) reads s[I0 + kap + ceil(k/2) - 1] and t[J0 + kap - floor(k/2) - 1].
+template <int D, int KW>
+__global__ __launch_bounds__(64, (D <= 4 ? 8 : 6)) void band_diag_kernel(
+    const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
+    int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
+    int32_t lcap, int32_t match, int32_t mismatch, int32_t indel, int32_t W, int32_t nseg,
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    constexpr int U = 8;       // iterations (2 anti-diagonal steps each) per unrolled block
+    constexpr int H = D / 2;   // slots of one parity
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t* keys = reinterpret_cast<int64_t*>(smem);  // per-lane row-n keys for the segment max
+    const int front = W + D + 16;
+    unsigned char* chars = smem + 512 + front;
+    const int lane = threadIdx.x;
+    const int P = (2 * W + D) / D;
+    const int seg_raw = lane / P;
+    const bool real = seg_raw < nseg;
+    const int seg = real ? seg_raw : nseg - 1;
+    const int sl = real ? lane - seg * P : 0;
+    const bool first = sl == 0;
+    const bool last = real && sl == P - 1;
+    unsigned char* ss = chars + (size_t)seg * 2 * lcap;
+    unsigned char* ts = ss + lcap;
+    const int32_t wneg = kBandNeg;
+    const int32_t sc_ma = match - indel, sc_mm = mismatch - indel;
+    const int64_t n_tasks = (n_pairs + nseg - 1) / nseg;
+    for (int64_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+        const int64_t pair = task * nseg + seg;
+        const bool live = real && pair < n_pairs;
+        int32_t n = 0, m = 0, jstar = 0;
+        const uint8_t* sg = codes;
+        const uint8_t* tg = codes;
+        bool bad = false;
+        if (live) {
+            const int32_t a = a_idx[pair], b = b_idx[pair];
+            bad = a < 0 || a >= n_reads || b < 0 || b >= n_reads;
+            if (!bad) {
+                n = len[a];
+                m = len[b];
+                jstar = out_end[pair];
+                bad = n > lcap || m > lcap || jstar < 0 || jstar > m;
+                sg = codes + off[a];
+                tg = codes + off[b];
+            }
+            if (bad) n = m = jstar = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // previous task's LDS readers are done
+        if (live) {
+#pragma unroll 4
+            for (int x = sl; x < n; x += P) ss[x] = sg[x];
+#pragma unroll 4
+            for (int x = sl; x < m; x += P) ts[x] = tg[x];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // geometry: band diagonals d = dlo + r, first anti-diagonal amin (parity of dlo)
+        const int32_t dstar = n - jstar, dlo = dstar - W, dhi = dstar + W;
+        int32_t amin = (dlo <= 0 && dhi >= 0) ? 2 : (dlo > 0 ? dlo + 2 : 2 - dhi);
+        amin -= (amin - dlo) & 1;
+        const int32_t d0 = dlo + D * sl;
+        const int32_t I0 = (amin + d0) >> 1, J0 = (amin - d0) >> 1;
+        const int32_t KN = (2 * n - d0 - amin) >> 1;  // slot k meets row n at iteration KN - ceil(k/2)
+        int32_t kend = 0, kpro = 0, ktlo = INT32_MAX, kthi = -1;
+        if (live && !bad) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const int32_t r = D * sl + k, d = d0 + k;
+                if (r > 2 * W) continue;
+                const int32_t par = k & 1;
+                const int32_t ast = (d < 0 ? -d : d) + 2;
+                const int32_t aend = min(2 * n - d, 2 * m + d);
+                kpro = max(kpro, (ast - amin - par) >> 1);
+                if (ast > aend) continue;
+                kend = max(kend, ((aend - amin - par) >> 1) + 1);
+                const int32_t jn = n - d;
+                if (jn >= 1 && jn <= m) {
+                    const int32_t kn = KN - ((k + 1) >> 1);
+                    ktlo = min(ktlo, kn);
+                    kthi = max(kthi, kn);
+                }
+            }
+        }
+        for (int o = 32; o; o >>= 1) {
+            kend = max(kend, __shfl_xor(kend, o, 64));
+            kpro = max(kpro, __shfl_xor(kpro, o, 64));
+            ktlo = min(ktlo, __shfl_xor(ktlo, o, 64));
+            kthi = max(kthi, __shfl_xor(kthi, o, 64));
+        }
+        // wave-uniform block bounds (multiples of U): masks before KP, row-n capture in [TL, TH)
+        kend = __builtin_amdgcn_readfirstlane(kend);
+        kpro = __builtin_amdgcn_readfirstlane(kpro);
+        ktlo = __builtin_amdgcn_readfirstlane(ktlo);
+        kthi = __builtin_amdgcn_readfirstlane(kthi);
+        const int32_t KE = (kend + U - 1) / U * U;
+        const int32_t KP = min(KE, (kpro + U - 1) / U * U);
+        const int32_t TL = kthi < 0 ? KE : ktlo / U * U;
+        const int32_t TH = kthi < 0 ? KE : min(KE, (kthi + U) / U * U);
+
+        int32_t w[D], cap[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            w[k] = indel;  // zero boundary (w = dp + indel)
+            cap[k] = wneg;
+        }
+        const int32_t Ai = 1 - I0, Bj = 1 - J0;  // slot k valid once kap + ceil(k/2) >= Ai, kap - floor(k/2) >= Bj
+        const unsigned char* sp = ss + I0 - 1;
+        const unsigned char* tp = ts + J0 - H;
+        auto block = [&](int32_t kb, auto pro_t, auto trk_t) {
+            constexpr bool PRO = decltype(pro_t)::value;
+            constexpr bool TRK = decltype(trk_t)::value;
+            int32_t S[U + H], T[U + H];
+            const unsigned char* spb = sp + kb;
+            const unsigned char* tpb = tp + kb;
+#pragma unroll
+            for (int x = 0; x < U + H; ++x) {
+                S[x] = spb[x];
+                T[x] = tpb[x];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t kap = kb + u;
+                // even step: even slots read the odd slots of the previous step
+                // wave_shr:1 (lane 0 is a segment's first lane: the mask covers it)
+                int32_t upsh = __builtin_amdgcn_mov_dpp(w[D - 1], 0x138, 0xF, 0xF, true);
+                upsh = first ? wneg : upsh;
+#pragma unroll
+                for (int k = 0; k < D; k += 2) {
+                    const int32_t up = k == 0 ? upsh : w[k - 1];
+                    const int32_t left = (k == KW) ? (last ? wneg : w[k + 1]) : w[k + 1];
+                    const int32_t sc = S[u + k / 2] == T[u + H - 1 - k / 2] ? sc_ma : sc_mm;
+                    int32_t nv = max(max(w[k] + sc, up), left) + indel;
+                    if constexpr (PRO) nv = ((kap + k / 2 >= Ai) & (kap - k / 2 >= Bj)) ? nv : indel;
+                    w[k] = nv;
+                    if constexpr (TRK) cap[k] = kap + k / 2 == KN ? nv : cap[k];
+                }
+                // odd step: odd slots read the even slots just written
+                // wave_shl:1 (lane 63 holds padding or an unused lane: its input is never read)
+                const int32_t lsh = __builtin_amdgcn_mov_dpp(w[0], 0x130, 0xF, 0xF, true);
+#pragma unroll
+                for (int k = 1; k < D; k += 2) {
+                    const int32_t up = w[k - 1];
+                    const int32_t left = k == D - 1 ? lsh : w[k + 1];
+                    const int32_t sc = S[u + (k + 1) / 2] == T[u + H - 1 - (k - 1) / 2] ? sc_ma : sc_mm;
+                    int32_t nv = max(max(w[k] + sc, up), left) + indel;
+                    if constexpr (PRO) nv = ((kap + (k + 1) / 2 >= Ai) & (kap - (k - 1) / 2 >= Bj)) ? nv : indel;
+                    w[k] = nv;
+                    if constexpr (TRK) cap[k] = kap + (k + 1) / 2 == KN ? nv : cap[k];
+                }
+            }
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        for (int32_t kb = 0; kb < KE;) {
+            const bool pro = kb < KP, trk = kb >= TL && kb < TH;
+            int32_t nx = KE;
+            if (KP > kb) nx = min(nx, KP);
+            if (TL > kb) nx = min(nx, TL);
+            if (TH > kb) nx = min(nx, TH);
+            if (pro && trk) for (; kb < nx; kb += U) block(kb, T_{}, T_{});
+            else if (pro) for (; kb < nx; kb += U) block(kb, T_{}, F_{});
+            else if (trk) for (; kb < nx; kb += U) block(kb, F_{}, T_{});
+            else for (; kb < nx; kb += U) block(kb, F_{}, F_{});
+        }
+        // row-n keys: max value, ties to the smallest column (the reference's first strict '>')
+        int64_t key = INT64_MIN;
+        if (live && !bad) {
+            if (first && jstar <= W) key = (int64_t)0xFFFFFFFFll;  // j = 0 inside the band: value 0
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const int32_t r = D * sl + k, d = d0 + k, jn = n - d;
+                if (r <= 2 * W && jn >= 1 && jn <= m) {
+                    const int64_t kk = ((int64_t)(cap[k] - indel) << 32) | (uint32_t)~jn;
+                    key = kk > key ? kk : key;
+                }
+            }
+        }
+        keys[lane] = key;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (live && first) {
+            for (int x = 1; x < P; ++x) {
+                const int64_t kx = keys[lane + x];
+                key = kx > key ? kx : key;
+            }
+            if (bad) {
+                atomicOr(err_flag, 1u);
+                out_score[pair] = -1;
+                out_end[pair] = -1;
+            } else {
+                out_score[pair] = (int32_t)(key >> 32);
+                out_end[pair] = (int32_t)~(uint32_t)key;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
 template <typename Acc, bool BANDED>
 static void launch_dp_t(const OvlDpArgs* g, unsigned blocks, size_t lds, hipStream_t stream) {
     dp_kernel<Acc, BANDED><<<blocks, 64, lds, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
@@ -1193,6 +1436,62 @@ static void launch_band_row_t(const OvlDpArgs* g, hipStream_t stream) {
         (int32_t)g->mismatch, (int32_t)g->indel, g->band, g->out_score, g->out_end, g->err_flag);
 }
 
+template <int D, int KW>
+static void launch_band_diag_t(const OvlDpArgs* g, int nseg, hipStream_t stream) {
+    const int W = g->band;
+    const int64_t lcap = g->mcap > 0 ? g->mcap : 1;
+    // keys + front pad + one 2*lcap stride per segment (s then t) + the over-read tail
+    const size_t lds = 512 + (size_t)(W + D + 16) + (size_t)(nseg + 1) * 2 * lcap + W + 64;
+    int64_t blocks = (g->n_pairs + nseg - 1) / nseg;
+    if (blocks > 32768) blocks = 32768;
+    band_diag_kernel<D, KW><<<(unsigned)blocks, 64, lds, stream>>>(
+        g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, (int32_t)lcap, (int32_t)g->match,
+        (int32_t)g->mismatch, (int32_t)g->indel, W, nseg, g->out_score, g->out_end, g->err_flag);
+}
+
+// Slots per lane for the anti-diagonal form: the VALU cost per pair-iteration is about
+// (5 D + 8) / segments-per-wave; the smallest wins.  Returns D (0: band too wide).
+extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out) {
+    int bestD = 0, bestseg = 0;
+    double bestc = 1e30;
+    for (int D = 2; D <= 8; D *= 2) {
+        const int P = (2 * band + D) / D;
+        if (P > 64) continue;
+        int nseg = 64 / P;
+        // keep the per-wave LDS near 24 KiB (at least one segment)
+        const int64_t per = 2 * (int64_t)(lcap > 0 ? lcap : 1);
+        const int64_t fit = (24576 - 1024 - 2 * (int64_t)band) / per - 1;
+        if (nseg > fit) nseg = fit > 1 ? (int)fit : 1;
+        const double c = (5.0 * D + 8.0) / nseg;
+        if (c < bestc - 1e-9) {
+            bestc = c;
+            bestD = D;
+            bestseg = nseg;
+        }
+    }
+    if (nseg_out) *nseg_out = bestseg;
+    return bestD;
+}
+
+static hipError_t launch_band_diag(const OvlDpArgs* g, hipStream_t stream) {
+    int nseg = 0;
+    const int D = ovl_band_diag_slots(g->band, g->mcap, &nseg);
+    if (D == 0) return hipErrorInvalidValue;
+    const int P = (2 * g->band + D) / D;
+    const int KW = 2 * g->band - D * (P - 1);
+    switch (D * 16 + KW) {
+        case 2 * 16 + 0: launch_band_diag_t<2, 0>(g, nseg, stream); break;
+        case 4 * 16 + 0: launch_band_diag_t<4, 0>(g, nseg, stream); break;
+        case 4 * 16 + 2: launch_band_diag_t<4, 2>(g, nseg, stream); break;
+        case 8 * 16 + 0: launch_band_diag_t<8, 0>(g, nseg, stream); break;
+        case 8 * 16 + 2: launch_band_diag_t<8, 2>(g, nseg, stream); break;
+        case 8 * 16 + 4: launch_band_diag_t<8, 4>(g, nseg, stream); break;
+        case 8 * 16 + 6: launch_band_diag_t<8, 6>(g, nseg, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     int64_t blocks = g->n_pairs;
@@ -1203,13 +1502,27 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
         // banded mode runs only where values fit int32 (the host checks) and never writes tb
         if (g->wide || g->tb) return hipErrorInvalidValue;
         const int lanes = 2 * g->band + 1;
-        if (g->band_rows && lanes <= 192) {
-            if (lanes <= 16) launch_band_row_t<16, 1>(g, stream);
-            else if (lanes <= 32) launch_band_row_t<32, 1>(g, stream);
-            else if (lanes <= 64) launch_band_row_t<64, 1>(g, stream);
-            else if (lanes <= 128) launch_band_row_t<64, 2>(g, stream);
-            else launch_band_row_t<64, 3>(g, stream);
-            return hipGetLastError();
+        switch (g->band_form) {
+            case OVL_BAND_FORM_DIAG:
+                return launch_band_diag(g, stream);
+            case OVL_BAND_FORM_ROWS:
+                if (lanes <= 16) launch_band_row_t<16, 1>(g, stream);
+                else if (lanes <= 32) launch_band_row_t<32, 1>(g, stream);
+                else if (lanes <= 64) launch_band_row_t<64, 1>(g, stream);
+                else if (lanes <= 128) launch_band_row_t<64, 2>(g, stream);
+                else if (lanes <= 192) launch_band_row_t<64, 3>(g, stream);
+                else return hipErrorInvalidValue;
+                return hipGetLastError();
+            case OVL_BAND_FORM_FAST: {
+                const int32_t pitch = ((g->mcap + 126) / 64) * 64 + 64;
+                const size_t lds2 = (size_t)2 * pitch * sizeof(int32_t) + (size_t)pitch;
+                dp_fast_kernel<int32_t, true><<<nb, 64, lds2, stream>>>(
+                    g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
+                    g->mismatch, g->indel, g->band, g->out_score, g->out_end, g->err_flag);
+                return hipGetLastError();
+            }
+            default:
+                break;
         }
         launch_dp_t<int32_t, true>(g, nb, lds, stream);
     } else if (!g->tb && !g->classic) {
@@ -1217,13 +1530,13 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
         const int32_t pitch = ((g->mcap + 126) / 64) * 64 + 64;
         const size_t lds2 = (size_t)2 * pitch * sizeof(int32_t) + (size_t)pitch;
         if (g->wide)
-            dp_fast_kernel<int64_t><<<nb, 64, lds2, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
-                                                              g->n_pairs, g->mcap, g->match, g->mismatch, g->indel,
-                                                              g->out_score, g->out_end, g->err_flag);
+            dp_fast_kernel<int64_t, false><<<nb, 64, lds2, stream>>>(
+                g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
+                g->mismatch, g->indel, -1, g->out_score, g->out_end, g->err_flag);
         else
-            dp_fast_kernel<int32_t><<<nb, 64, lds2, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
-                                                              g->n_pairs, g->mcap, g->match, g->mismatch, g->indel,
-                                                              g->out_score, g->out_end, g->err_flag);
+            dp_fast_kernel<int32_t, false><<<nb, 64, lds2, stream>>>(
+                g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
+                g->mismatch, g->indel, -1, g->out_score, g->out_end, g->err_flag);
     } else if (g->wide) {
         launch_dp_t<int64_t, false>(g, nb, lds, stream);
     } else {

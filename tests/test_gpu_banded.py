@@ -99,21 +99,47 @@ def test_banded_unsupported_magnitudes(engine):
         engine.score([0], [1], 2 ** 28, -1, -1, 4)
 
 
-@pytest.mark.parametrize("band", [0, 3, 8, 31, 63, 64, 95, 96])
-def test_strip_and_row_forms_agree_with_oracle(oracle_mod, reads_pairs, band):
-    """The band knob has two kernels (row form by default, strip form for wide bands / long reads /
-    large magnitudes); OVL_BAND_STRIP=1 forces the strip form: both must equal the oracle."""
+FORMS = {"default": {}, "rows": {"OVL_BAND_FORM": "rows"}, "fast": {"OVL_BAND_FORM": "fast"},
+         "strip": {"OVL_BAND_FORM": "strip"}}
+
+
+def _score_with_env(env, reads, a, b, params, band):
     import os
     from ovlgraph import OverlapEngine
+    os.environ.update(env)
+    try:
+        with OverlapEngine(0) as eng:
+            eng.set_reads(reads)
+            return eng.score(a, b, *params, band)
+    finally:
+        for k in env:
+            del os.environ[k]
+
+
+@pytest.mark.parametrize("band", [0, 1, 2, 3, 8, 15, 16, 31, 32, 33, 63, 64, 95, 96, 150, 255, 256])
+@pytest.mark.parametrize("form", sorted(FORMS))
+def test_band_forms_agree_with_oracle(oracle_mod, reads_pairs, band, form):
+    """The band knob has four kernels: the anti-diagonal form (default), the row form (lanes on band
+    diagonals, a row per step; up to 192 lanes), the chunked strip kernel with band masks and the
+    classic strip form, picked with OVL_BAND_FORM: each must equal the oracle."""
     reads, a, b = reads_pairs
     rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
-    for strip in ("0", "1"):
-        os.environ["OVL_BAND_STRIP"] = strip
-        try:
-            with OverlapEngine(0) as eng:
-                eng.set_reads(reads)
-                sc, en = eng.score(a, b, 10, -1, -2, band)
-        finally:
-            del os.environ["OVL_BAND_STRIP"]
-        np.testing.assert_array_equal(sc, rs)
-        np.testing.assert_array_equal(en, re_)
+    sc, en = _score_with_env(FORMS[form], reads, a, b, (10, -1, -2), band)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("band", [5, 40, 100, 300])
+def test_banded_long_reads_vs_oracle(engine, oracle_mod, band):
+    """Reads past the row form's 1024-base limit, mixed with short ones (seed diagonals far off the
+    main one in both directions: bands starting many strips down or many chunks right)."""
+    rng = random.Random(31 + band)
+    reads = _indel_reads(rng, 40, 1500) + _indel_reads(rng, 40, 90) + _indel_reads(rng, 20, 600)
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(600)], np.int32)
+    b = np.array([rng.randrange(n) for _ in range(600)], np.int32)
+    engine.set_reads(reads)
+    sc, en = engine.score(a, b, 10, -1, -2, band)
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)

@@ -1,4 +1,4 @@
-# rocprofv3 kernel-trace/stats for the non-metric kernels: cfg5 band sweep (seed + band_row_kernel / dp_kernel),
+# rocprofv3 kernel-trace/stats for the non-metric kernels: cfg5 band sweep (seed + band_diag_kernel / dp_fast_kernel),
 # device candidate enumeration + local alignment (bench extras at cfg2).  usage: bash tools/gpu_profile_extras.sh <tag>
 set -u
 TAG=${1:-extras}
