@@ -24,6 +24,7 @@ namespace {
 
 constexpr int32_t kFastMaxLen = 256;   // bit-plane layouts up to W = 8 words of 32 bases
 constexpr int32_t kDpMaxLen = 8192;    // DP kernel: LDS row of the t read
+constexpr int32_t kLaneMaxLen = 1024;  // lane-per-pair DP: hand-off column buffer per wavefront slot
 
 struct DevBuf {
     void* p = nullptr;
@@ -42,6 +43,12 @@ struct ovl_ctx {
     int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
     int32_t band_form = -1;       // OVL_BAND_FORM env (diag|rows|fast|strip): band knob kernel (tests)
     int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
+    int32_t dp_lane = -1;         // OVL_DP_LANE env: lane-per-pair full DP (-1 auto by list size, 0 off, 1 forced)
+    int32_t lane_cw = 32;         // OVL_LANE_CW env: lane kernel strip width (16 or 32 columns)
+    int64_t lane_min_pairs = 65536;  // OVL_LANE_MIN_PAIRS env: auto threshold (one tile per SIMD)
+    int32_t lane_prof = 1;        // OVL_LANE_PROF=0: compare/select scores instead of the byte profile (tests)
+    int32_t lane_col16 = 1;       // OVL_LANE_COL16=0: int32 hand-off column even when int16 holds (tests)
+    int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
     int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
                                   // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
     // resident reads
@@ -54,6 +61,8 @@ struct ovl_ctx {
     DevBuf codes, off, len, sfx, pfx, lut, full;  // full: bit r set iff len[r] == lmax
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
+    DevBuf lane_col;      // lane-per-pair DP: per-wavefront strip hand-off columns
+    int64_t codes_bytes = 0;
     // device candidate enumeration (ovl_candidates): per-read keys / groups and the pair list
     DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
     int64_t cand_n = -1;  // -1: no candidate list for the resident reads
@@ -190,6 +199,18 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s);
 
+// Lane-per-pair full DP (ovl_dp_lane.hip): one lane per pair, so it needs many pairs to fill the
+// chip (below that the one-wavefront-per-pair dp_fast_kernel is faster), reads short enough for
+// the per-wavefront hand-off columns, and G = dp - indel*(i+j) inside int32.
+bool use_dp_lane(const ovl_ctx* c, int64_t match, int64_t mismatch, int64_t indel, int64_t n_pairs) {
+    if (c->dp_lane == 0) return false;
+    const int64_t L = std::max<int32_t>(c->lmax, 1);
+    const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
+    if (L > kLaneMaxLen || (4 * L + 4) * M >= (int64_t(1) << 30) || c->codes_bytes + 64 >= (int64_t(1) << 32))
+        return false;
+    return c->dp_lane == 1 || n_pairs >= c->lane_min_pairs;
+}
+
 // Kernels queue pair indices as int32 (LDS side ring); split huge lists.
 int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                  int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
@@ -270,6 +291,26 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
         g.wide = pl.wide ? 1 : 0;
         g.band = pl.kernel == OVL_KERNEL_BANDED ? pl.band : -1;
         g.classic = c->dp_classic;
+        if (g.band < 0 && !g.wide && !g.classic && use_dp_lane(c, match, mismatch, indel, n_pairs)) {
+            OvlLaneArgs k{};
+            k.cw = c->lane_cw;
+            k.slots = (int64_t)c->cu_count * 4 * ovl_dp_lane_waves_per_simd(k.cw);
+            const size_t col_bytes = (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t);
+            HIPCHK(c, ensure(c->lane_col, col_bytes));
+            const int64_t L = std::max<int32_t>(c->lmax, 1);
+            const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
+            const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
+            k.prof = c->lane_prof && c->planes == 2 && indel <= 0 && sma >= -128 && sma <= 127 && smm >= -128 &&
+                     smm <= 127;
+            k.col16 = c->lane_col16 && (4 * L + 4) * M < (int64_t(1) << 15);
+            k.sfx = k.prof && c->lane_sfx && c->wmax > 0;
+            k.sfx_words = as<uint32_t>(c->sfx);
+            k.srow = c->srow;
+            k.wsfx = c->wmax;
+            k.colbuf = as<uint32_t>(c->lane_col);
+            HIPCHK(c, ovl_launch_dp_lane(&g, &k, s));
+            return OVL_OK;
+        }
         if (g.band >= 0) {
             // "-inf" (kBandNeg) must stay below every value: |values| <= (2*lmax + 1) * M and the row
             // form's scan adds up to 2*band*|indel|
@@ -340,6 +381,12 @@ OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
         else if (!strcmp(e, "strip")) c->band_form = OVL_BAND_FORM_STRIP;
     }
     if (const char* e = getenv("OVL_DP_CLASSIC")) c->dp_classic = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_DP_LANE")) c->dp_lane = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_CW")) c->lane_cw = atoi(e) == 32 ? 32 : 16;
+    if (const char* e = getenv("OVL_LANE_MIN_PAIRS")) c->lane_min_pairs = atoll(e);
+    if (const char* e = getenv("OVL_LANE_PROF")) c->lane_prof = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_COL16")) c->lane_col16 = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_SFX")) c->lane_sfx = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 1024) c->blocks_per_cu = v;
@@ -366,7 +413,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->full, &c->a, &c->b, &c->score, &c->end,
                       &c->tb, &c->err_flag, &c->k_pre, &c->k_suf, &c->k_sorted, &c->k_iota, &c->k_order, &c->k_lo,
                       &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b, &c->l_q, &c->l_r, &c->l_row,
-                      &c->l_tb, &c->l_best})
+                      &c->l_tb, &c->l_best, &c->lane_col})
         release(*b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -416,7 +463,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     DevBuf raw;
     HIPCHK(c, ensure(c->off, sizeof(int64_t) * off.size()));
     HIPCHK(c, ensure(c->len, sizeof(int32_t) * len.size()));
-    HIPCHK(c, ensure(c->codes, (size_t)total));
+    HIPCHK(c, ensure(c->codes, (size_t)total + 64));  // tail pad: clamped reads of empty last reads
     HIPCHK(c, ensure(c->lut, 256));
     hipError_t e = ensure(raw, (size_t)total);
     if (e != hipSuccess) return fail(c, OVL_E_OOM, "raw read buffer: %s", hipGetErrorString(e));
@@ -458,6 +505,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     if (e != hipSuccess)
         return fail(c, e == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP, "ovl_set_reads: %s", hipGetErrorString(e));
     c->lmax = lmax;
+    c->codes_bytes = total;
     c->planes = planes;
     c->wmax = wmax;
     c->srow = srow;

@@ -1,0 +1,311 @@
+// ovl_dp_lane.hip — lane-per-pair full DP for gapped scoring (scores only), gfx950.
+//
+// aligners.py:27-57 for a finite indel: the full (n+1) x (m+1) table with
+// dp[i][j] = max(dp[i-1][j-1] + s(i,j), dp[i-1][j] + indel, dp[i][j-1] + indel),
+// row 0 and column 0 zero, then the last row's first strict-'>' argmax.
+//
+// One lane owns one candidate pair (64 consecutive pairs per wavefront), so no
+// cell waits on another lane and no lane idles on the table's corners (the
+// anti-diagonal kernels do both).  The lane sweeps vertical strips of CW columns:
+// the strip's current row sits in CW registers and the rows advance top to
+// bottom; the strip's last column is handed to the next strip through a per-wave
+// global column buffer ([row][lane], coalesced), the only memory traffic besides
+// the read codes.
+//
+// Potential: G[i][j] = dp[i][j] - indel * (i + j).  Then
+//   G[i][j] = max3(G[i-1][j-1] + s(i,j) - 2*indel, G[i-1][j], G[i][j-1])
+// so a cell is compare, select, add, max3 -- no indel adds on the gap moves.
+// Values are exact in int32 when the host's bound holds (|values| + |indel|*(n+m)
+// < 2^30; otherwise the int64 anti-diagonal kernel runs).
+//
+// Rows are aligned at the END: lane row i = it - sk + 1 with sk = nmax - n (plus a
+// pad making the row count a multiple of the 4-row body), so every lane reaches its
+// row n on the last iteration and the row-n scan happens once per strip from
+// registers.  Iterations with i <= 0 are "virtual": masked to the row-0 boundary
+// (dp = 0), only in the leading iterations where some lane has them.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "ovl_kernels.h"
+
+namespace ovl {
+namespace {
+
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+__device__ __forceinline__ int32_t wave_min(int32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+}  // namespace
+
+// codes: dense symbol codes (ovl_set_reads), off/len per read.  colbuf: rcap dwords per lane for each
+// resident wavefront slot ([row][lane], or [row pair][lane] with COL16), rcap >= lmax rounded to 32.
+//   PROF   <= 4 symbols, diagonal scores within int8, indel <= 0: byte score profile + SDWA adds
+//          (2 VALU per cell); virtual rows select an all-zero profile, which reproduces row 0
+//          exactly (row 0 rises by -indel per column, so neither the diagonal nor the left move
+//          can exceed it), so no cell needs a mask
+//   COL16  |G| < 2^15: the hand-off column as int16, two rows per dword (half the traffic)
+//   SFX    (PROF) the row symbols come from the resident bit-plane rows (sfx, right-aligned):
+//          with the row count a multiple of 32, row iteration `it` reads bit it % 32 of word
+//          it / 32 + W - R / 32 on every lane, so a lane loads 8 bytes per 32 rows instead of
+//          a byte gather per row
+template <int CW, int OCC, bool PROF, bool COL16, bool SFX>
+__global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __restrict__ codes,
+                                                           const int64_t* __restrict__ off,
+                                                           const int32_t* __restrict__ len, int32_t n_reads,
+                                                           const uint32_t* __restrict__ sfx, int32_t srow,
+                                                           int32_t wsfx, const int32_t* __restrict__ a_idx,
+                                                           const int32_t* __restrict__ b_idx, int64_t n_pairs,
+                                                           int32_t lcap, int32_t rcap, int32_t match,
+                                                           int32_t mismatch, int32_t indel,
+                                                           uint32_t* __restrict__ colbuf,
+                                                           int32_t* __restrict__ out_score,
+                                                           int32_t* __restrict__ out_end,
+                                                           uint32_t* __restrict__ err_flag) {
+    static_assert(!SFX || PROF, "bit-plane row symbols need the byte profile");
+    const int lane = threadIdx.x & 63;
+    const int64_t wslot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nslots = (int64_t)gridDim.x * 4;
+    uint32_t* __restrict__ col = colbuf + wslot * (int64_t)rcap * 64 + lane;
+    const int64_t ntiles = (n_pairs + 63) >> 6;
+    const int32_t g = indel;
+    const int32_t s_ma = match - 2 * g;     // diagonal move, match, in G units
+    const int32_t s_mm = mismatch - 2 * g;  // diagonal move, mismatch
+    for (int64_t tile = wslot; tile < ntiles; tile += nslots) {
+        const int64_t p = tile * 64 + lane;
+        const bool live = p < n_pairs;
+        int32_t a = live ? a_idx[p] : 0;
+        int32_t b = live ? b_idx[p] : 0;
+        bool bad = live && (a < 0 || a >= n_reads || b < 0 || b >= n_reads);
+        if (!live || bad) { a = 0; b = 0; }
+        int32_t n = (live && !bad) ? len[a] : 0;
+        int32_t m = (live && !bad) ? len[b] : 0;
+        if (n > lcap || m > lcap) { bad = true; n = 0; m = 0; }
+        const uint32_t sa = (uint32_t)off[a];
+        const uint32_t tb = (uint32_t)off[b];
+        const int32_t nmax = wave_max(n);
+        const int32_t nmin = wave_min(n);
+        const int32_t mmax = wave_max(m);
+        constexpr int RQ = SFX ? 32 : 4;
+        const int32_t R = (nmax + RQ - 1) / RQ * RQ;  // row iterations (end-aligned rows)
+        const int32_t sk = R - n;                      // this lane's virtual rows
+        const int32_t mcut = R - nmin;                 // iterations in which some lane is virtual
+        const uint32_t* __restrict__ srow_p = sfx + (int64_t)a * srow + 2 * (wsfx - R / 32);
+        int32_t best = 0, bend = 0;                    // dp[n][0] = 0 is the j = 0 candidate
+
+        // one strip of CW columns j0+1 .. j0+CW; FIRST: the left boundary is column 0 (no loads)
+        auto strip = [&](int32_t j0, auto first_tag) {
+            constexpr bool FIRST = decltype(first_tag)::value;
+            uint32_t tc[CW];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                // columns past m compute unread values: any symbol will do
+                const int32_t jc = j0 + c < m ? j0 + c : 0;
+                tc[c] = (uint32_t)codes[tb + (uint32_t)jc];
+            }
+            // PROF: per symbol x a byte profile of the strip, PX[x][w] byte k = s(x, t[j0 + 4w + k]); a
+            // row picks its symbol's words with three bit muxes per word and a cell adds its byte with a
+            // sign-extending SDWA add
+            constexpr int PW = PROF ? CW / 4 : 1;
+            uint32_t PX[4][PW];
+            if constexpr (PROF) {
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+#pragma unroll
+                    for (int w = 0; w < PW; ++w) {
+                        uint32_t word = 0;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            word |= ((uint32_t)(tc[4 * w + k] == (uint32_t)x ? s_ma : s_mm) & 0xFFu) << (8 * k);
+                        PX[x][w] = word;
+                    }
+                }
+            }
+            int32_t A[CW], B[CW];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) A[c] = -g * (j0 + 1 + c);  // row 0: G[0][j] = -indel * j
+            int32_t prevL = -g * j0;                                 // G[i-1][j0] entering row 1
+
+            // queue for rows it .. it+3: s codes (byte path) and the raw hand-off words
+            constexpr int NCW = COL16 ? 2 : 4;
+            constexpr int NQS = SFX ? 1 : 4;
+            uint32_t qs[NQS], qc[NCW];
+            uint32_t S0 = 0, S1 = 0, S0n = 0, S1n = 0;  // SFX: bit planes of the current / next 32 rows
+            auto fetch4 = [&](int32_t it4) {
+                if constexpr (!SFX) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int32_t i0 = it4 + k - sk;  // s index i - 1
+                        const int32_t ic = i0 < 0 ? 0 : (i0 >= n ? (n > 0 ? n - 1 : 0) : i0);
+                        qs[k] = (uint32_t)codes[sa + (uint32_t)ic];
+                    }
+                }
+                if constexpr (!FIRST) {
+#pragma unroll
+                    for (int k = 0; k < NCW; ++k) qc[k] = col[(int64_t)((COL16 ? it4 / 2 : it4) + k) * 64];
+                }
+            };
+            auto fetch_planes = [&](int32_t kb) {
+                const uint2 v = *reinterpret_cast<const uint2*>(srow_p + 2 * kb);
+                S0n = v.x;
+                S1n = v.y;
+            };
+            auto left = [&](int32_t it, const uint32_t(&cw)[NCW], int k) -> int32_t {
+                if constexpr (FIRST) return -g * (it - sk + 1);  // G[i][0] = -indel * i
+                else if constexpr (COL16) return (int32_t)(int16_t)(uint16_t)(cw[k >> 1] >> (16 * (k & 1)));
+                else return (int32_t)cw[k];
+            };
+            // one row: O (row i-1) -> N (row i); returns N[CW-1], the hand-off value
+            auto row = [&](int32_t it, int32_t(&O)[CW], int32_t(&N)[CW], uint32_t sc, int32_t lb,
+                           auto masked_tag) -> int32_t {
+                constexpr bool MASKED = decltype(masked_tag)::value;
+                const bool virt = it < sk;
+                int32_t d = prevL;
+                int32_t l = lb;
+                uint32_t P[PW];
+                if constexpr (PROF) {
+                    uint32_t m0, m1;  // bit 0 / bit 1 of the row symbol, as all-ones / all-zero masks
+                    if constexpr (SFX) {
+                        const uint32_t r = (uint32_t)it & 31u;
+                        m0 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)S0, r, 1);
+                        m1 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)S1, r, 1);
+                    } else {
+                        m0 = (uint32_t)(((int32_t)(sc << 31)) >> 31);
+                        m1 = (uint32_t)(((int32_t)(sc << 30)) >> 31);
+                    }
+                    const uint32_t nv = (uint32_t)~((it - sk) >> 31);  // 0 on virtual rows
+#pragma unroll
+                    for (int w = 0; w < PW; ++w) {
+                        const uint32_t lo = __builtin_amdgcn_bitop3_b32(m0, PX[1][w], PX[0][w], 0xCA);  // m0 ? : mux
+                        const uint32_t hi = __builtin_amdgcn_bitop3_b32(m0, PX[3][w], PX[2][w], 0xCA);
+                        P[w] = __builtin_amdgcn_bitop3_b32(m1, hi, lo, 0xCA);
+                        if constexpr (MASKED) P[w] &= nv;  // zero profile: the row repeats row 0
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    int32_t s2;
+                    if constexpr (PROF) s2 = (int32_t)(int8_t)(uint8_t)(P[c >> 2] >> (8 * (c & 3)));
+                    else s2 = sc == tc[c] ? s_ma : s_mm;
+                    int32_t v = max(max(d + s2, O[c]), l);
+                    if constexpr (MASKED && !PROF) v = virt ? __builtin_amdgcn_readfirstlane(-g * (j0 + 1 + c)) : v;
+                    N[c] = v;
+                    d = O[c];
+                    l = v;
+                }
+                prevL = lb;
+                return N[CW - 1];
+            };
+            auto body = [&](int32_t it, auto masked_tag) {
+                // rows it .. it+3 (A -> B -> A -> B -> A); the queue refills 4 rows ahead
+                uint32_t s4[NQS], c4[NCW];
+#pragma unroll
+                for (int k = 0; k < NQS; ++k) s4[k] = qs[k];
+#pragma unroll
+                for (int k = 0; k < NCW; ++k) c4[k] = qc[k];
+                if constexpr (SFX) {
+                    if ((it & 31) == 0) {  // next 32 rows: rotate the plane words, prefetch the block after
+                        S0 = S0n;
+                        S1 = S1n;
+                        if (it + 32 < R) fetch_planes((it + 32) >> 5);
+                    }
+                }
+                if (it + 4 < R) fetch4(it + 4);
+                const int32_t v0 = row(it, A, B, s4[0], left(it, c4, 0), masked_tag);
+                const int32_t v1 = row(it + 1, B, A, s4[SFX ? 0 : 1], left(it + 1, c4, 1), masked_tag);
+                const int32_t v2 = row(it + 2, A, B, s4[SFX ? 0 : 2], left(it + 2, c4, 2), masked_tag);
+                const int32_t v3 = row(it + 3, B, A, s4[SFX ? 0 : 3], left(it + 3, c4, 3), masked_tag);
+                // hand-off column for the next strip (also after the last strip: never read, no branch)
+                if constexpr (COL16) {
+                    col[(int64_t)(it / 2) * 64] = ((uint32_t)v0 & 0xFFFFu) | ((uint32_t)v1 << 16);
+                    col[(int64_t)(it / 2 + 1) * 64] = ((uint32_t)v2 & 0xFFFFu) | ((uint32_t)v3 << 16);
+                } else {
+                    col[(int64_t)it * 64] = (uint32_t)v0;
+                    col[(int64_t)(it + 1) * 64] = (uint32_t)v1;
+                    col[(int64_t)(it + 2) * 64] = (uint32_t)v2;
+                    col[(int64_t)(it + 3) * 64] = (uint32_t)v3;
+                }
+            };
+            if constexpr (SFX) fetch_planes(0);
+            fetch4(0);
+            int32_t it = 0;
+            for (; it < mcut; it += 4) body(it, std::true_type{});
+            for (; it < R; it += 4) body(it, std::false_type{});
+            // A holds row n of every lane: the strip's part of the last-row scan (strict '>', j ascending)
+            const int32_t base = g * (n + j0 + 1);  // dp = G + indel * (n + j)
+#pragma unroll
+            for (int c = 0; c < CW; ++c) {
+                const int32_t v = A[c] + base + g * c;
+                const bool better = (j0 + 1 + c <= m) && v > best;
+                best = better ? v : best;
+                bend = better ? j0 + 1 + c : bend;
+            }
+        };
+        if (mmax > 0) strip(0, std::true_type{});
+        // the next strip reads this strip's hand-off column (same lane, program order)
+        for (int32_t j0 = CW; j0 < mmax; j0 += CW) strip(j0, std::false_type{});
+        if (live) {
+            if (bad) {
+                atomicOr(err_flag, 1u);
+                out_score[p] = -1;
+                out_end[p] = -1;
+            } else {
+                out_score[p] = best;
+                out_end[p] = bend;
+            }
+        }
+    }
+}
+
+}  // namespace ovl
+
+using ovl::dp_lane_kernel;
+
+extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap) { return ((lcap + 31) & ~31) + 4; }
+
+// strip width per lane-kernel variant: 16 columns at 6 waves/SIMD, 32 columns at 4 waves/SIMD
+extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw) { return cw == 32 ? 4 : 6; }
+
+extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* k, hipStream_t stream) {
+    if (g->n_pairs <= 0) return hipSuccess;
+    const int64_t tiles = (g->n_pairs + 63) / 64;
+    int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    const int32_t lcap = g->mcap;
+    const int32_t rcap = ovl_dp_lane_rcap(lcap);
+    if (k->sfx && (!k->prof || !k->sfx_words || k->wsfx * 32 < lcap)) return hipErrorInvalidValue;
+#define OVL_LANE(CW, OCC, PR, C16, SX)                                                                        \
+    dp_lane_kernel<CW, OCC, PR, C16, SX><<<(unsigned)blocks, 256, 0, stream>>>(                             \
+        g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx, g->n_pairs, \
+        lcap, rcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, k->colbuf, g->out_score,     \
+        g->out_end, g->err_flag)
+    const int key = (k->cw == 32 ? 8 : k->cw == 16 ? 0 : 64) | (k->prof ? 4 : 0) | (k->col16 ? 2 : 0) |
+                    (k->sfx ? 1 : 0);
+    switch (key) {
+        case 0: OVL_LANE(16, 6, false, false, false); break;
+        case 2: OVL_LANE(16, 6, false, true, false); break;
+        case 4: OVL_LANE(16, 6, true, false, false); break;
+        case 5: OVL_LANE(16, 6, true, false, true); break;
+        case 6: OVL_LANE(16, 6, true, true, false); break;
+        case 7: OVL_LANE(16, 6, true, true, true); break;
+        case 8: OVL_LANE(32, 4, false, false, false); break;
+        case 10: OVL_LANE(32, 4, false, true, false); break;
+        case 12: OVL_LANE(32, 4, true, false, false); break;
+        case 13: OVL_LANE(32, 4, true, false, true); break;
+        case 14: OVL_LANE(32, 4, true, true, false); break;
+        case 15: OVL_LANE(32, 4, true, true, true); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef OVL_LANE
+    return hipGetLastError();
+}

@@ -64,6 +64,21 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream
 
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);
 extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out);
+// lane-per-pair full DP (ovl_dp_lane.hip): colbuf holds slots x ovl_dp_lane_rcap(mcap) x 64 dwords
+struct OvlLaneArgs {
+    int32_t cw;                 // strip width: 16 or 32 columns
+    int32_t prof;               // byte score profile (<= 4 symbols, diagonal scores in int8, indel <= 0)
+    int32_t col16;              // int16 hand-off column (|G| < 2^15)
+    int32_t sfx;                // (prof) row symbols from the resident suffix bit planes
+    const uint32_t* sfx_words;  // sfx layout of ovl_set_reads (2 planes), srow words per read, wsfx words
+    int32_t srow;
+    int32_t wsfx;
+    uint32_t* colbuf;
+    int64_t slots;              // resident wavefront slots (one hand-off column each)
+};
+extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
+extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);
+extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
 
 // candidate enumeration (ovl_candidates.hip)
 extern "C" hipError_t ovl_cand_keys(const uint8_t* codes, const int64_t* off, const int32_t* len, int32_t n_reads,

@@ -73,6 +73,20 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+def _share_torch_hip_runtime() -> None:
+    """Load torch's HIP runtime first when torch is installed.
+
+    torch's libc10_hip needs ``libamdhip64.so`` from torch/lib, while libovl needs the
+    soname ``libamdhip64.so.7``.  Loaded in that order both resolve to torch's copy; the
+    other order maps a second runtime, and the later one sees no GPU.  Only the import
+    happens here (no device is touched).
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load():
     """Load and type libovl.so; raises OvlError if it is absent.
 
@@ -86,6 +100,7 @@ def load():
             if not os.path.exists(path):
                 raise OvlError(-2, f"{path} not built: run __graft_entry__.build() "
                                    "(make -C genome-assembly-using-overlap-graphs_amd/csrc)")
+            _share_torch_hip_runtime()
             lib = ctypes.CDLL(path)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)
