@@ -41,7 +41,7 @@ struct ovl_ctx {
     std::string err;
     int32_t cu_count = 256;
     int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
-    int32_t band_form = -1;       // OVL_BAND_FORM env (diag|rows|fast|strip): band knob kernel (tests)
+    int32_t band_form = -1;       // OVL_BAND_FORM env (lane|diag|rows|fast|strip): band knob kernel (tests)
     int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
     int32_t dp_lane = -1;         // OVL_DP_LANE env: lane-per-pair full DP (-1 auto by list size, 0 off, 1 forced)
     int32_t lane_cw = 32;         // OVL_LANE_CW env: lane kernel strip width (16 or 32 columns)
@@ -320,11 +320,31 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
             const int64_t lanes = 2 * (int64_t)g.band + 1;
             const bool diag_ok = neg_ok && ovl_band_diag_slots(g.band, c->lmax, nullptr) > 0;
             const bool rows_ok = neg_ok && lanes <= 192 && c->lmax <= 1024;
+            // lane per pair: byte scores (match/mismatch - 2*indel, -2*indel, -indel in int8), indel <= 0,
+            // <= 4 symbols, G = dp - indel*(i+j) in int32 with j down to -(2*lmax + band)
+            const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
+            auto i8 = [](int64_t v) { return v >= -128 && v <= 127; };
+            const bool lane_ok = c->planes == 2 && g.band <= ovl_band_lane_max() && indel <= 0 && i8(sma) &&
+                                 i8(smm) && i8(-2 * indel) && (6 * L + 2 * g.band + 8) * Mx < (int64_t(1) << 30) &&
+                                 c->lmax <= kLaneMaxLen && c->codes_bytes + 64 < (int64_t(1) << 32);
             switch (c->band_form) {
                 case OVL_BAND_FORM_ROWS: g.band_form = rows_ok ? OVL_BAND_FORM_ROWS : OVL_BAND_FORM_STRIP; break;
                 case OVL_BAND_FORM_FAST: g.band_form = OVL_BAND_FORM_FAST; break;
                 case OVL_BAND_FORM_STRIP: g.band_form = OVL_BAND_FORM_STRIP; break;
-                default: g.band_form = diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST; break;
+                case OVL_BAND_FORM_DIAG: g.band_form = diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST; break;
+                case OVL_BAND_FORM_LANE:
+                    g.band_form = lane_ok ? OVL_BAND_FORM_LANE : (diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST);
+                    break;
+                default:
+                    g.band_form = (lane_ok && n_pairs >= c->lane_min_pairs)
+                                      ? OVL_BAND_FORM_LANE
+                                      : (diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST);
+                    break;
+            }
+            if (g.band_form == OVL_BAND_FORM_LANE) {
+                const int64_t slots = (int64_t)c->cu_count * 4 * 6;
+                HIPCHK(c, ovl_launch_band_lane(&g, slots, s));
+                return OVL_OK;
             }
         }
         HIPCHK(c, ovl_launch_dp(&g, s));
@@ -379,6 +399,7 @@ OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
         else if (!strcmp(e, "rows")) c->band_form = OVL_BAND_FORM_ROWS;
         else if (!strcmp(e, "fast")) c->band_form = OVL_BAND_FORM_FAST;
         else if (!strcmp(e, "strip")) c->band_form = OVL_BAND_FORM_STRIP;
+        else if (!strcmp(e, "lane")) c->band_form = OVL_BAND_FORM_LANE;
     }
     if (const char* e = getenv("OVL_DP_CLASSIC")) c->dp_classic = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_DP_LANE")) c->dp_lane = atoi(e) ? 1 : 0;

@@ -267,6 +267,154 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
     }
 }
 
+// ----------------------------------------------------------------------------- band knob, lane per pair
+//
+// The build's seed-and-extend band (oracle_overlap_banded; not a reference mode): cells with
+// |(i - j) - d*| <= W, d* = n - j*, j* the ungapped seed end already in out_end.  One lane owns a
+// pair; its NB = 2W+1 band cells of the current row sit in registers indexed by diagonal
+// k = j - i + d* + W, so a row needs no data from other lanes:
+//   V[k] <- max3(V[k] + s2(i, k), V[k+1], V[k-1])          (in place, k ascending)
+// diag is the same diagonal of the previous row, up is diagonal k+1 of the previous row (absent at
+// k = 2W) and left is diagonal k-1 of this row (absent at k = 0) -- exactly the band edges of the
+// oracle -- in G = dp - indel*(i+j) units (s2 = s - 2*indel).
+//
+// Scores: the t codes of the row's window sit as bytes in NBW words (byte k = t[j_k - 1]) and slide
+// down one byte per row; the row's profile is P = perm(TBL, T ^ x) -- byte (x ^ t) of an 8-byte
+// table: 0 -> match, 1..3 -> mismatch, 4..7 -> the pad code of positions left of t (s2 = -2*indel,
+// i.e. s = 0, which keeps dp = 0 for every j <= 0 cell: column 0 and the band cells left of it).
+// Virtual leading rows (end-aligned rows, i <= 0) use s2 = -indel, which maps row 0's G pattern
+// (-indel * j, diagonals shifting one column per row) onto itself, edge cells included.
+template <int NB, int OCC>
+__global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __restrict__ codes,
+                                                             const int64_t* __restrict__ off,
+                                                             const int32_t* __restrict__ len, int32_t n_reads,
+                                                             const int32_t* __restrict__ a_idx,
+                                                             const int32_t* __restrict__ b_idx, int64_t n_pairs,
+                                                             int32_t lcap, int32_t match, int32_t mismatch,
+                                                             int32_t indel, int32_t* __restrict__ out_score,
+                                                             int32_t* __restrict__ out_end,
+                                                             uint32_t* __restrict__ err_flag) {
+    constexpr int W = (NB - 1) / 2;
+    constexpr int NBW = (NB + 3) / 4;
+    constexpr uint32_t PAD = 4;  // t code left of the read
+    const int lane = threadIdx.x & 63;
+    const int64_t wslot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nslots = (int64_t)gridDim.x * 4;
+    const int64_t ntiles = (n_pairs + 63) >> 6;
+    const int32_t g = indel;
+    const uint32_t b_ma = (uint32_t)(match - 2 * g) & 0xFFu;
+    const uint32_t b_mm = (uint32_t)(mismatch - 2 * g) & 0xFFu;
+    const uint32_t b_pad = (uint32_t)(-2 * g) & 0xFFu;
+    const uint32_t tbl_lo = b_ma | (b_mm << 8) | (b_mm << 16) | (b_mm << 24);  // x ^ t = 0..3
+    const uint32_t tbl_hi = b_pad * 0x01010101u;                             // x ^ t = 4..7
+    const uint32_t p_virt = ((uint32_t)(-g) & 0xFFu) * 0x01010101u;
+    for (int64_t tile = wslot; tile < ntiles; tile += nslots) {
+        const int64_t p = tile * 64 + lane;
+        const bool live = p < n_pairs;
+        int32_t a = live ? a_idx[p] : 0;
+        int32_t b = live ? b_idx[p] : 0;
+        bool bad = live && (a < 0 || a >= n_reads || b < 0 || b >= n_reads);
+        if (!live || bad) { a = 0; b = 0; }
+        int32_t n = (live && !bad) ? len[a] : 0;
+        int32_t m = (live && !bad) ? len[b] : 0;
+        int32_t jstar = (live && !bad) ? out_end[p] : 0;
+        if (n > lcap || m > lcap || jstar < 0 || jstar > m) { bad = bad || live; n = 0; m = 0; jstar = 0; }
+        const uint32_t sa = (uint32_t)off[a];
+        const uint32_t tb = (uint32_t)off[b];
+        const int32_t cc = n - jstar + W;  // j = i - cc + k
+        const int32_t nmax = wave_max(n);
+        const int32_t nmin = wave_min(n);
+        const int32_t R = (nmax + 3) & ~3;  // row iterations (end-aligned rows)
+        const int32_t sk = R - n;
+        const int32_t mcut = R - nmin;
+        // t code of 0-based position u (the cell column is u + 1)
+        auto tcode = [&](int32_t u) -> uint32_t {
+            const int32_t uc = u < 0 ? 0 : (u >= m ? (m > 0 ? m - 1 : 0) : u);
+            const uint32_t v = (uint32_t)codes[tb + (uint32_t)uc];
+            return u < 0 ? PAD : v;
+        };
+        // row i = it - sk + 1; its window holds t positions u = i - cc - 1 + k
+        const int32_t u0 = -sk - cc;
+        uint32_t T[NBW];
+#pragma unroll
+        for (int w = 0; w < NBW; ++w) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * w + q < NB) word |= tcode(u0 + 4 * w + q) << (8 * q);
+            T[w] = word;
+        }
+        int32_t V[NB];
+#pragma unroll
+        for (int k = 0; k < NB; ++k) V[k] = -g * (u0 + k);  // row -sk (row 0 pattern): G = -indel * j
+        // prefetch queues: s codes of rows it..it+3 and the t codes entering the window after each row
+        uint32_t qs[4], qt[4];
+        auto fetch4 = [&](int32_t it4) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t i0 = it4 + k - sk;  // s index i - 1
+                const int32_t ic = i0 < 0 ? 0 : (i0 >= n ? (n > 0 ? n - 1 : 0) : i0);
+                qs[k] = (uint32_t)codes[sa + (uint32_t)ic];
+                qt[k] = tcode(it4 + k - sk - cc + NB);  // top cell of row it4 + k + 1
+            }
+        };
+        auto row = [&](int32_t it, uint32_t x, uint32_t tnew, auto masked_tag) {
+            constexpr bool MASKED = decltype(masked_tag)::value;
+            const uint32_t x4 = __builtin_amdgcn_perm(0u, x, 0u);  // x in every byte
+            uint32_t P[NBW];
+#pragma unroll
+            for (int w = 0; w < NBW; ++w) {
+                P[w] = __builtin_amdgcn_perm(tbl_hi, tbl_lo, T[w] ^ x4);
+                if constexpr (MASKED) P[w] = it < sk ? p_virt : P[w];
+            }
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                const int32_t d = V[k] + (int32_t)(int8_t)(uint8_t)(P[k >> 2] >> (8 * (k & 3)));
+                if constexpr (NB == 1) V[k] = d;
+                else if (k == 0) V[k] = max(d, V[k + 1]);
+                else if (k == NB - 1) V[k] = max(d, V[k - 1]);
+                else V[k] = max(max(d, V[k + 1]), V[k - 1]);
+            }
+            // slide the window one position and append the next row's top t code
+#pragma unroll
+            for (int w = 0; w < NBW; ++w) T[w] = __builtin_amdgcn_alignbit(w + 1 < NBW ? T[w + 1] : 0u, T[w], 8);
+            T[(NB - 1) >> 2] |= tnew << (8 * ((NB - 1) & 3));
+        };
+        auto body = [&](int32_t it, auto masked_tag) {
+            uint32_t s4[4], t4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { s4[k] = qs[k]; t4[k] = qt[k]; }
+            if (it + 4 < R) fetch4(it + 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row(it + k, s4[k], t4[k], masked_tag);
+        };
+        fetch4(0);
+        int32_t it = 0;
+        for (; it < mcut; it += 4) body(it, std::true_type{});
+        for (; it < R; it += 4) body(it, std::false_type{});
+        // row n: in-band cells with 0 <= j <= m, largest value, first j (the oracle's scan)
+        int32_t best = INT32_MIN, bend = -1;
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int32_t j = jstar - W + k;
+            const int32_t v = V[k] + g * (n + j);
+            const bool better = j >= 0 && j <= m && v > best;
+            best = better ? v : best;
+            bend = better ? j : bend;
+        }
+        if (live) {
+            if (bad) {
+                atomicOr(err_flag, 1u);
+                out_score[p] = -1;
+                out_end[p] = -1;
+            } else {
+                out_score[p] = best;
+                out_end[p] = bend;
+            }
+        }
+    }
+}
+
 }  // namespace ovl
 
 using ovl::dp_lane_kernel;
@@ -308,4 +456,37 @@ extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* 
     }
 #undef OVL_LANE
     return hipGetLastError();
+}
+
+// band knob, lane per pair: one instantiation per band half-width 0..kBandLaneMax
+namespace {
+constexpr int kBandLaneMax = 32;
+
+template <int W>
+hipError_t launch_band_lane_w(const OvlDpArgs* g, int64_t blocks, hipStream_t stream) {
+    constexpr int NB = 2 * W + 1;
+    constexpr int OCC = NB <= 25 ? 6 : (NB <= 57 ? 4 : 3);
+    ovl::band_lane_kernel<NB, OCC><<<(unsigned)blocks, 256, 0, stream>>>(
+        g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, (int32_t)g->match,
+        (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end, g->err_flag);
+    return hipGetLastError();
+}
+
+template <int W>
+hipError_t dispatch_band_lane(int band, const OvlDpArgs* g, int64_t blocks, hipStream_t stream) {
+    if (band == W) return launch_band_lane_w<W>(g, blocks, stream);
+    if constexpr (W < kBandLaneMax) return dispatch_band_lane<W + 1>(band, g, blocks, stream);
+    return hipErrorInvalidValue;
+}
+}  // namespace
+
+extern "C" int32_t ovl_band_lane_max(void) { return kBandLaneMax; }
+
+extern "C" hipError_t ovl_launch_band_lane(const OvlDpArgs* g, int64_t slots, hipStream_t stream) {
+    if (g->n_pairs <= 0) return hipSuccess;
+    if (g->band < 0 || g->band > kBandLaneMax) return hipErrorInvalidValue;
+    const int64_t tiles = (g->n_pairs + 63) / 64;
+    int64_t blocks = (std::min<int64_t>(slots, tiles) + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    return dispatch_band_lane<0>(g->band, g, blocks, stream);
 }

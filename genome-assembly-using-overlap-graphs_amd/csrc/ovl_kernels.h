@@ -31,6 +31,7 @@ enum {
     OVL_BAND_FORM_ROWS = 1,   // band_row_kernel: lanes on band diagonals, a row per step (<= 192 lanes)
     OVL_BAND_FORM_FAST = 2,   // dp_fast_kernel<int32_t, true>: chunked strips with band masks
     OVL_BAND_FORM_DIAG = 3,   // band_diag_kernel: lanes on band diagonals, an anti-diagonal per step
+    OVL_BAND_FORM_LANE = 4,   // band_lane_kernel: a lane per pair, band diagonals in registers (band <= 32)
 };
 
 struct OvlDpArgs {
@@ -79,6 +80,9 @@ struct OvlLaneArgs {
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
+// band knob, a lane per pair (ovl_dp_lane.hip): band <= ovl_band_lane_max(), <= 4 symbols, scores in int8
+extern "C" int32_t ovl_band_lane_max(void);
+extern "C" hipError_t ovl_launch_band_lane(const OvlDpArgs* args, int64_t slots, hipStream_t stream);
 
 // candidate enumeration (ovl_candidates.hip)
 extern "C" hipError_t ovl_cand_keys(const uint8_t* codes, const int64_t* off, const int32_t* len, int32_t n_reads,

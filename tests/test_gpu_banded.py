@@ -99,8 +99,8 @@ def test_banded_unsupported_magnitudes(engine):
         engine.score([0], [1], 2 ** 28, -1, -1, 4)
 
 
-FORMS = {"default": {}, "rows": {"OVL_BAND_FORM": "rows"}, "fast": {"OVL_BAND_FORM": "fast"},
-         "strip": {"OVL_BAND_FORM": "strip"}}
+FORMS = {"default": {}, "lane": {"OVL_BAND_FORM": "lane"}, "diag": {"OVL_BAND_FORM": "diag"},
+         "rows": {"OVL_BAND_FORM": "rows"}, "fast": {"OVL_BAND_FORM": "fast"}, "strip": {"OVL_BAND_FORM": "strip"}}
 
 
 def _score_with_env(env, reads, a, b, params, band):
@@ -119,9 +119,10 @@ def _score_with_env(env, reads, a, b, params, band):
 @pytest.mark.parametrize("band", [0, 1, 2, 3, 8, 15, 16, 31, 32, 33, 63, 64, 95, 96, 150, 255, 256])
 @pytest.mark.parametrize("form", sorted(FORMS))
 def test_band_forms_agree_with_oracle(oracle_mod, reads_pairs, band, form):
-    """The band knob has four kernels: the anti-diagonal form (default), the row form (lanes on band
-    diagonals, a row per step; up to 192 lanes), the chunked strip kernel with band masks and the
-    classic strip form, picked with OVL_BAND_FORM: each must equal the oracle."""
+    """The band knob has five kernels: a lane per pair (band <= 32; the default for >= 65,536 pairs),
+    the anti-diagonal form (the default below that), the row form (lanes on band diagonals, a row per
+    step; up to 192 lanes), the chunked strip kernel with band masks and the classic strip form,
+    picked with OVL_BAND_FORM: each must equal the oracle (lane falls back above band 32)."""
     reads, a, b = reads_pairs
     rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
     sc, en = _score_with_env(FORMS[form], reads, a, b, (10, -1, -2), band)
@@ -141,5 +142,25 @@ def test_banded_long_reads_vs_oracle(engine, oracle_mod, band):
     engine.set_reads(reads)
     sc, en = engine.score(a, b, 10, -1, -2, band)
     rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (5, -4, -1), (10, -1, -30), (3, 2, -1),
+                                    (5, -4, 0), (0, 0, -1), (-1, -2, -1), (100, -90, -60), (2, -1, 3)])
+@pytest.mark.parametrize("band", [0, 1, 4, 8, 13, 24, 32])
+def test_band_lane_kernel_vs_oracle(oracle_mod, params, band):
+    """The lane-per-pair band kernel over mixed lengths (empty reads, reads shorter than the band,
+    seed diagonals left and right of the table) and scorings inside and outside its int8 byte scores
+    (those fall back to the anti-diagonal form)."""
+    rng = random.Random(band * 31 + sum(params) % 97)
+    lens = [0, 1, 2, 3, 7, 16, 31, 33, 64, 100, 180, 250]
+    reads = ["".join(rng.choice("ACGT") for _ in range(rng.choice(lens))) for _ in range(160)]
+    reads += _indel_reads(rng, 100, 250)
+    n = len(reads)
+    a = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
+    b = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, *params, band)
+    sc, en = _score_with_env({"OVL_BAND_FORM": "lane"}, reads, a, b, params, band)
     np.testing.assert_array_equal(sc, rs)
     np.testing.assert_array_equal(en, re_)
