@@ -305,6 +305,7 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
             k.col16 = c->lane_col16 && (4 * L + 4) * M < (int64_t(1) << 15);
             k.sfx = k.prof && c->lane_sfx && c->wmax > 0;
             k.sfx_words = as<uint32_t>(c->sfx);
+            k.pfx_words = as<uint32_t>(c->pfx);
             k.srow = c->srow;
             k.wsfx = c->wmax;
             k.colbuf = as<uint32_t>(c->lane_col);
@@ -324,7 +325,7 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
             // <= 4 symbols, G = dp - indel*(i+j) in int32 with j down to -(2*lmax + band)
             const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
             auto i8 = [](int64_t v) { return v >= -128 && v <= 127; };
-            const bool lane_ok = c->planes == 2 && g.band <= ovl_band_lane_max() && indel <= 0 && i8(sma) &&
+            const bool lane_ok = c->planes == 2 && ovl_band_lane_ok(g.band) && indel <= 0 && i8(sma) &&
                                  i8(smm) && i8(-2 * indel) && (6 * L + 2 * g.band + 8) * Mx < (int64_t(1) << 30) &&
                                  c->lmax <= kLaneMaxLen && c->codes_bytes + 64 < (int64_t(1) << 32);
             switch (c->band_form) {
@@ -342,8 +343,14 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
                     break;
             }
             if (g.band_form == OVL_BAND_FORM_LANE) {
-                const int64_t slots = (int64_t)c->cu_count * 4 * 6;
-                HIPCHK(c, ovl_launch_band_lane(&g, slots, s));
+                OvlLaneArgs k{};
+                k.slots = (int64_t)c->cu_count * 4 * 6;
+                k.sfx = c->lane_sfx && c->wmax > 0;
+                k.sfx_words = as<uint32_t>(c->sfx);
+                k.pfx_words = as<uint32_t>(c->pfx);
+                k.srow = c->srow;
+                k.wsfx = c->wmax;
+                HIPCHK(c, ovl_launch_band_lane(&g, &k, s));
                 return OVL_OK;
             }
         }

@@ -284,11 +284,18 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
 // i.e. s = 0, which keeps dp = 0 for every j <= 0 cell: column 0 and the band cells left of it).
 // Virtual leading rows (end-aligned rows, i <= 0) use s2 = -indel, which maps row 0's G pattern
 // (-indel * j, diagonals shifting one column per row) onto itself, edge cells included.
-template <int NB, int OCC>
+//
+// PL: row symbols and the t codes entering the window come from the resident bit planes (sfx / pfx,
+// W words of 32 bases, two planes per word) instead of a byte gather per row each: with the row count
+// a multiple of 32 every lane reads bit it % 32 of its current 32-row words, 8 + 16 bytes per lane
+// per 32 rows (the t words funnel-shifted once per block by the lane's window offset).
+template <int NB, int OCC, bool PL>
 __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __restrict__ codes,
                                                              const int64_t* __restrict__ off,
                                                              const int32_t* __restrict__ len, int32_t n_reads,
-                                                             const int32_t* __restrict__ a_idx,
+                                                             const uint32_t* __restrict__ sfx,
+                                                             const uint32_t* __restrict__ pfx, int32_t prow,
+                                                             int32_t wpl, const int32_t* __restrict__ a_idx,
                                                              const int32_t* __restrict__ b_idx, int64_t n_pairs,
                                                              int32_t lcap, int32_t match, int32_t mismatch,
                                                              int32_t indel, int32_t* __restrict__ out_score,
@@ -324,7 +331,8 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
         const int32_t cc = n - jstar + W;  // j = i - cc + k
         const int32_t nmax = wave_max(n);
         const int32_t nmin = wave_min(n);
-        const int32_t R = (nmax + 3) & ~3;  // row iterations (end-aligned rows)
+        constexpr int RQ = PL ? 32 : 4;
+        const int32_t R = (nmax + RQ - 1) / RQ * RQ;  // row iterations (end-aligned rows)
         const int32_t sk = R - n;
         const int32_t mcut = R - nmin;
         // t code of 0-based position u (the cell column is u + 1)
@@ -348,18 +356,42 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
 #pragma unroll
         for (int k = 0; k < NB; ++k) V[k] = -g * (u0 + k);  // row -sk (row 0 pattern): G = -indel * j
         // prefetch queues: s codes of rows it..it+3 and the t codes entering the window after each row
-        uint32_t qs[4], qt[4];
+        // (the code entering after row it is at t position it + ub)
+        const int32_t ub = NB - sk - cc;
+        constexpr int NQ = PL ? 1 : 4;
+        uint32_t qs[NQ], qt[NQ];
         auto fetch4 = [&](int32_t it4) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < NQ; ++k) {
                 const int32_t i0 = it4 + k - sk;  // s index i - 1
                 const int32_t ic = i0 < 0 ? 0 : (i0 >= n ? (n > 0 ? n - 1 : 0) : i0);
                 qs[k] = (uint32_t)codes[sa + (uint32_t)ic];
-                qt[k] = tcode(it4 + k - sk - cc + NB);  // top cell of row it4 + k + 1
+                qt[k] = tcode(it4 + k + ub);  // top cell of row it4 + k + 1
             }
+        };
+        // PL: s planes of the 32-row block (sfx, right-aligned: block kb is word kb + wpl - R/32) and the
+        // t planes of the positions entering in that block, funnel-shifted to bit 0 (pfx, left-aligned)
+        const uint32_t* __restrict__ sp = sfx + (int64_t)a * prow + 2 * (wpl - R / 32);
+        const uint32_t* __restrict__ tp = pfx + (int64_t)b * prow;
+        const uint32_t tsh = (uint32_t)ub & 31u;
+        uint32_t S0 = 0, S1 = 0, T0 = 0, T1 = 0;      // current block
+        uint2 sn = make_uint2(0, 0), t0n = sn, t1n = sn;  // next block (raw words)
+        auto fetch_planes = [&](int32_t kb) {
+            sn = *reinterpret_cast<const uint2*>(sp + 2 * kb);
+            const int32_t q = (32 * kb + ub) >> 5;  // floor
+            const int32_t q0 = q < 0 ? 0 : (q >= wpl ? wpl - 1 : q);
+            const int32_t q1 = q + 1 < 0 ? 0 : (q + 1 >= wpl ? wpl - 1 : q + 1);
+            t0n = *reinterpret_cast<const uint2*>(tp + 2 * q0);
+            t1n = *reinterpret_cast<const uint2*>(tp + 2 * q1);
         };
         auto row = [&](int32_t it, uint32_t x, uint32_t tnew, auto masked_tag) {
             constexpr bool MASKED = decltype(masked_tag)::value;
+            if constexpr (PL) {
+                const uint32_t r = (uint32_t)it & 31u;
+                x = __builtin_amdgcn_ubfe(S0, r, 1) | (__builtin_amdgcn_ubfe(S1, r, 1) << 1);
+                tnew = __builtin_amdgcn_ubfe(T0, r, 1) | (__builtin_amdgcn_ubfe(T1, r, 1) << 1);
+                tnew = it + ub < 0 ? PAD : tnew;
+            }
             const uint32_t x4 = __builtin_amdgcn_perm(0u, x, 0u);  // x in every byte
             uint32_t P[NBW];
 #pragma unroll
@@ -381,14 +413,27 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
             T[(NB - 1) >> 2] |= tnew << (8 * ((NB - 1) & 3));
         };
         auto body = [&](int32_t it, auto masked_tag) {
-            uint32_t s4[4], t4[4];
+            if constexpr (PL) {
+                if ((it & 31) == 0) {  // next 32 rows: rotate the block words, prefetch the block after
+                    S0 = sn.x;
+                    S1 = sn.y;
+                    T0 = __builtin_amdgcn_alignbit(t1n.x, t0n.x, tsh);
+                    T1 = __builtin_amdgcn_alignbit(t1n.y, t0n.y, tsh);
+                    if (it + 32 < R) fetch_planes((it + 32) >> 5);
+                }
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { s4[k] = qs[k]; t4[k] = qt[k]; }
-            if (it + 4 < R) fetch4(it + 4);
+                for (int k = 0; k < 4; ++k) row(it + k, 0u, 0u, masked_tag);
+            } else {
+                uint32_t s4[4], t4[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) row(it + k, s4[k], t4[k], masked_tag);
+                for (int k = 0; k < 4; ++k) { s4[k] = qs[k]; t4[k] = qt[k]; }
+                if (it + 4 < R) fetch4(it + 4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) row(it + k, s4[k], t4[k], masked_tag);
+            }
         };
-        fetch4(0);
+        if constexpr (PL) fetch_planes(0);
+        else fetch4(0);
         int32_t it = 0;
         for (; it < mcut; it += 4) body(it, std::true_type{});
         for (; it < R; it += 4) body(it, std::false_type{});
@@ -460,33 +505,43 @@ extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* 
 
 // band knob, lane per pair: one instantiation per band half-width 0..kBandLaneMax
 namespace {
-constexpr int kBandLaneMax = 32;
+constexpr int kBandLaneMax = 64;
 
-template <int W>
-hipError_t launch_band_lane_w(const OvlDpArgs* g, int64_t blocks, hipStream_t stream) {
+template <int W, bool PL>
+hipError_t launch_band_lane_w(const OvlDpArgs* g, const OvlLaneArgs* k, int64_t blocks, hipStream_t stream) {
     constexpr int NB = 2 * W + 1;
-    constexpr int OCC = NB <= 25 ? 6 : (NB <= 57 ? 4 : 3);
-    ovl::band_lane_kernel<NB, OCC><<<(unsigned)blocks, 256, 0, stream>>>(
-        g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, (int32_t)g->match,
-        (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end, g->err_flag);
+    constexpr int OCC = NB <= 25 ? 6 : (NB <= 57 ? 4 : (NB <= 65 ? 3 : (NB <= 113 ? 2 : 1)));
+    ovl::band_lane_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
+        g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx,
+        g->n_pairs, g->mcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,
+        g->err_flag);
     return hipGetLastError();
 }
 
+// every half-width up to 32, then 40, 48, 56, 64 (other widths above 32 take the anti-diagonal form)
+constexpr int next_band_lane(int w) { return w < 32 ? w + 1 : w + 8; }
+
 template <int W>
-hipError_t dispatch_band_lane(int band, const OvlDpArgs* g, int64_t blocks, hipStream_t stream) {
-    if (band == W) return launch_band_lane_w<W>(g, blocks, stream);
-    if constexpr (W < kBandLaneMax) return dispatch_band_lane<W + 1>(band, g, blocks, stream);
+hipError_t dispatch_band_lane(int band, const OvlDpArgs* g, const OvlLaneArgs* k, int64_t blocks,
+                              hipStream_t stream) {
+    if (band == W)
+        return k->sfx ? launch_band_lane_w<W, true>(g, k, blocks, stream)
+                      : launch_band_lane_w<W, false>(g, k, blocks, stream);
+    if constexpr (W < kBandLaneMax) return dispatch_band_lane<next_band_lane(W)>(band, g, k, blocks, stream);
     return hipErrorInvalidValue;
 }
 }  // namespace
 
-extern "C" int32_t ovl_band_lane_max(void) { return kBandLaneMax; }
+extern "C" int32_t ovl_band_lane_ok(int32_t band) {
+    return band >= 0 && (band <= 32 || (band <= kBandLaneMax && band % 8 == 0)) ? 1 : 0;
+}
 
-extern "C" hipError_t ovl_launch_band_lane(const OvlDpArgs* g, int64_t slots, hipStream_t stream) {
+extern "C" hipError_t ovl_launch_band_lane(const OvlDpArgs* g, const OvlLaneArgs* k, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     if (g->band < 0 || g->band > kBandLaneMax) return hipErrorInvalidValue;
+    if (k->sfx && (!k->sfx_words || !k->pfx_words || k->wsfx * 32 < g->mcap)) return hipErrorInvalidValue;
     const int64_t tiles = (g->n_pairs + 63) / 64;
-    int64_t blocks = (std::min<int64_t>(slots, tiles) + 3) / 4;
+    int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 3) / 4;
     if (blocks < 1) blocks = 1;
-    return dispatch_band_lane<0>(g->band, g, blocks, stream);
+    return dispatch_band_lane<0>(g->band, g, k, blocks, stream);
 }

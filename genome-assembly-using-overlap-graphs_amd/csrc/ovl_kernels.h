@@ -71,7 +71,8 @@ struct OvlLaneArgs {
     int32_t prof;               // byte score profile (<= 4 symbols, diagonal scores in int8, indel <= 0)
     int32_t col16;              // int16 hand-off column (|G| < 2^15)
     int32_t sfx;                // (prof) row symbols from the resident suffix bit planes
-    const uint32_t* sfx_words;  // sfx layout of ovl_set_reads (2 planes), srow words per read, wsfx words
+    const uint32_t* sfx_words;  // sfx / pfx layouts of ovl_set_reads (2 planes), srow words per read, wsfx words
+    const uint32_t* pfx_words;
     int32_t srow;
     int32_t wsfx;
     uint32_t* colbuf;
@@ -80,9 +81,10 @@ struct OvlLaneArgs {
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
-// band knob, a lane per pair (ovl_dp_lane.hip): band <= ovl_band_lane_max(), <= 4 symbols, scores in int8
-extern "C" int32_t ovl_band_lane_max(void);
-extern "C" hipError_t ovl_launch_band_lane(const OvlDpArgs* args, int64_t slots, hipStream_t stream);
+// band knob, a lane per pair (ovl_dp_lane.hip): ovl_band_lane_ok(band), <= 4 symbols, scores in int8;
+// uses lane->slots, and lane->sfx (row symbols and t codes from the bit planes) with sfx/pfx_words
+extern "C" int32_t ovl_band_lane_ok(int32_t band);
+extern "C" hipError_t ovl_launch_band_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
 
 // candidate enumeration (ovl_candidates.hip)
 extern "C" hipError_t ovl_cand_keys(const uint8_t* codes, const int64_t* off, const int32_t* len, int32_t n_reads,

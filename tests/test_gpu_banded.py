@@ -149,10 +149,12 @@ def test_banded_long_reads_vs_oracle(engine, oracle_mod, band):
 @pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (5, -4, -1), (10, -1, -30), (3, 2, -1),
                                     (5, -4, 0), (0, 0, -1), (-1, -2, -1), (100, -90, -60), (2, -1, 3)])
 @pytest.mark.parametrize("band", [0, 1, 4, 8, 13, 24, 32])
-def test_band_lane_kernel_vs_oracle(oracle_mod, params, band):
+@pytest.mark.parametrize("planes", ["1", "0"])
+def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes):
     """The lane-per-pair band kernel over mixed lengths (empty reads, reads shorter than the band,
     seed diagonals left and right of the table) and scorings inside and outside its int8 byte scores
-    (those fall back to the anti-diagonal form)."""
+    (those fall back to the anti-diagonal form).  planes=1 reads row symbols and t codes from the
+    resident bit planes, planes=0 gathers code bytes (OVL_LANE_SFX)."""
     rng = random.Random(band * 31 + sum(params) % 97)
     lens = [0, 1, 2, 3, 7, 16, 31, 33, 64, 100, 180, 250]
     reads = ["".join(rng.choice("ACGT") for _ in range(rng.choice(lens))) for _ in range(160)]
@@ -161,6 +163,6 @@ def test_band_lane_kernel_vs_oracle(oracle_mod, params, band):
     a = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
     b = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
     rs, re_ = oracle_mod.batch_banded(reads, a, b, *params, band)
-    sc, en = _score_with_env({"OVL_BAND_FORM": "lane"}, reads, a, b, params, band)
+    sc, en = _score_with_env({"OVL_BAND_FORM": "lane", "OVL_LANE_SFX": planes}, reads, a, b, params, band)
     np.testing.assert_array_equal(sc, rs)
     np.testing.assert_array_equal(en, re_)
