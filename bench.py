@@ -398,6 +398,11 @@ def main() -> None:
                                "roofline_frac": xa / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel": x.kernel}
                 del x
             line["extra_configs"] = extra
+            if args.config != "cfg5" and not args.band_sweep:
+                # BASELINE configs[4]: the cfg5 band-width sweep at indel -2 (gaps can win), per-GPU kernels
+                x = Workload("cfg5", seed=0, dev=dev, engine=w.eng)
+                line["cfg5_band_sweep"] = band_sweep(x, [4, 8, 16, 32, 64, -1], args.sweep_indel, 3, dev)
+                del x
             w.eng.set_reads(w.reads)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(w.reads, w.a, w.b, args.cpu_budget)
