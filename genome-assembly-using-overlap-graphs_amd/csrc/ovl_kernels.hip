@@ -53,6 +53,14 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t 
     return __builtin_amdgcn_alignbit(hi, lo, r);
 }
 
+// popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
+// would otherwise sum a block's word counts with an extra v_add3)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t v, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(v), "v"(acc));
+    return r;
+}
+
 // ----------------------------------------------------------------------------- packing
 
 __global__ void map_codes_kernel(const uint8_t* __restrict__ raw, const uint8_t* __restrict__ lut,
@@ -313,10 +321,10 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
                 const int i = k + q - (W - 1);
                 uint32_t mm = __builtin_amdgcn_bitop3_b32(Sw[k * P + 1], U[i][1], Sw[k * P] ^ U[i][0], 0xBE);
                 if (i == 0) mm &= vt;
-                X += (uint32_t)__builtin_popcount(mm);
+                X = k == (W - 1 - q > 0 ? W - 1 - q : 0) ? (uint32_t)__builtin_popcount(mm) : bcnt_acc(mm, X);
             }
             if constexpr (KM == 0) {
-                kq[q] = ((int32_t)X * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24
+                kq[q] = ((((int32_t)X << 8) >> 8) * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24
             } else {
                 kq[q] = (int64_t)dms * 4294967296ll * (int64_t)X + rm;
             }
