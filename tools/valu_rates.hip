@@ -77,6 +77,15 @@ KERNEL(k_mix_xor_bcnt, "v_xor_b32 %0, %0, %1\n\tv_bcnt_u32_b32 %0, %1, %0")
 KERNEL(k_mix_xor_bitop3, "v_xor_b32 %0, %0, %1\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0xbe")
 KERNEL(k_mix_bcnt_alignbit, "v_bcnt_u32_b32 %0, %1, %0\n\tv_alignbit_b32 %0, %0, %1, %2")
 KERNEL(k_mix_add_max, "v_add_u32 %0, %0, %1\n\tv_max_i32 %0, %0, %1")
+// lane-DP cell candidates: SDWA byte add (+ max3), packed 16-bit add / max / mad, 16-bit max3
+#define SDWA_ADD "v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+KERNEL(k_sdwa_add, SDWA_ADD)
+KERNEL(k_pk_add, "v_pk_add_i16 %0, %0, %1")
+KERNEL(k_pk_max, "v_pk_max_i16 %0, %0, %1")
+KERNEL(k_pk_mad, "v_pk_mad_i16 %0, %0, %1, %2")
+KERNEL(k_max3_i16, "v_max3_i16 %0, %0, %1, %2")
+KERNEL(k_mix_sdwa_max3, SDWA_ADD "\n\tv_max3_i32 %0, %0, %1, %2")
+KERNEL(k_mix_pk_add_max, "v_pk_add_i16 %0, %0, %1\n\tv_pk_max_i16 %0, %0, %2")
 
 // shader clock: s_memtime ticks over a fixed VALU loop, one wave per SIMD
 __global__ __launch_bounds__(64) void k_clock(unsigned long long* out, unsigned seed) {
@@ -107,6 +116,9 @@ int main() {
         {"v_or_b32", k_or}, {"v_mov_b32", k_mov}, {"v_lshrrev_b32", k_lshrrev},
         {"mix xor+bcnt", k_mix_xor_bcnt}, {"mix xor+bitop3", k_mix_xor_bitop3},
         {"mix bcnt+alignbit", k_mix_bcnt_alignbit}, {"mix add+max", k_mix_add_max},
+        {"v_add_u32_sdwa", k_sdwa_add}, {"v_pk_add_i16", k_pk_add}, {"v_pk_max_i16", k_pk_max},
+        {"v_pk_mad_i16", k_pk_mad}, {"v_max3_i16", k_max3_i16}, {"mix sdwa+max3", k_mix_sdwa_max3},
+        {"mix pk_add+pk_max", k_mix_pk_add_max},
     };
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
