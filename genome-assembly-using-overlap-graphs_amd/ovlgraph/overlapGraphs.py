@@ -16,8 +16,11 @@ Also provided: ``construct_overlap_graph_string`` (:196-232) and
 ``combinations`` and keep edges with ``score > 0``; and ``build_overlap_graph``,
 the name BASELINE.json's north_star uses, as an alias.
 
-Layout, cycle removal and contig walking (:64-193) consume this graph and are
-out of scope.
+``remove_cycles_from_graph`` (:106-130) removes the same edges as the
+reference's find_cycle / remove-weakest-edge loop, through an exact replay of
+that loop in native code (``ovl_remove_cycles``) that does not restart its DFS
+after each removal.  Topological sorting and contig walking (:64-103, :133-193)
+stay networkx/Python.
 """
 from __future__ import annotations
 
@@ -285,3 +288,42 @@ def construct_string_graph(reads, engine: Optional[OverlapEngine] = None, scorer
                      for x, y, s, e in zip(a.tolist(), b.tolist(), sc, en) if s > 0)
     print(f"graph: {G.edges}")
     return G
+
+
+def remove_cycles_from_graph(overlap_graph):
+    """Remove the weakest edge of the first cycle networkx's ``find_cycle`` reports until the
+    graph is a DAG (overlapGraphs.py:106-130), in place; returns the graph.
+
+    Removes exactly the reference's edges (same cycles, same ``weight`` minimum, first in cycle
+    order on ties), in the same order, by replaying its DFS in ``ovl_remove_cycles`` (C++,
+    csrc/ovl_graph.cpp).  ``weight`` must be an integer on every edge.
+    """
+    from . import _lib
+    import ctypes
+    G = overlap_graph
+    nodes = list(G)
+    index = {v: i for i, v in enumerate(nodes)}
+    adj = G._adj
+    deg = np.fromiter((len(adj[u]) for u in nodes), dtype=np.int64, count=len(nodes))
+    off = np.zeros(len(nodes) + 1, dtype=np.int64)
+    np.cumsum(deg, out=off[1:])
+    n_edges = int(off[-1])
+    heads = np.fromiter((index[v] for u in nodes for v in adj[u]), dtype=np.int32, count=n_edges)
+    wlist = [d["weight"] for u in nodes for d in adj[u].values()]
+    if not all(isinstance(w, (int, np.integer)) and not isinstance(w, bool) for w in wlist):
+        raise TypeError("remove_cycles_from_graph needs an integer 'weight' on every edge")
+    weights = np.array(wlist, dtype=np.int64) if wlist else np.zeros(0, dtype=np.int64)
+    removed = np.zeros(max(n_edges, 1), dtype=np.int64)
+    n_removed = ctypes.c_int64(0)
+    L = _lib.load()
+    _lib.check(L.ovl_remove_cycles(off.ctypes.data_as(ctypes.c_void_p), heads.ctypes.data_as(ctypes.c_void_p),
+                                   weights.ctypes.data_as(ctypes.c_void_p), len(nodes),
+                                   removed.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n_removed)))
+    if n_removed.value:
+        # CSR index -> (u, v): the tail is the node whose adjacency range holds the index
+        idx = removed[: n_removed.value]
+        tails = np.searchsorted(off, idx, side="right") - 1
+        for t, e in zip(tails.tolist(), idx.tolist()):
+            G.remove_edge(nodes[t], nodes[heads[e]])
+    return G
+

@@ -155,6 +155,16 @@ int ovl_local_align(ovl_ctx* ctx, const uint8_t* query, int32_t n, const uint8_t
                     int32_t* out_end_j, int32_t* out_start_i, int32_t* out_start_j, int8_t* ops,
                     int64_t ops_cap, int64_t* out_n_ops);
 
+/* Cycle removal of overlapGraphs.py:106-130 (remove_cycles_from_graph), host-side, no context.
+ * Replaces:  while True: cycle = nx.find_cycle(G, orientation='original') ... G.remove_edge(u, v)
+ * The graph is CSR: n_nodes nodes in the DiGraph's node order; node v's out-edges are
+ * head[off[v] .. off[v+1]) in its adjacency (insertion) order with integer weight[] ("weight").
+ * Writes to removed[] (capacity off[n_nodes]) the CSR indices of the edges the reference loop
+ * removes, in its removal order, and their count to *n_removed: networkx 3.x find_cycle's
+ * cycle (edge DFS from the first unexplored node in node order), its first minimum-weight edge. */
+int ovl_remove_cycles(const int64_t* off, const int32_t* head, const int64_t* weight, int32_t n_nodes,
+                      int64_t* removed, int64_t* n_removed);
+
 #ifdef __cplusplus
 }
 #endif

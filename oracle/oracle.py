@@ -343,3 +343,18 @@ def graph_nx_k(reads: Sequence[str], k: int = 5,
                     for y in range(cb):
                         G.add_edge(f"{ra}_{x}", f"{rb}_{y}", weight=sc, end_position=en)
     return G, copies
+
+
+def remove_cycles(G):
+    """Restatement of overlapGraphs.py:106-130 (remove_cycles_from_graph), the reference loop itself:
+    networkx's find_cycle (orientation 'original'), then the cycle's first minimum-'weight' edge is
+    removed, until no cycle is left.  In place; returns G.  Quadratic: small graphs only."""
+    import networkx as nx
+    while True:
+        try:
+            cycle = nx.find_cycle(G, orientation="original")
+        except nx.NetworkXNoCycle:
+            break
+        u, v, _ = min(((u, v, G[u][v]["weight"]) for u, v, _ in cycle), key=lambda x: x[2])
+        G.remove_edge(u, v)
+    return G

@@ -1,0 +1,118 @@
+"""remove_cycles_from_graph (overlapGraphs.py:106-130): the native exact replay (csrc/ovl_graph.cpp,
+ovl_remove_cycles; host code, no GPU) removes exactly the reference's edges.
+
+Pinned by tests/golden/cycles.json, written by oracle/gen_golden_cycles.py from the reference's own
+function; the oracle's restatement (the same networkx loop) is checked against those records too and
+then used for larger random graphs and PhiX overlap graphs.
+"""
+import random
+
+import networkx as nx
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+
+@pytest.fixture(scope="module")
+def golden_cycles():
+    return load_golden("cycles.json")["records"]
+
+
+def _rebuild(rec):
+    G = nx.DiGraph()
+    G.add_nodes_from(rec["nodes"])
+    for u, nbrs in zip(rec["nodes"], rec["adj"]):
+        for v, w in nbrs:
+            G.add_edge(u, v, weight=w)
+    return G
+
+
+def _same(G1, G2):
+    return (list(G1.nodes()) == list(G2.nodes()) and list(G1.edges(data=True)) == list(G2.edges(data=True))
+            and all(list(G1.pred[n]) == list(G2.pred[n]) for n in G1))
+
+
+def test_native_matches_reference_golden(golden_cycles):
+    from ovlgraph.overlapGraphs import remove_cycles_from_graph
+    assert len(golden_cycles) >= 60
+    for rec in golden_cycles:
+        G = remove_cycles_from_graph(_rebuild(rec))
+        assert [[u, v] for u, v in G.edges()] == rec["kept"], rec["name"]
+        assert nx.is_directed_acyclic_graph(G)
+
+
+def test_oracle_matches_reference_golden(oracle_mod, golden_cycles):
+    for rec in golden_cycles:
+        if rec["reference_seconds"] > 0.5:
+            continue
+        G = oracle_mod.remove_cycles(_rebuild(rec))
+        assert [[u, v] for u, v in G.edges()] == rec["kept"], rec["name"]
+
+
+def _random_graph(rng, n, p, loops=0.1, wlo=-3, whi=5):
+    G = nx.DiGraph()
+    order = list(range(n))
+    rng.shuffle(order)
+    G.add_nodes_from(order)
+    edges = [(u, v) for u in range(n) for v in range(n) if (u != v or rng.random() < loops) and rng.random() < p]
+    rng.shuffle(edges)
+    for u, v in edges:
+        G.add_edge(u, v, weight=rng.randint(wlo, whi), end_position=u)
+    return G
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_native_matches_oracle_random(oracle_mod, seed):
+    from ovlgraph.overlapGraphs import remove_cycles_from_graph
+    rng = random.Random(seed)
+    for _ in range(40):
+        G = _random_graph(rng, rng.randint(1, 60), rng.choice([0.02, 0.05, 0.1, 0.3, 0.6]),
+                          whi=rng.choice([0, 1, 5, 1000]))
+        assert _same(oracle_mod.remove_cycles(G.copy()), remove_cycles_from_graph(G.copy()))
+
+
+def test_native_matches_oracle_overlap_graph(oracle_mod):
+    """A PhiX overlap graph (1,200 reads, l = 100, p = 0.01, k = 5) with its copies and attributes."""
+    from ovlgraph import overlapGraphs as og
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import read_genome_from_fasta, simulate_reads
+    reads, copies = dedup_reads(simulate_reads(read_genome_from_fasta(), 100, 1200, 0.01, seed=9))
+    a, b = enumerate_candidates(reads, 5)
+    sc, en = oracle_mod.batch_ungapped(reads, a, b, 10, -1)
+    G = og.assemble_graph(reads, copies, a, b, sc, en)
+    H = og.remove_cycles_from_graph(G.copy())
+    assert H.number_of_edges() < G.number_of_edges()
+    assert _same(oracle_mod.remove_cycles(G.copy()), H)
+
+
+def test_degenerate_graphs_and_errors():
+    from ovlgraph.overlapGraphs import remove_cycles_from_graph
+    assert remove_cycles_from_graph(nx.DiGraph()).number_of_nodes() == 0
+    G = nx.DiGraph()
+    G.add_nodes_from("abc")
+    assert list(remove_cycles_from_graph(G).nodes()) == ["a", "b", "c"]
+    G.add_edge("a", "a", weight=3)
+    assert remove_cycles_from_graph(G).number_of_edges() == 0
+    G.add_edge("a", "b", weight=1.5)
+    G.add_edge("b", "a", weight=2)
+    with pytest.raises(TypeError):
+        remove_cycles_from_graph(G)
+
+
+def test_abi_rejects_bad_csr():
+    import ctypes
+    from ovlgraph import _lib
+    L = _lib.load()
+    off = np.array([0, 2, 1], dtype=np.int64)  # decreasing offsets
+    head = np.array([1, 0], dtype=np.int32)
+    w = np.array([1, 1], dtype=np.int64)
+    rem = np.zeros(2, dtype=np.int64)
+    n = ctypes.c_int64()
+    p = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    assert L.ovl_remove_cycles(p(off), p(head), p(w), 2, p(rem), ctypes.byref(n)) == -1  # OVL_E_ARG
+    off = np.array([0, 1, 2], dtype=np.int64)
+    head = np.array([1, 5], dtype=np.int32)  # head out of range
+    assert L.ovl_remove_cycles(p(off), p(head), p(w), 2, p(rem), ctypes.byref(n)) < 0
+    head = np.array([1, 0], dtype=np.int32)
+    assert L.ovl_remove_cycles(p(off), p(head), p(w), 2, p(rem), ctypes.byref(n)) == 0 and n.value == 1
