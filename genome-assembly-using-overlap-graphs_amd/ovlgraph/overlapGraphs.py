@@ -327,3 +327,59 @@ def remove_cycles_from_graph(overlap_graph):
             G.remove_edge(nodes[t], nodes[heads[e]])
     return G
 
+
+def topological_sort(dag):
+    """overlapGraphs.py:133-148: networkx's topological order, ValueError on a cycle."""
+    print("Sorting graph topologically...")
+    try:
+        return list(nx.topological_sort(dag))
+    except nx.NetworkXUnfeasible:
+        raise ValueError("Graph is not a DAG! Cycles still exist.")
+
+
+def create_contig(start_read, dag, visited, topo_order):
+    """overlapGraphs.py:64-103: greedy walk from ``start_read`` to the unvisited successor read that is
+    first in topological order, appending each read past the edge's ``end_position``."""
+    contig = start_read.split("_")[0]
+    visited.add(start_read.split("_")[0])
+    neighbors = list(dag.neighbors(start_read))
+    while neighbors:
+        valid = [nb for nb in neighbors if nb.split("_")[0] not in visited]
+        if not valid:
+            break
+        next_read = min(valid, key=lambda nb: topo_order.get(nb.split("_")[0], float("inf")))
+        end = dag.edges[start_read, next_read]["end_position"]
+        contig += next_read.split("_")[0][end:]
+        start_read = next_read
+        neighbors = list(dag.neighbors(start_read))
+        visited.add(start_read.split("_")[0])
+    return contig
+
+
+def assemble_contigs_using_overlap_graphs(reads, k=5, params=None, engine: Optional[OverlapEngine] = None,
+                                          scorer=None):
+    """overlapGraphs.py:151-193: overlap graph (GPU candidates + scoring), cycle removal (native
+    replay), topological order, greedy contig walks -- the same contigs in the same order.
+    ``params`` (the reference's experiment dict) only feeds the progress lines; ``scorer`` is the
+    graph builders' hook for (score, end) from another backend."""
+    def say(step):
+        if params is not None:
+            print(f"{step} for experiment_name={params['experiment_name']} - N={params['N']}, l={params['l']}, "
+                  f"p={params['error_prob']}, k={params['k']}, num_iteration={params['num_iteration']}...")
+    say("Constructing overlap graph")
+    overlap_graph, read_copies = construct_overlap_graph_nx_k(reads, k=k, engine=engine, scorer=scorer)
+    say("Removing cycles from graph")
+    dag = remove_cycles_from_graph(overlap_graph)
+    topo_with_copies = {node: i for i, node in enumerate(nx.topological_sort(dag))}
+    topo_order: Dict[str, int] = {}
+    for read_with_copy, i in topo_with_copies.items():
+        topo_order[read_with_copy.split("_")[0]] = i
+    say("Creating contig")
+    visited: set = set()
+    contigs = []
+    for read in topo_order.keys():
+        if read not in visited:
+            for copy_index in range(read_copies[read]):
+                contigs.append(create_contig(f"{read}_{copy_index}", dag, visited, topo_order))
+    return contigs
+

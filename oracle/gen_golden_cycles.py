@@ -76,8 +76,38 @@ def overlap_graph(n_reads, seed):
     return H
 
 
+def assembly_cases(aligners, overlapGraphs, gefr):
+    """assemble_contigs_using_overlap_graphs end to end on small read sets (scoring typed as Numba does,
+    as in gen_golden.py)."""
+    import contextlib
+    import functools
+    import io
+    import numpy as np
+    from gen_golden import REF
+    overlapGraphs.overlap_alignment = functools.partial(aligners.overlap_alignment, indel=np.int64(-(2 ** 31)))
+    genome = gefr.read_genome_from_fasta(os.path.join(REF, "sequence.fasta"))
+    rng = random.Random(7)
+    cases = []
+    for n_reads, l, p, k in ((120, 100, 0.0, 5), (200, 80, 0.01, 5), (150, 60, 0.02, 3)):
+        reads = []
+        for _ in range(n_reads):
+            st = rng.randrange(len(genome))
+            r = genome[st:st + l]
+            r = "".join(rng.choice([c for c in "ACGT" if c != ch]) if rng.random() < p else ch for ch in r)
+            reads.append(r)
+        reads += reads[:3]  # copies
+        params = {"N": len(reads), "l": l, "k": k, "error_prob": p, "experiment_name": "golden", "num_iteration": 0}
+        t0 = time.time()
+        with contextlib.redirect_stdout(io.StringIO()):
+            contigs = overlapGraphs.assemble_contigs_using_overlap_graphs(reads, k=k, params=params)
+        cases.append({"reads": reads, "k": k, "params": params, "contigs": list(contigs),
+                      "reference_seconds": round(time.time() - t0, 2)})
+        print("assembly", n_reads, l, p, k, len(contigs), "contigs", f"{time.time() - t0:.1f} s", flush=True)
+    return cases
+
+
 def main():
-    _, overlapGraphs, _ = import_reference()
+    aligners, overlapGraphs, gefr = import_reference()
     rng = random.Random(20261016)
     inputs = []
     for i in range(60):
@@ -102,6 +132,10 @@ def main():
     with open(os.path.join(GOLDEN, "cycles.json"), "w") as fh:
         json.dump({"source": "reference overlapGraphs.remove_cycles_from_graph (networkx "
                              f"{nx.__version__})", "records": records}, fh, separators=(",", ":"))
+    with open(os.path.join(GOLDEN, "assembly.json"), "w") as fh:
+        json.dump({"source": "reference overlapGraphs.assemble_contigs_using_overlap_graphs (numba absent: njit "
+                             "identity, scoring args as np.int64)",
+                   "cases": assembly_cases(aligners, overlapGraphs, gefr)}, fh, separators=(",", ":"))
 
 
 if __name__ == "__main__":

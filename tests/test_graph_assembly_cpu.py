@@ -110,3 +110,19 @@ def test_overlap_edges_k_golden_graphs(golden_graphs, oracle_mod):
             continue
         E = og.overlap_edges_k(rec["reads"], scorer=_oracle_scorer(oracle_mod), **rec["kwargs"])
         assert_graph_matches_record(E.to_digraph(), rec, E.read_copies())
+
+
+def test_assembly_pipeline_matches_reference_contigs(oracle_mod):
+    """assemble_contigs_using_overlap_graphs (overlapGraphs.py:151-193): graph, native cycle removal,
+    topological order and contig walks give the reference's contigs (tests/golden/assembly.json,
+    written by oracle/gen_golden_cycles.py from the reference function), with oracle scores."""
+    from conftest import load_golden
+    cases = load_golden("assembly.json")["cases"]
+    assert len(cases) == 3
+    for case in cases:
+        out = io.StringIO()
+        with contextlib.redirect_stdout(out):
+            contigs = og.assemble_contigs_using_overlap_graphs(case["reads"], k=case["k"], params=case["params"],
+                                                               scorer=_oracle_scorer(oracle_mod))
+        assert contigs == case["contigs"]
+        assert "Removing cycles from graph for experiment_name=golden" in out.getvalue()
