@@ -216,7 +216,8 @@ def candidate_timing(w: Workload, reps: int = 5):
 def end_to_end(w: Workload, seed: int = 0):
     """``construct_overlap_graph_nx_k`` for this workload, split into its stages (not the metric):
     dedup + device enumeration + scoring with results on the host, then the DiGraph via the
-    direct builder and, for comparison, via networkx ``add_edges_from`` (the reference's way)."""
+    direct builder and, for comparison, via networkx ``add_edges_from`` (the reference's way);
+    then cycle removal on that graph and the whole ``assemble_contigs_using_overlap_graphs``."""
     from ovlgraph import overlapGraphs as og
     from ovlgraph.reads import config_reads
     raw = config_reads(w.name, seed=seed)
@@ -229,11 +230,26 @@ def end_to_end(w: Workload, seed: int = 0):
     t3 = time.perf_counter()
     n_e = G.number_of_edges()
     assert n_e == G2.number_of_edges()
-    del G, G2
+    del G2
+    # the rest of the reference pipeline (overlapGraphs.py:151-193): cycle removal (native replay of
+    # overlapGraphs.py:106-130), topological order, contig walks
+    t4 = time.perf_counter()
+    og.remove_cycles_from_graph(G)
+    t5 = time.perf_counter()
+    n_dag = G.number_of_edges()
+    del G
+    import contextlib
+    import io
+    t6 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        contigs = og.assemble_contigs_using_overlap_graphs(raw, w.cfg["k"], engine=w.eng)
+    t7 = time.perf_counter()
     return {"reads": len(raw), "pairs": len(edges), "edges": n_e,
             "dedup_enumerate_score_s": round(t1 - t0, 4), "digraph_direct_s": round(t2 - t1, 4),
             "digraph_networkx_s": round(t3 - t2, 4),
-            "end_to_end_s": round(t2 - t0, 4)}
+            "end_to_end_s": round(t2 - t0, 4),
+            "remove_cycles_s": round(t5 - t4, 4), "edges_removed": n_e - n_dag,
+            "assemble_contigs_s": round(t7 - t6, 4), "contigs": len(contigs)}
 
 
 def local_alignment_timing(eng, reps: int = 5):
