@@ -389,6 +389,7 @@ def main() -> None:
                 "algorithmic_bytes_per_launch": algo,
             },
             "valu_roofline": valu_roofline(args.config, kernel_ms),
+            "occupancy": load_profile(args.config).get("occupancy"),
             "host_setup_s": {"read_sim_and_enumeration": round(w.t_enum, 3), "upload_and_pack": round(w.t_pack, 4)},
         }
         if world == 1:
