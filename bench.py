@@ -282,6 +282,42 @@ def local_alignment_timing(eng, reps: int = 5):
             "gpu_cells_per_s_score_only": cells / sc_s, "cpu_port_ms_1core": cpu_s * 1e3}
 
 
+def device_list_timing(eng, name: str, steps: int, dev):
+    """A whole config scored from its device-enumerated candidate list (no host list): BASELINE
+    configs[3] (cfg4, 38 M pairs) fits one GPU; the 8-GPU run shards the same list 8 ways."""
+    import torch
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.reads import CONFIGS, config_reads
+    t0 = time.perf_counter()
+    reads, _ = dedup_reads(config_reads(name, seed=0))
+    eng.set_reads(reads)
+    n = eng.enumerate_candidates(CONFIGS[name]["k"])
+    torch.cuda.synchronize(dev)
+    t_setup = time.perf_counter() - t0
+    pa, pb, n = eng.candidates_device()
+    ds = torch.empty(n, dtype=torch.int32, device=dev)
+    de = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    launch = lambda: eng.score_device(pa, pb, n, ds.data_ptr(), de.data_ptr(), stream=stream.cuda_stream)
+    launch()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        launch()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    km = ev0.elapsed_time(ev1) / steps
+    lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
+    algo = int(n) * (2 * int((lens.max() + 3) // 4) + 16)  # uniform-length estimate of SURVEY §8d bytes
+    return {"workload": WORKLOAD_DESC[name], "reads": len(reads), "pairs": int(n),
+            "setup_s (simulate, upload, device enumeration)": round(t_setup, 3),
+            "value": n * steps / el, "kernel_ms": km, "kernel_pairs_per_s": n / (km * 1e-3),
+            "roofline_frac": algo / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
     """Config 5's band-width sweep: the same resident pairs at each band (-1 = full DP).
 
@@ -415,6 +451,8 @@ def main() -> None:
                                "roofline_frac": xa / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernel": x.kernel}
                 del x
             line["extra_configs"] = extra
+            if args.config != "cfg4":
+                extra["cfg4"] = device_list_timing(w.eng, "cfg4", 10, dev)
             if args.config != "cfg5" and not args.band_sweep:
                 # BASELINE configs[4]: the cfg5 band-width sweep at indel -2 (gaps can win), per-GPU kernels
                 x = Workload("cfg5", seed=0, dev=dev, engine=w.eng)
