@@ -15,6 +15,15 @@
 //    DFS event for event up to the moment the removed edge was yielded (that edge lies on the active
 //    path: the cycle is a suffix of it).  So the DFS state is rewound to that moment through an undo log
 //    (iterator advances, first visits, 'seen' insertions), the edge is marked dead, and the DFS goes on.
+//  * Settled nodes.  A node that cannot reach any cycle of the current graph (no path to a
+//    non-trivial strongly connected component or a self-loop) never closes a cycle and is never on
+//    the path when one closes; removals only delete edges, so it stays that way.  An edge into such
+//    a node is skipped like an edge into an explored node: the reference's excursion below it
+//    appends and later pops path edges whose heads cannot be the next yield's tail (that node
+//    reaches them, so they would be on a cycle with it), leaving the path and active set exactly as
+//    they are without the excursion.  The settled set is recomputed (Tarjan SCC + reverse
+//    reachability over the live edges, linear) whenever the DFS has yielded as many edges as the
+//    graph has since the last computation, which keeps it within a constant factor of the DFS work.
 //  * DFS semantics are networkx 3.x edge_dfs + find_cycle for a DiGraph: one out-edge iterator per node,
 //    created at its first visit and resumed when the node is pushed again; an edge into an explored
 //    node is skipped (its excursion only yields skipped edges); an edge into an active-path node closes
@@ -22,7 +31,10 @@
 //
 // Input is the graph in CSR form: nodes in G's node order, each node's out-edges in its adjacency
 // (insertion) order, edge weights.  Output is the removed edges (CSR indices) in removal order.
+#include <stddef.h>
 #include <stdint.h>
+
+#include <stdlib.h>
 
 #include <vector>
 
@@ -35,6 +47,84 @@ struct Event {
     int32_t node;
     int64_t old;
 };
+
+// settled[v] = 1 iff v cannot reach a cycle over the live edges.  tail/rev: reverse CSR (edge
+// indices grouped by head).  Iterative Tarjan, then reverse reachability from the cyclic nodes.
+// Nodes already settled or explored cannot reach a cycle (explored nodes were all reached by a start
+// whose DFS found none), so they and the edges into them are left out.
+void settle(const int64_t* off, const int32_t* head, const uint8_t* alive, int32_t n,
+            const std::vector<int32_t>& tail, const std::vector<int64_t>& roff, const std::vector<int64_t>& rev,
+            const std::vector<uint8_t>& explored, std::vector<uint8_t>& settled) {
+    if ((int32_t)settled.size() != n) settled.assign(n, 0);
+    std::vector<uint8_t> done(n);
+    for (int32_t v = 0; v < n; ++v) done[v] = settled[v] | explored[v];
+    std::vector<int32_t> idx(n, -1), low(n, 0), st;
+    std::vector<uint8_t> on(n, 0), bad(n, 0);
+    std::vector<int64_t> it(n, 0);
+    std::vector<int32_t> call;
+    int32_t counter = 0;
+    for (int32_t r = 0; r < n; ++r) {
+        if (idx[r] >= 0 || done[r]) continue;
+        call.push_back(r);
+        idx[r] = low[r] = counter++;
+        it[r] = off[r];
+        st.push_back(r);
+        on[r] = 1;
+        while (!call.empty()) {
+            const int32_t v = call.back();
+            bool descended = false;
+            while (it[v] < off[v + 1]) {
+                const int64_t e = it[v]++;
+                if (!alive[e]) continue;
+                const int32_t w = head[e];
+                if (done[w]) continue;
+                if (w == v) { bad[v] = 1; continue; }   // self-loop
+                if (idx[w] < 0) {
+                    idx[w] = low[w] = counter++;
+                    it[w] = off[w];
+                    st.push_back(w);
+                    on[w] = 1;
+                    call.push_back(w);
+                    descended = true;
+                    break;
+                }
+                if (on[w] && idx[w] < low[v]) low[v] = idx[w];
+            }
+            if (descended) continue;
+            call.pop_back();
+            if (!call.empty()) {
+                const int32_t u = call.back();
+                if (low[v] < low[u]) low[u] = low[v];
+            }
+            if (low[v] == idx[v]) {  // v roots a component: pop it
+                size_t size = 0, top = st.size();
+                while (true) {
+                    const int32_t w = st[--top];
+                    on[w] = 0;
+                    ++size;
+                    if (w == v) break;
+                }
+                if (size > 1)
+                    for (size_t k = top; k < st.size(); ++k) bad[st[k]] = 1;
+                st.resize(top);
+            }
+        }
+    }
+    // everything that reaches a cyclic node
+    std::vector<int32_t> queue;
+    for (int32_t v = 0; v < n; ++v)
+        if (bad[v]) queue.push_back(v);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int32_t v = queue[qi];
+        for (int64_t k = roff[v]; k < roff[v + 1]; ++k) {
+            const int64_t e = rev[k];
+            if (!alive[e]) continue;
+            const int32_t u = tail[e];
+            if (!bad[u] && !done[u]) { bad[u] = 1; queue.push_back(u); }
+        }
+    }
+    for (int32_t v = 0; v < n; ++v) settled[v] = !bad[v];
+}
 
 }  // namespace
 
@@ -55,6 +145,8 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<uint8_t> alive(n_edges, 1), explored(n_nodes, 0), visited(n_nodes, 0), active(n_nodes, 0),
         seen(n_nodes, 0);
     std::vector<int64_t> pos(n_nodes, 0);  // out-edge iterator position (CSR index) of visited nodes
+    std::vector<int64_t> skip(n_edges + 1);   // skip[e] == e for live edges (and the end), else > e
+    for (int64_t e = 0; e <= n_edges; ++e) skip[e] = e;
     std::vector<int64_t> path;             // find_cycle's `edges`: the active path, as CSR indices
     std::vector<int64_t> ckpt;             // per path edge: undo-log size just before it was yielded
     std::vector<int32_t> stack;            // edge_dfs stack: the start node, then the path heads
@@ -63,8 +155,28 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<int32_t> tail_of;          // path edge -> its tail (the node whose iterator yielded it)
     int64_t nrem = 0;
 
+    std::vector<int32_t> tail(n_edges);
+    std::vector<int64_t> roff(n_nodes + 1, 0), rev(n_edges);
+    for (int32_t v = 0; v < n_nodes; ++v)
+        for (int64_t e = off[v]; e < off[v + 1]; ++e) {
+            tail[e] = v;
+            ++roff[head[e] + 1];
+        }
+    for (int32_t v = 0; v < n_nodes; ++v) roff[v + 1] += roff[v];
+    {
+        std::vector<int64_t> fill(roff.begin(), roff.end() - 1);
+        for (int64_t e = 0; e < n_edges; ++e) rev[fill[head[e]]++] = e;
+    }
+    std::vector<uint8_t> settled;
+    settle(off, head, alive.data(), n_nodes, tail, roff, rev, explored, settled);
+    // yields between recomputations (OVL_CYCLES_SETTLE_EVERY: a test knob, e.g. 1 = after every yield)
+    int64_t every = n_edges / 2;
+    if (const char* env = getenv("OVL_CYCLES_SETTLE_EVERY")) every = atoll(env);
+    if (every <= 0) every = INT64_MAX;  // only the initial computation
+    int64_t budget = every;
+
     for (int32_t s = 0; s < n_nodes; ++s) {
-        if (explored[s]) continue;
+        if (explored[s] || settled[s]) continue;
         log.clear();
         path.clear();
         ckpt.clear();
@@ -91,9 +203,26 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 pos[cur] = off[cur];
                 log.push_back({0, cur, 0});
             }
+            // next yield of cur's iterator.  Edges into explored or settled nodes are walked by edge_dfs
+            // without any effect on find_cycle, and both sets only grow, so such an edge is spliced out
+            // of every later iteration (skip pointers, shared with the removed edges) instead of being
+            // yielded; the iterator advance over a run of them is logged once with the yield after it.
+            const int64_t end = off[cur + 1];
             int64_t q = pos[cur];
-            while (q < off[cur + 1] && !alive[q]) ++q;
-            if (q == off[cur + 1]) {  // iterator exhausted: pop
+            for (;;) {
+                while (skip[q] != q) {  // first live edge at or after q (path halving)
+                    skip[q] = skip[skip[q]];
+                    q = skip[q];
+                }
+                if (q >= end) {
+                    q = end;
+                    break;
+                }
+                const int32_t hq = head[q];
+                if (!explored[hq] && !settled[hq]) break;
+                skip[q] = q + 1;
+            }
+            if (q == end) {  // iterator exhausted: pop
                 if (pos[cur] != q) {
                     log.push_back({1, cur, pos[cur]});
                     pos[cur] = q;
@@ -106,7 +235,11 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
             log.push_back({1, cur, pos[cur]});
             pos[cur] = q + 1;
             const int32_t h = head[q];
-            if (explored[h]) continue;  // pushed and fully walked by edge_dfs, skipped by find_cycle
+            if (--budget < 0) {
+                settle(off, head, alive.data(), n_nodes, tail, roff, rev, explored, settled);
+                budget = every;
+                if (settled[h]) continue;
+            }
             stack.push_back(h);
             if (prev_head >= 0 && cur != prev_head) {
                 // backtracking: pop the path back to the edge whose head is cur (or empty it)
@@ -139,6 +272,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 const int32_t tail_of_dead = tail_of[kmin];
                 removed[nrem++] = dead;
                 alive[dead] = 0;
+                skip[dead] = dead + 1;
                 // rewind the DFS to the moment `dead` was about to be yielded
                 const int64_t target = ckpt[kmin];
                 while ((int64_t)log.size() > target) {

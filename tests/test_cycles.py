@@ -72,6 +72,60 @@ def test_native_matches_oracle_random(oracle_mod, seed):
         assert _same(oracle_mod.remove_cycles(G.copy()), remove_cycles_from_graph(G.copy()))
 
 
+def _layered_graph(rng, blobs):
+    """Strongly connected blobs joined by DAG edges, acyclic tails in and out of them, node order
+    shuffled: starts that reach only acyclic territory, DFS excursions into nodes that can no longer
+    reach a cycle (the native replay's settled nodes) and blobs that break up as edges go."""
+    G = nx.DiGraph()
+    nodes, groups = [], []
+    for bi in range(blobs):
+        size = rng.randint(1, 9)
+        grp = [f"b{bi}_{i}" for i in range(size)]
+        groups.append(grp)
+        nodes += grp
+    tails = [f"t{i}" for i in range(rng.randint(0, 25))]
+    order = nodes + tails
+    rng.shuffle(order)
+    G.add_nodes_from(order)
+    edges = []
+    for grp in groups:
+        for u in grp:
+            for v in grp:
+                if (u != v or rng.random() < 0.05) and rng.random() < 0.5:
+                    edges.append((u, v))
+    for i in range(len(groups)):
+        for j in range(i + 1, len(groups)):
+            if rng.random() < 0.3:
+                edges.append((rng.choice(groups[i]), rng.choice(groups[j])))
+    rank = {t: i for i, t in enumerate(tails)}
+    for t in tails:
+        for _ in range(rng.randint(1, 4)):
+            x = rng.choice(nodes + tails)
+            if x in rank and rank[x] <= rank[t]:
+                continue
+            edges.append((t, x) if rng.random() < 0.5 or x in rank else (x, t))
+    rng.shuffle(edges)
+    for u, v in edges:
+        G.add_edge(u, v, weight=rng.randint(-2, 6))
+    return G
+
+
+@pytest.mark.parametrize("every", ["default", "1", "3", "0"])
+def test_native_matches_oracle_layered(oracle_mod, monkeypatch, every):
+    """Settled-node skipping (ovl_graph.cpp): the settled set recomputed after every yield, every
+    third yield, at the default interval and only once must all remove the oracle's edges."""
+    from ovlgraph.overlapGraphs import remove_cycles_from_graph
+    if every != "default":
+        monkeypatch.setenv("OVL_CYCLES_SETTLE_EVERY", every)
+    rng = random.Random(1234)
+    for _ in range(60):
+        G = _layered_graph(rng, rng.randint(1, 8))
+        assert _same(oracle_mod.remove_cycles(G.copy()), remove_cycles_from_graph(G.copy()))
+    for _ in range(20):
+        G = _random_graph(rng, rng.randint(1, 40), rng.choice([0.03, 0.08, 0.2]), whi=rng.choice([1, 5]))
+        assert _same(oracle_mod.remove_cycles(G.copy()), remove_cycles_from_graph(G.copy()))
+
+
 def test_native_matches_oracle_overlap_graph(oracle_mod):
     """A PhiX overlap graph (1,200 reads, l = 100, p = 0.01, k = 5) with its copies and attributes."""
     from ovlgraph import overlapGraphs as og
