@@ -297,7 +297,13 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
         best[q] = -qoff[q];  // "key <= 0" for block q
     }
     const int32_t d16 = (int32_t)((uint32_t)dms << 16);
-    const int32_t dv = __builtin_amdgcn_readfirstlane(d16);
+    // the mismatch factor in a VGPR: v_mad_i32_i24 then reads only one SGPR (the scalar row offset
+    // rm), within gfx9's one-scalar operand limit, and needs no per-shift v_mov of rm
+    int32_t dv;
+    {
+        const int32_t ds = (__builtin_amdgcn_readfirstlane(d16) << 8) >> 8;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(dv) : "s"(ds));
+    }
     // keys of one r over blocks [0, NQ) (NQ compile-time), r scalar
     auto keys = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag, T (&kq)[W + 1]) {
         constexpr int NQ = decltype(nq_tag)::value;
@@ -324,7 +330,7 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
                 X = k == (W - 1 - q > 0 ? W - 1 - q : 0) ? (uint32_t)__builtin_popcount(mm) : bcnt_acc(mm, X);
             }
             if constexpr (KM == 0) {
-                kq[q] = ((((int32_t)X << 8) >> 8) * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24
+                kq[q] = ((((int32_t)X << 8) >> 8) * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24 (dv: 24-bit)
             } else {
                 kq[q] = (int64_t)dms * 4294967296ll * (int64_t)X + rm;
             }
