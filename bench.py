@@ -194,6 +194,18 @@ def timed_steps(w: Workload, steps: int, warmup: int, dev, world: int):
     return t1 - t0, ev0.elapsed_time(ev1) / max(steps, 1)
 
 
+def host_buffer_timing(w: Workload, reps: int = 20):
+    """The same pairs through ovl_score_host: pair list in host memory, (score, end) back in host
+    memory, so PCIe copies are included (SURVEY.md §8d's ABI-call step).  Not the metric."""
+    w.eng.score(w.a, w.b, 10, -1, w.indel, w.band)  # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        w.eng.score(w.a, w.b, 10, -1, w.indel, w.band)
+    dt = (time.perf_counter() - t0) / reps
+    return {"pairs": w.n_pairs, "ms_per_call": dt * 1e3, "pairs_per_s": w.n_pairs / dt,
+            "what": "ovl_score_host: H2D of a_idx/b_idx, scoring, D2H of score/end (reads resident)"}
+
+
 def candidate_timing(w: Workload, reps: int = 5):
     """Candidate enumeration (overlapGraphs.py:30-52) for this workload: the device path
     (ovl_candidates: keys, radix sort, lookup, scan, ordered emit; synchronous, list left
@@ -430,6 +442,7 @@ def main() -> None:
         }
         if world == 1:
             line["candidates"] = candidate_timing(w)
+            line["host_buffers"] = host_buffer_timing(w)
             if not args.no_extra:
                 line["end_to_end"] = end_to_end(w)
                 line["local_alignment"] = local_alignment_timing(w.eng)
