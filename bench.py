@@ -330,6 +330,40 @@ def device_list_timing(eng, name: str, steps: int, dev):
             "roofline_frac": algo / (km * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def sharded_gather_timing(eng, dev, world: int, backend: str, steps: int):
+    """N > 1, every rank: ONE candidate list (the target point, seed 0, the same on every rank) scored
+    pair-sharded with the RCCL all_gather of (score, end) that restores reference order
+    (ovlgraph.sharded.ShardedStep) -- the multi-GPU drop-in, strong scaling.  Also
+    checks the gathered result against this rank scoring the whole list alone."""
+    import torch
+    import torch.distributed as dist
+    from ovlgraph.sharded import ShardedStep
+    x = Workload("target", seed=0, dev=dev, engine=eng)
+    st = ShardedStep(x.reads, x.a, x.b, engine=eng)
+    for _ in range(3):
+        st.step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    sc, en = st.results()
+    x.launch()
+    torch.cuda.synchronize(dev)
+    ok = bool(np.array_equal(sc, x.ds.cpu().numpy()) and np.array_equal(en, x.de.cpu().numpy()))
+    red = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(red, op=dist.ReduceOp.MAX)
+    el, bad = float(red[0]), float(red[1])
+    return {"workload": WORKLOAD_DESC["target"], "pairs": x.n_pairs, "ranks": world, "scaling": "strong",
+            "steps": steps, "ms_per_step": el / steps * 1e3, "pairs_per_s": x.n_pairs * steps / el,
+            "gather_bytes_per_rank_per_step": st.gather_bytes(),
+            "collective": "all_gather_into_tensor (RCCL over xGMI)" if backend == "nccl" else "all_gather (gloo, host)",
+            "matches_single_gpu": bad == 0.0}
+
+
 def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
     """Config 5's band-width sweep: the same resident pairs at each band (-1 = full DP).
 
@@ -367,6 +401,7 @@ def main() -> None:
                          "(config 5's sweep: 8,16,32,64,-1); reported under band_sweep")
     ap.add_argument("--sweep-indel", type=int, default=-2)
     ap.add_argument("--sweep-steps", type=int, default=5)
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the sharded one-list RCCL-gather timing")
     args = ap.parse_args()
 
     import torch
@@ -400,6 +435,10 @@ def main() -> None:
         total_pairs = int(tot[2])
     else:
         total_pairs = w.n_pairs
+
+    gather = None
+    if world > 1 and not args.no_gather:
+        gather = sharded_gather_timing(w.eng, dev, world, backend, max(20, args.steps // 10))
 
     if rank == 0:
         algo = w.algo_bytes()
@@ -440,6 +479,8 @@ def main() -> None:
             "occupancy": load_profile(args.config).get("occupancy"),
             "host_setup_s": {"read_sim_and_enumeration": round(w.t_enum, 3), "upload_and_pack": round(w.t_pack, 4)},
         }
+        if gather is not None:
+            line["sharded_gather"] = gather
         if world == 1:
             line["candidates"] = candidate_timing(w)
             line["host_buffers"] = host_buffer_timing(w)

@@ -336,10 +336,51 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
             }
         }
     };
+    // the same keys for r >= 1 with s shifted down by 32 - r instead of t up by it (the same base pairs
+    // meet): the word shifted in from above is zero, so the top word of s is one v_lshrrev (fast class)
+    // where t's bottom word needed a v_alignbit with zero (slow class).  Compared positions end inside
+    // s word W-1 (its low r bits, mask vt = ~0 >> (32 - r)); block q pairs shifted s word k with t word
+    // k - (W-1-q).  NQ <= W (block W only at r = 0).
+    auto keys_s = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag, T (&kq)[W + 1]) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        static_assert(NQ <= W, "keys_s: r >= 1 has at most W blocks");
+        const uint32_t sg = 32u - r;  // 1..31
+        uint32_t V[W][P];
+#pragma unroll
+        for (int k = W - NQ; k < W; ++k) {
+#pragma unroll
+            for (int c = 0; c < P; ++c)
+                V[k][c] = k < W - 1 ? alignbit(Sw[(k + 1) * P + c], Sw[k * P + c], sg) : Sw[k * P + c] >> sg;
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            uint32_t X = 0;
+#pragma unroll
+            for (int k = W - 1 - q; k < W; ++k) {
+                const int i = k - (W - 1 - q);
+                uint32_t mm = __builtin_amdgcn_bitop3_b32(V[k][1], Tw[i * P + 1], V[k][0] ^ Tw[i * P], 0xBE);
+                if (k == W - 1) mm &= vt;
+                X = k == W - 1 - q ? (uint32_t)__builtin_popcount(mm) : bcnt_acc(mm, X);
+            }
+            if constexpr (KM == 0) {
+                kq[q] = ((((int32_t)X << 8) >> 8) * ((dv << 8) >> 8)) + rm;    // v_mad_i32_i24 (dv: 24-bit)
+            } else {
+                kq[q] = (int64_t)dms * 4294967296ll * (int64_t)X + rm;
+            }
+        }
+    };
+    // r = 0 (t unshifted, block W when lw = 32W) through keys; r >= 1 through keys_s for W <= 4 (A/B on
+    // one box: cfg2 -0.7 %, target -0.4 %; at W = 5, cfg3, +1.3 %, so W >= 5 keeps the t shift)
+    constexpr bool SHIFT_S = W <= 4;
     auto body = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag) {
         constexpr int NQ = decltype(nq_tag)::value;
         T kq[W + 1];
-        keys(r, vt, rm, nq_tag, kq);
+        if constexpr (NQ > W || !SHIFT_S) {
+            keys(r, vt, rm, nq_tag, kq);
+        } else {
+            if (r == 0) keys(r, vt, rm, nq_tag, kq);
+            else keys_s(r, 0xFFFFFFFFu >> (32u - r), rm, nq_tag, kq);
+        }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) best[q] = kq[q] > best[q] ? kq[q] : best[q];
     };
@@ -347,8 +388,13 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     auto body2 = [&](uint32_t r, T rm, auto nq_tag) {
         constexpr int NQ = decltype(nq_tag)::value;
         T k0[W + 1], k1[W + 1];
-        keys(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, nq_tag, k0);
-        keys(r + 1, (uint32_t)((int32_t)0x80000000 >> r), rm + mq, nq_tag, k1);
+        if constexpr (SHIFT_S) {
+            keys_s(r, 0xFFFFFFFFu >> (32u - r), rm, nq_tag, k0);
+            keys_s(r + 1, 0xFFFFFFFFu >> (31u - r), rm + mq, nq_tag, k1);
+        } else {
+            keys(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, nq_tag, k0);
+            keys(r + 1, (uint32_t)((int32_t)0x80000000 >> r), rm + mq, nq_tag, k1);
+        }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const T m01 = k0[q] > k1[q] ? k0[q] : k1[q];

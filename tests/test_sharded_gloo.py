@@ -44,8 +44,15 @@ def _worker(rank, world, port, q):
     distinct, _ = dedup_reads(reads)
     a, b = enumerate_candidates(distinct, 3)
     sc, en = score_pairs_sharded(distinct, a, b, local_scorer=lambda r, x, y: oracle.batch_ungapped(r, x, y))
+    # the repeated-step form bench.py times at N > 1: setup once, step twice, gather in reference order
+    from ovlgraph.sharded import ShardedStep
+    st = ShardedStep(distinct, a, b, local_scorer=lambda r, x, y: oracle.batch_ungapped(r, x, y))
+    st.step()
+    st.step()
+    sc2, en2 = st.results()
+    assert st.gather_bytes() == world * 2 * st.width * 4
     if rank == 0:
-        q.put((a, b, sc, en, distinct))
+        q.put((a, b, sc, en, distinct, sc2, en2))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -57,7 +64,7 @@ def test_gloo_world2_matches_single_process(oracle_mod):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    a, b, sc, en, distinct = q.get(timeout=240)
+    a, b, sc, en, distinct, sc2, en2 = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -65,3 +72,5 @@ def test_gloo_world2_matches_single_process(oracle_mod):
     assert len(a) > 100
     np.testing.assert_array_equal(sc, ref_sc)
     np.testing.assert_array_equal(en, ref_en)
+    np.testing.assert_array_equal(sc2, ref_sc)
+    np.testing.assert_array_equal(en2, ref_en)

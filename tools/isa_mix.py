@@ -8,7 +8,7 @@ tools/valu_rates.hip measurements committed in profiles/r01_valu_rates.txt.
 import re
 import sys
 
-FAST = {"v_xor_b32", "v_add_u32", "v_and_b32", "v_or_b32", "v_bitop3_b32", "v_sub_u32", "v_mov_b32"}
+FAST = {"v_xor_b32", "v_add_u32", "v_and_b32", "v_or_b32", "v_bitop3_b32", "v_sub_u32", "v_mov_b32", "v_lshrrev_b32"}
 COST_FAST, COST_SLOW = 2.85, 4.4
 
 
