@@ -163,17 +163,35 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 
 template <typename T>
 __device__ __forceinline__ T group_max(T best, int ppw) {
-    // combine the RS lanes of a pair (lanes slot, slot + ppw, ...)
-    for (int off = 32; off >= ppw; off >>= 1) {
+    // combine the RS lanes of a pair (lanes slot, slot + ppw, ...): across rows (offsets 32, 16) with
+    // ds_bpermute, inside a 16-lane row with DPP row rotations (offsets 8, 4, 2, 1 reach the same lanes
+    // as xor for a max, as one VALU op each instead of an LDS round trip)
+    auto xchg = [&](T v, auto off_tag) -> T {
+        constexpr int OFF = decltype(off_tag)::value;
+        auto one = [&](int x) -> int {
+            if constexpr (OFF >= 16) return __shfl_xor(x, OFF, 64);
+            else return __builtin_amdgcn_update_dpp(x, x, 0x120 + OFF, 0xF, 0xF, false);  // row_ror:OFF
+        };
         if constexpr (sizeof(T) == 4) {
-            best = max(best, (T)__shfl_xor((int)best, off, 64));
+            return (T)one((int)v);
         } else {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)best, off, 64);
-            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)((uint64_t)best >> 32), off, 64);
-            const T o = (T)(((uint64_t)hi << 32) | lo);
+            const uint32_t lo = (uint32_t)one((int)(uint32_t)v);
+            const uint32_t hi = (uint32_t)one((int)(uint32_t)((uint64_t)v >> 32));
+            return (T)(((uint64_t)hi << 32) | lo);
+        }
+    };
+    auto step = [&](auto off_tag) {
+        if (ppw <= decltype(off_tag)::value) {
+            const T o = xchg(best, off_tag);
             best = o > best ? o : best;
         }
-    }
+    };
+    step(std::integral_constant<int, 32>{});
+    step(std::integral_constant<int, 16>{});
+    step(std::integral_constant<int, 8>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 1>{});
     return best;
 }
 
@@ -600,6 +618,10 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             const int cnt = __popcll(pm);
 #ifndef OVL_ABLATE_DRAIN  // diagnostic build only: side pairs left unscored
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            // issue priority over the co-resident sweeps while the side pairs drain: the drain's chain
+            // (LDS restaging, a general sweep, the group max) is the launch's tail otherwise (A/B on one
+            // box, cfg2: 8.87 -> 8.39 us with levels 1-3 alike; raised from the wave's start: 8.62 us)
+            __builtin_amdgcn_s_setprio(1);
             for (int h = 0; h < cnt; h += 16) {
                 const int count = cnt - h < 16 ? cnt - h : 16;
                 const int rs = count > 8 ? 2 : (count > 4 ? 3 : (count > 2 ? 4 : 5));
@@ -627,6 +649,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
                     out_end[en.x] = e2;
                 }
             }
+            __builtin_amdgcn_s_setprio(0);
 #endif
             OVL_TR_CLOCK(2, cnt);
             OVL_TR_VAL(7, cnt);
@@ -663,13 +686,22 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
 #ifndef OVL_ABLATE_DRAIN
         if constexpr (!LAT) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#ifdef OVL_DRAIN_PRIO
+            if (tail - head >= 16) __builtin_amdgcn_s_setprio(OVL_DRAIN_PRIO);
+#endif
             while (tail - head >= 16) drain(16);
+#ifdef OVL_DRAIN_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
         }
 #endif
     }
 #ifndef OVL_ABLATE_DRAIN
     if constexpr (!LAT) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#ifdef OVL_DRAIN_PRIO
+        __builtin_amdgcn_s_setprio(OVL_DRAIN_PRIO);
+#endif
         if (tail > head) drain(tail - head);
     }
 #endif
