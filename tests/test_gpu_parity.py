@@ -339,6 +339,31 @@ def test_uniform_kernel_key_variants(engine, oracle_mod, params):
     np.testing.assert_array_equal(en, re_)
 
 
+@pytest.mark.parametrize("n_short", [1, 12, 60])
+def test_clustered_side_pairs_vs_oracle(engine, oracle_mod, n_short):
+    """Candidate lists in read order, as overlapGraphs.py:43-53 emits them: the pairs of a truncated
+    read are consecutive, so whole tiles of side pairs reach one latency-mode side wave (drained at
+    raised issue priority) or one throughput-mode ring."""
+    rng = random.Random(7 + n_short)
+    reads = [_rand(rng, 100) for _ in range(300)] + [_rand(rng, rng.randint(1, 99)) for _ in range(n_short)]
+    rng.shuffle(reads)
+    n = len(reads)
+    a, b = [], []
+    for i in range(n):
+        for j in rng.sample(range(n), 40):
+            if j != i:
+                a.append(i)
+                b.append(j)
+    a = np.array(a, dtype=np.int32)
+    b = np.array(b, dtype=np.int32)
+    engine.set_reads(reads)
+    assert engine.plan() == "ungapped"
+    sc, en = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
 def test_split_knob_equivalence(oracle_mod):
     """OVL_SPLIT (0 = one wavefront per tile, >0 = latency mode with a side-pair
     wavefront beside each sweeping one) must not change results, including a list
