@@ -69,6 +69,9 @@ struct ovl_ctx {
     // local alignment (ovl_local_align): query / reference bytes, carried rows, progress, traceback
     DevBuf l_q, l_r, l_row, l_tb, l_best;
     uint32_t l_epoch = 0;  // tags this launch's row hand-off words (l_row is zeroed when allocated)
+    // pinned host copy of the part of the traceback table the walk can reach (grown on demand)
+    int8_t* l_tb_host = nullptr;
+    size_t l_tb_host_bytes = 0;
 };
 
 namespace {
@@ -443,6 +446,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
                       &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b, &c->l_q, &c->l_r, &c->l_row,
                       &c->l_tb, &c->l_best, &c->lane_col})
         release(*b);
+    if (c->l_tb_host) (void)hipHostFree(c->l_tb_host);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return OVL_OK;
@@ -841,11 +845,6 @@ OVL_API int ovl_local_align(ovl_ctx* c, const uint8_t* query, int32_t n, const u
     uint32_t flag = 0;
     HIPCHK(c, hipMemcpyAsync(&key, c->l_best.p, sizeof(key), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(&flag, c->err_flag.p, sizeof(flag), hipMemcpyDeviceToHost, s));
-    std::vector<int8_t> tb;
-    if (ops) {
-        tb.resize(tb_bytes);
-        HIPCHK(c, hipMemcpyAsync(tb.data(), c->l_tb.p, tb_bytes, hipMemcpyDeviceToHost, s));
-    }
     HIPCHK(c, hipStreamSynchronize(s));
     if (flag) {
         HIPCHK(c, hipMemset(c->err_flag.p, 0, sizeof(uint32_t)));
@@ -862,11 +861,27 @@ OVL_API int ovl_local_align(ovl_ctx* c, const uint8_t* query, int32_t n, const u
     *out_end_j = bj;
     int32_t i = bi, j = bj;
     int64_t k = 0;
-    if (ops) {
+    if (ops && bi > 0 && bj > 0) {
+        // the walk moves up and left from (bi, bj): it reads strips 0 .. (bi-1)/64 and, in each,
+        // steps j + L - 1 <= bj + 62.  Only that corner of the table comes back, as one strided copy
+        // into a pinned buffer (the whole table is ~22 MB at contig x PhiX scale).
+        const size_t n_st = (size_t)((bi - 1) >> 6) + 1;
+        const size_t w = (size_t)(bj + 63) * 64;  // bytes of steps 0 .. bj + 62 in one strip
+        const size_t need = n_st * w;
+        if (c->l_tb_host_bytes < need) {
+            if (c->l_tb_host) (void)hipHostFree(c->l_tb_host);
+            c->l_tb_host = nullptr;
+            c->l_tb_host_bytes = 0;
+            HIPCHK(c, hipHostMalloc((void**)&c->l_tb_host, need, hipHostMallocDefault));
+            c->l_tb_host_bytes = need;
+        }
+        HIPCHK(c, hipMemcpy2DAsync(c->l_tb_host, w, c->l_tb.p, (size_t)steps * 64, w, n_st, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const int8_t* tb = c->l_tb_host;
         // aligners.py:133-153: walk while i > 0, j > 0 and dp[i][j] > 0
         while (i > 0 && j > 0) {
             const int32_t st = (i - 1) >> 6, L = (i - 1) & 63;
-            const int8_t code = tb[((size_t)st * (size_t)steps + (size_t)(j + L - 1)) * 64 + (size_t)L];
+            const int8_t code = tb[(size_t)st * w + (size_t)(j + L - 1) * 64 + (size_t)L];
             if (!(code & 4)) break;
             const int8_t op = code & 3;
             if (op == 1) { --i; --j; }
