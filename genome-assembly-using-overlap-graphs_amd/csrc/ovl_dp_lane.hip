@@ -113,10 +113,10 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                 const int32_t jc = j0 + c < m ? j0 + c : 0;
                 tc[c] = (uint32_t)codes[tb + (uint32_t)jc];
             }
-            // PROF: per symbol x a byte profile of the strip, PX[x][w] byte k = s(x, t[j0 + 4w + k]); a
-            // row picks its symbol's words with three bit muxes per word and a cell adds its byte with a
-            // sign-extending SDWA add
+            // PROF: a row's profile word w holds s(x, t[j0 + 4w + k]) in byte k (x = the row's symbol); a
+            // cell adds its byte with a sign-extending SDWA add
             constexpr int PW = PROF ? CW / 4 : 1;
+#ifdef OVL_LANE_MUX  // A/B reference: four byte profiles per strip, three bit muxes per word per row
             uint32_t PX[4][PW];
             if constexpr (PROF) {
 #pragma unroll
@@ -131,6 +131,18 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                     }
                 }
             }
+#else
+            // the strip's t codes as bytes (TW[w] byte k = t[j0 + 4w + k], codes 0..3); a row's profile
+            // word is one v_perm_b32 of its 4-byte score table by these codes
+            uint32_t TW[PW];
+            if constexpr (PROF) {
+#pragma unroll
+                for (int w = 0; w < PW; ++w)
+                    TW[w] = tc[4 * w] | (tc[4 * w + 1] << 8) | (tc[4 * w + 2] << 16) | (tc[4 * w + 3] << 24);
+            }
+            const uint32_t tbl_base = ((uint32_t)s_mm & 0xFFu) * 0x01010101u;   // every t mismatches
+            const uint32_t tbl_diff = ((uint32_t)(s_ma ^ s_mm)) & 0xFFu;        // byte x -> match score
+#endif
             int32_t A[CW], B[CW];
 #pragma unroll
             for (int c = 0; c < CW; ++c) A[c] = -g * (j0 + 1 + c);  // row 0: G[0][j] = -indel * j
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                         m1 = (uint32_t)(((int32_t)(sc << 30)) >> 31);
                     }
                     const uint32_t nv = (uint32_t)~((it - sk) >> 31);  // 0 on virtual rows
+#ifdef OVL_LANE_MUX
 #pragma unroll
                     for (int w = 0; w < PW; ++w) {
                         const uint32_t lo = __builtin_amdgcn_bitop3_b32(m0, PX[1][w], PX[0][w], 0xCA);  // m0 ? : mux
@@ -191,6 +204,14 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                         P[w] = __builtin_amdgcn_bitop3_b32(m1, hi, lo, 0xCA);
                         if constexpr (MASKED) P[w] &= nv;  // zero profile: the row repeats row 0
                     }
+#else
+                    // row symbol x = bit0 | bit1 << 1; its table: byte t = s(x, t) in G units
+                    const uint32_t x8 = (m0 & 8u) | (m1 & 16u);          // 8 * x
+                    uint32_t tbl = tbl_base ^ (tbl_diff << x8);
+                    if constexpr (MASKED) tbl &= nv;                       // zero profile: the row repeats row 0
+#pragma unroll
+                    for (int w = 0; w < PW; ++w) P[w] = __builtin_amdgcn_perm(tbl, tbl, TW[w]);
+#endif
                 }
 #pragma unroll
                 for (int c = 0; c < CW; ++c) {
