@@ -1,13 +1,20 @@
 // ovl_api.cpp — the C ABI of include/ovl.h on top of the gfx950 kernels.
 //
-// Owns: the HIP stream, the resident read store (codes + bit-plane layouts in
-// HBM), scratch for host-array calls and the device error flag.  Chooses the
-// kernel per call (ovl_plan): the ungapped popcount kernel whenever gaps
-// provably cannot win and the read store has a bit-plane layout, else the
-// int64-exact DP kernel.  Never falls back to the CPU.
+// A context (ovl_ctx) drives one or more HIP devices from one host thread.  Each
+// device (Dev) owns: a compute stream and two copy streams (H2D, D2H), its copy
+// of the resident read store (codes + bit-plane layouts in HBM), scratch for
+// host-array calls, pinned staging rings and the device error flag.  Host-array
+// scoring calls shard the pair list over the devices (contiguous ranges balanced
+// by sum n*m) and run a chunked pipeline per device: H2D of chunk
+// k+1, the kernel on chunk k and the D2H of chunk k-1 overlap, and results land
+// directly in the caller's arrays when they are pinned (else through pinned
+// staging).  Kernel choice per call (ovl_plan): the ungapped popcount kernel
+// whenever gaps provably cannot win and the read store has a bit-plane layout,
+// else a DP kernel.  Never falls back to the CPU.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +32,7 @@ namespace {
 constexpr int32_t kFastMaxLen = 256;   // bit-plane layouts up to W = 8 words of 32 bases
 constexpr int32_t kDpMaxLen = 8192;    // DP kernel: LDS row of the t read
 constexpr int32_t kLaneMaxLen = 1024;  // lane-per-pair DP: hand-off column buffer per wavefront slot
+constexpr int kSlots = 3;              // pipeline depth: staging slots / events per device
 
 struct DevBuf {
     void* p = nullptr;
@@ -33,13 +41,8 @@ struct DevBuf {
 
 thread_local std::string g_err;
 
-}  // namespace
-
-struct ovl_ctx {
-    int32_t device = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
-    int32_t cu_count = 256;
+// Tuning / test knobs, read from the environment once per context.
+struct Knobs {
     int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
     int32_t band_form = -1;       // OVL_BAND_FORM env (lane|diag|rows|fast|strip): band knob kernel (tests)
     int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
@@ -51,6 +54,34 @@ struct ovl_ctx {
     int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
     int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
                                   // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
+    int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic)
+    int32_t pipe_direct = 1;      // OVL_PIPE_DIRECT=0: pinned outputs through D2H copies instead of kernel stores
+};
+
+}  // namespace
+
+struct ovl_ctx;
+
+// Per-device state.
+struct Dev {
+    ovl_ctx* owner = nullptr;
+    int32_t device = 0;
+    hipStream_t stream = nullptr;  // kernels
+    hipStream_t s_in = nullptr;    // H2D copies of host-array calls
+    hipStream_t s_out = nullptr;   // D2H copies of host-array calls
+    int32_t cu_count = 256;
+    Knobs k;
+    // knob aliases used by the launch code
+    int32_t& split_override = k.split_override;
+    int32_t& band_form = k.band_form;
+    int32_t& dp_classic = k.dp_classic;
+    int32_t& dp_lane = k.dp_lane;
+    int32_t& lane_cw = k.lane_cw;
+    int64_t& lane_min_pairs = k.lane_min_pairs;
+    int32_t& lane_prof = k.lane_prof;
+    int32_t& lane_col16 = k.lane_col16;
+    int32_t& lane_sfx = k.lane_sfx;
+    int32_t& blocks_per_cu = k.blocks_per_cu;
     // resident reads
     int32_t n_reads = -1;
     int32_t lmax = 0;
@@ -59,23 +90,45 @@ struct ovl_ctx {
     int32_t srow = 0;  // sfx row stride (words)
     int32_t trow = 0;  // pfx row stride (words)
     DevBuf codes, off, len, sfx, pfx, lut, full;  // full: bit r set iff len[r] == lmax
+    DevBuf raw;                                   // upload staging of ovl_set_reads (freed after the upload)
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
     DevBuf lane_col;      // lane-per-pair DP: per-wavefront strip hand-off columns
+    hipEvent_t lane_evt = nullptr;        // last launch that used lane_col ...
+    hipStream_t lane_stream = nullptr;    // ... and its stream (launches on other streams wait for it)
+    bool lane_used = false;
     int64_t codes_bytes = 0;
     // device candidate enumeration (ovl_candidates): per-read keys / groups and the pair list
     DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
     int64_t cand_n = -1;  // -1: no candidate list for the resident reads
+    int64_t cand_tail[2] = {0, 0};
+    DevBuf sh_cum, sh_temp, sh_cuts;  // shard bounds (ovl_candidates_shards)
     // local alignment (ovl_local_align): query / reference bytes, carried rows, progress, traceback
     DevBuf l_q, l_r, l_row, l_tb, l_best;
     uint32_t l_epoch = 0;  // tags this launch's row hand-off words (l_row is zeroed when allocated)
     // pinned host copy of the part of the traceback table the walk can reach (grown on demand)
     int8_t* l_tb_host = nullptr;
     size_t l_tb_host_bytes = 0;
+    // host-array pipeline: events per slot and pinned staging (slots x cap pairs x {a, b} / {score, end})
+    hipEvent_t ev_h2d[kSlots] = {}, ev_in[kSlots] = {}, ev_k[kSlots] = {}, ev_out[kSlots] = {};
+    int32_t* st_in = nullptr;
+    int32_t* st_out = nullptr;
+    int64_t st_cap = 0;
+    uint32_t* h_flag = nullptr;  // pinned error-flag readback
+    std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
+};
+
+struct ovl_ctx {
+    std::vector<Dev*> devs;
+    std::string err;
+    std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
+    int32_t timing = 0;          // ovl_set_timing
+    double t_kernel_ms = 0.0, t_call_ms = 0.0;
 };
 
 namespace {
 
+int fail(const ovl_ctx* c, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
 int fail(const ovl_ctx* c, int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -84,6 +137,18 @@ int fail(const ovl_ctx* c, int code, const char* fmt, ...) {
     va_end(ap);
     g_err = buf;
     if (c) const_cast<ovl_ctx*>(c)->err = buf;
+    return code;
+}
+
+int fail(const Dev* d, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail(const Dev* d, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    if (d && d->owner) d->owner->err = buf;
     return code;
 }
 
@@ -139,13 +204,13 @@ struct Plan {
     bool seed_wide = true;
 };
 
-int make_plan_full(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, Plan* out);
+int make_plan_full(const Dev* c, int32_t match, int32_t mismatch, int64_t indel, Plan* out);
 
 // band >= 0: the build's seed-and-extend knob (oracle_overlap_banded), exact
 // (== the reference) whenever gaps cannot win -- the seed cell (n, j*) is
 // always in the band and nothing off the ungapped diagonals can beat it -- and
 // whenever the band covers every diagonal (band >= 2 * lmax).
-int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* out) {
+int make_plan(const Dev* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* out) {
     if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
     const int64_t L = std::max<int32_t>(c->lmax, 1);
     if (band < 0 || band >= 2 * L || gaps_cannot_win(match, mismatch, indel, L))
@@ -172,7 +237,7 @@ int make_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, 
     return OVL_OK;
 }
 
-int make_plan_full(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, Plan* out) {
+int make_plan_full(const Dev* c, int32_t match, int32_t mismatch, int64_t indel, Plan* out) {
     const int64_t L = std::max<int32_t>(c->lmax, 1);
     const int64_t amax = std::max(iabs64(match), iabs64(mismatch));
     Plan p;
@@ -198,14 +263,14 @@ int make_plan_full(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t in
     return OVL_OK;
 }
 
-int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
+int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s);
 
 // Lane-per-pair full DP (ovl_dp_lane.hip): one lane per pair, so it needs many pairs to fill the
 // chip (below that the one-wavefront-per-pair dp_fast_kernel is faster), reads short enough for
 // the per-wavefront hand-off columns, and G = dp - indel*(i+j) inside int32.
-bool use_dp_lane(const ovl_ctx* c, int64_t match, int64_t mismatch, int64_t indel, int64_t n_pairs) {
+bool use_dp_lane(const Dev* c, int64_t match, int64_t mismatch, int64_t indel, int64_t n_pairs) {
     if (c->dp_lane == 0) return false;
     const int64_t L = std::max<int32_t>(c->lmax, 1);
     const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
@@ -215,7 +280,7 @@ bool use_dp_lane(const ovl_ctx* c, int64_t match, int64_t mismatch, int64_t inde
 }
 
 // Kernels queue pair indices as int32 (LDS side ring); split huge lists.
-int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
+int launch_score(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                  int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                  hipStream_t s) {
     constexpr int64_t kChunk = int64_t(1) << 30;
@@ -227,7 +292,7 @@ int launch_score(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* 
     return OVL_OK;
 }
 
-int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
+int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s) {
     if (n_pairs == 0) return OVL_OK;
@@ -299,7 +364,13 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
             k.cw = c->lane_cw;
             k.slots = (int64_t)c->cu_count * 4 * ovl_dp_lane_waves_per_simd(k.cw);
             const size_t col_bytes = (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t);
-            HIPCHK(c, ensure(c->lane_col, col_bytes));
+            if (c->lane_col.bytes < col_bytes) {
+                // reallocation frees the buffer a launch on another stream may still use
+                if (c->lane_used) HIPCHK(c, hipEventSynchronize(c->lane_evt));
+                HIPCHK(c, ensure(c->lane_col, col_bytes));
+            }
+            // one hand-off buffer per device: launches on different streams must not overlap on it
+            if (c->lane_used && c->lane_stream != s) HIPCHK(c, hipStreamWaitEvent(s, c->lane_evt, 0));
             const int64_t L = std::max<int32_t>(c->lmax, 1);
             const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
             const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
@@ -313,6 +384,9 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
             k.wsfx = c->wmax;
             k.colbuf = as<uint32_t>(c->lane_col);
             HIPCHK(c, ovl_launch_dp_lane(&g, &k, s));
+            HIPCHK(c, hipEventRecord(c->lane_evt, s));
+            c->lane_stream = s;
+            c->lane_used = true;
             return OVL_OK;
         }
         if (g.band >= 0) {
@@ -362,265 +436,764 @@ int launch_score_chunk(ovl_ctx* c, const Plan& pl, const int32_t* d_a, const int
     return OVL_OK;
 }
 
-int check_indices(const ovl_ctx* c, const int32_t* a, const int32_t* b, int64_t n) {
-    for (int64_t p = 0; p < n; ++p) {
-        if (a[p] < 0 || a[p] >= c->n_reads || b[p] < 0 || b[p] >= c->n_reads)
-            return fail(c, OVL_E_INDEX, "pair %lld = (%d, %d) outside [0, %d)", (long long)p, a[p], b[p],
-                        c->n_reads);
+// ----------------------------------------------------------------------------- devices
+
+// Restores the caller's current device when a public entry point returns.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
+Knobs read_knobs() {
+    Knobs k;
+    if (const char* sp = getenv("OVL_SPLIT")) {
+        const int v = atoi(sp);
+        if (v >= 0 && v <= 2) k.split_override = v;
+    }
+    if (const char* e = getenv("OVL_BAND_FORM")) {
+        if (!strcmp(e, "diag")) k.band_form = OVL_BAND_FORM_DIAG;
+        else if (!strcmp(e, "rows")) k.band_form = OVL_BAND_FORM_ROWS;
+        else if (!strcmp(e, "fast")) k.band_form = OVL_BAND_FORM_FAST;
+        else if (!strcmp(e, "strip")) k.band_form = OVL_BAND_FORM_STRIP;
+        else if (!strcmp(e, "lane")) k.band_form = OVL_BAND_FORM_LANE;
+    }
+    if (const char* e = getenv("OVL_DP_CLASSIC")) k.dp_classic = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_DP_LANE")) k.dp_lane = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_CW")) k.lane_cw = atoi(e) == 32 ? 32 : 16;
+    if (const char* e = getenv("OVL_LANE_MIN_PAIRS")) k.lane_min_pairs = atoll(e);
+    if (const char* e = getenv("OVL_LANE_PROF")) k.lane_prof = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_COL16")) k.lane_col16 = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_SFX")) k.lane_sfx = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 1024) k.blocks_per_cu = v;
+    }
+    if (const char* e = getenv("OVL_PIPE_DIRECT")) k.pipe_direct = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PIPE_CHUNK")) {
+        const long long v = atoll(e);
+        if (v >= 64) k.pipe_chunk = v;
+    }
+    return k;
+}
+
+void free_staging(int32_t*& p) {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+}
+
+void destroy_dev(Dev* d) {
+    if (!d) return;
+    (void)hipSetDevice(d->device);
+    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
+        if (s) (void)hipStreamSynchronize(s);
+    for (DevBuf* b : {&d->codes, &d->off, &d->len, &d->sfx, &d->pfx, &d->lut, &d->full, &d->raw, &d->a, &d->b,
+                      &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
+                      &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
+                      &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
+                      &d->lane_col})
+        release(*b);
+    if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
+    free_staging(d->st_in);
+    free_staging(d->st_out);
+    if (d->h_flag) (void)hipHostFree(d->h_flag);
+    for (int i = 0; i < kSlots; ++i)
+        for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i]})
+            if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d->t_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (d->lane_evt) (void)hipEventDestroy(d->lane_evt);
+    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
+        if (s) (void)hipStreamDestroy(s);
+    delete d;
+}
+
+hipError_t init_dev(Dev* d) {
+    hipError_t e = hipSetDevice(d->device);
+    if (e != hipSuccess) return e;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
+        d->cu_count = prop.multiProcessorCount;
+    for (hipStream_t* s : {&d->stream, &d->s_in, &d->s_out}) {
+        e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+        if (e != hipSuccess) return e;
+    }
+    for (int i = 0; i < kSlots; ++i)
+        for (hipEvent_t* ev : {&d->ev_h2d[i], &d->ev_in[i], &d->ev_k[i], &d->ev_out[i]}) {
+            e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+    e = hipEventCreateWithFlags(&d->lane_evt, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    e = hipHostMalloc((void**)&d->h_flag, 64, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    e = ensure(d->err_flag, 16);
+    if (e != hipSuccess) return e;
+    return hipMemset(d->err_flag.p, 0, 16);
+}
+
+int create_on(const int32_t* ids, int32_t n, ovl_ctx** out) {
+    int count = 0;
+    HIPCHK((ovl_ctx*)nullptr, hipGetDeviceCount(&count));
+    if (count <= 0) return fail((ovl_ctx*)nullptr, OVL_E_HIP, "no HIP device visible");
+    if (n <= 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "no devices requested");
+    for (int32_t i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= count)
+            return fail((ovl_ctx*)nullptr, OVL_E_ARG, "device %d outside [0, %d)", ids[i], count);
+        for (int32_t j = 0; j < i; ++j)
+            if (ids[j] == ids[i]) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "device %d listed twice", ids[i]);
+    }
+    DeviceGuard guard;
+    ovl_ctx* c = new ovl_ctx();
+    const Knobs knobs = read_knobs();
+    for (int32_t i = 0; i < n; ++i) {
+        Dev* d = new Dev();
+        d->owner = c;
+        d->device = ids[i];
+        d->k = knobs;
+        c->devs.push_back(d);
+        hipError_t e = init_dev(d);
+        if (e != hipSuccess) {
+            int rc = fail((ovl_ctx*)nullptr, e == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP,
+                          "context setup on device %d: %s", ids[i], hipGetErrorString(e));
+            ovl_destroy(c);
+            return rc;
+        }
+    }
+    *out = c;
+    return OVL_OK;
+}
+
+// ----------------------------------------------------------------------------- host-array pipeline
+
+// True when [p, p + bytes) is pinned host memory (hipHostMalloc'd or registered), so DMA can
+// read or write it in place.  hipPointerGetAttributes fails (or reports "unregistered") for
+// pageable memory; its sticky error is cleared so later hipGetLastError callers (torch) see none.
+bool host_pinned(const void* p, size_t bytes) {
+    if (!p || bytes == 0) return false;
+    const char* ends[2] = {(const char*)p, (const char*)p + bytes - 1};
+    for (const char* q : ends) {
+        hipPointerAttribute_t at;
+        memset(&at, 0, sizeof(at));
+        if (hipPointerGetAttributes(&at, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (at.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
+// Pairs per pipeline chunk.  Measured on MI355X (tools/pipe_ab.py, profiles/r02_pipe_ab_*.json): every
+// chunk's D2H copy costs ~0.1 ms of fixed overhead, which is more than the kernel time a chunk hides, so
+// copies of pinned arrays run as one chunk; only pageable arrays, which go through pinned staging slots,
+// are cut into 4 M-pair chunks (the slot size).  Direct kernel stores need no chunks at all.
+int64_t pick_chunk(const Dev* d, int64_t n, bool staged) {
+    if (d->k.pipe_chunk > 0) return d->k.pipe_chunk;
+    const int64_t cap = int64_t(1) << 22;
+    return std::max<int64_t>(1, staged ? std::min(n, cap) : n);
+}
+
+hipError_t alloc_staging(int32_t*& p, int64_t cap) {
+    return hipHostMalloc((void**)&p, (size_t)kSlots * 2 * (size_t)cap * sizeof(int32_t), hipHostMallocDefault);
+}
+
+struct Call {
+    const Plan* plan = nullptr;
+    int32_t match = 0, mismatch = 0;
+    int64_t indel = 0;
+    const int32_t* h_a = nullptr;  // host pair list (global indexing), or null: device lists per job
+    const int32_t* h_b = nullptr;
+    bool in_pinned = false;
+    int32_t* out_s = nullptr;      // host results; out_s[p - out_base] for global pair p
+    int32_t* out_e = nullptr;
+    int64_t out_base = 0;
+    bool out_pinned = false;
+    bool direct = false;           // kernels store results straight into the pinned host arrays
+    bool timing = false;
+};
+
+struct Job {
+    Dev* d = nullptr;
+    int64_t lo = 0, hi = 0;  // global pair range of this device
+    int64_t chunk = 1, nchunks = 0;
+    int64_t st_in_cap = 0, st_out_cap = 0;
+    const int32_t* dev_a = nullptr;  // device pair list (global indexing) when the call has no host list
+    const int32_t* dev_b = nullptr;
+    int32_t* ka = nullptr;  // device copies of the host list (local indexing)
+    int32_t* kb = nullptr;
+    int32_t* d_score = nullptr;  // device results (local indexing)
+    int32_t* d_end = nullptr;
+};
+
+int setup_job(const Call& C, Job& J) {
+    Dev* d = J.d;
+    const int64_t n = J.hi - J.lo;
+    if (n <= 0) return OVL_OK;
+    HIPCHK(d, hipSetDevice(d->device));
+    // direct stores from a resident list need no pipeline: one launch per device
+    const bool staged = (C.h_a && !C.in_pinned) || !C.out_pinned;
+    J.chunk = (C.direct && !C.h_a) ? n : pick_chunk(d, n, staged);
+    J.nchunks = (n + J.chunk - 1) / J.chunk;
+    const size_t bytes = sizeof(int32_t) * (size_t)n;
+    if (C.h_a) {
+        HIPCHK(d, ensure(d->a, bytes));
+        HIPCHK(d, ensure(d->b, bytes));
+        J.ka = as<int32_t>(d->a);
+        J.kb = as<int32_t>(d->b);
+    }
+    if (C.direct) {
+        // the device's address of this slice of the caller's pinned arrays
+        void* ps = nullptr;
+        void* pe = nullptr;
+        HIPCHK(d, hipHostGetDevicePointer(&ps, C.out_s + (J.lo - C.out_base), 0));
+        HIPCHK(d, hipHostGetDevicePointer(&pe, C.out_e + (J.lo - C.out_base), 0));
+        J.d_score = reinterpret_cast<int32_t*>(ps);
+        J.d_end = reinterpret_cast<int32_t*>(pe);
+    } else {
+        HIPCHK(d, ensure(d->score, bytes));
+        HIPCHK(d, ensure(d->end, bytes));
+        J.d_score = as<int32_t>(d->score);
+        J.d_end = as<int32_t>(d->end);
+    }
+    // pinned staging rings for pageable caller arrays, both allocated with capacity d->st_cap
+    const bool need_in = C.h_a && !C.in_pinned, need_out = !C.out_pinned;
+    if ((need_in || need_out) && J.chunk > d->st_cap) {
+        free_staging(d->st_in);
+        free_staging(d->st_out);
+        d->st_cap = J.chunk;
+    }
+    if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_cap));
+    if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_cap));
+    if (C.timing && (int64_t)d->t_ev.size() < 2 * J.nchunks) {
+        while ((int64_t)d->t_ev.size() < 2 * J.nchunks) {
+            hipEvent_t ev;
+            HIPCHK(d, hipEventCreate(&ev));
+            d->t_ev.push_back(ev);
+        }
     }
     return OVL_OK;
 }
 
+int issue_chunk(const Call& C, Job& J, int64_t k) {
+    Dev* d = J.d;
+    HIPCHK(d, hipSetDevice(d->device));
+    const int64_t off = k * J.chunk;
+    const int64_t g = J.lo + off;
+    const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
+    const size_t nb = sizeof(int32_t) * (size_t)n;
+    const int slot = (int)(k % kSlots);
+    const int32_t* ka;
+    const int32_t* kb;
+    if (C.h_a) {
+        const int32_t* sa = C.h_a + g;
+        const int32_t* sb = C.h_b + g;
+        if (!C.in_pinned) {
+            // the slot's previous H2D (chunk k - kSlots) must have read it
+            if (k >= kSlots) HIPCHK(d, hipEventSynchronize(d->ev_in[slot]));
+            int32_t* st = d->st_in + (size_t)slot * 2 * (size_t)d->st_cap;
+            memcpy(st, sa, nb);
+            memcpy(st + d->st_cap, sb, nb);
+            sa = st;
+            sb = st + d->st_cap;
+        }
+        HIPCHK(d, hipMemcpyAsync(J.ka + off, sa, nb, hipMemcpyHostToDevice, d->s_in));
+        HIPCHK(d, hipMemcpyAsync(J.kb + off, sb, nb, hipMemcpyHostToDevice, d->s_in));
+        if (!C.in_pinned) HIPCHK(d, hipEventRecord(d->ev_in[slot], d->s_in));
+        HIPCHK(d, hipEventRecord(d->ev_h2d[slot], d->s_in));
+        HIPCHK(d, hipStreamWaitEvent(d->stream, d->ev_h2d[slot], 0));
+        ka = J.ka + off;
+        kb = J.kb + off;
+    } else {
+        ka = J.dev_a + g;
+        kb = J.dev_b + g;
+    }
+    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
+    int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, J.d_score + off, J.d_end + off,
+                          d->stream);
+    if (rc != OVL_OK) return rc;
+    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
+    if (C.direct) return OVL_OK;  // the kernel stored the results in the caller's arrays
+    HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
+    HIPCHK(d, hipStreamWaitEvent(d->s_out, d->ev_k[slot], 0));
+    int32_t* ds;
+    int32_t* de;
+    if (C.out_pinned) {
+        ds = C.out_s + (g - C.out_base);
+        de = C.out_e + (g - C.out_base);
+    } else {
+        ds = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
+        de = ds + d->st_cap;
+    }
+    HIPCHK(d, hipMemcpyAsync(ds, J.d_score + off, nb, hipMemcpyDeviceToHost, d->s_out));
+    HIPCHK(d, hipMemcpyAsync(de, J.d_end + off, nb, hipMemcpyDeviceToHost, d->s_out));
+    HIPCHK(d, hipEventRecord(d->ev_out[slot], d->s_out));
+    return OVL_OK;
+}
+
+// Pageable outputs: copy chunk k out of its staging slot once its D2H is done.
+int drain_chunk(const Call& C, Job& J, int64_t k) {
+    Dev* d = J.d;
+    const int64_t off = k * J.chunk;
+    const int64_t g = J.lo + off;
+    const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
+    const int slot = (int)(k % kSlots);
+    HIPCHK(d, hipEventSynchronize(d->ev_out[slot]));
+    const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
+    memcpy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);
+    memcpy(C.out_e + (g - C.out_base), ss + d->st_cap, sizeof(int32_t) * (size_t)n);
+    return OVL_OK;
+}
+
+void quiesce(std::vector<Job>& jobs) {
+    for (Job& J : jobs) {
+        (void)hipSetDevice(J.d->device);
+        for (hipStream_t s : {J.d->stream, J.d->s_in, J.d->s_out}) (void)hipStreamSynchronize(s);
+    }
+}
+
+int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = OVL_OK;
+    for (Job& J : jobs)
+        if ((rc = setup_job(C, J)) != OVL_OK) return rc;
+    int64_t maxch = 0;
+    for (const Job& J : jobs) maxch = std::max(maxch, J.nchunks);
+    for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
+        for (Job& J : jobs) {
+            if (k >= J.nchunks) continue;
+            if ((rc = issue_chunk(C, J, k)) != OVL_OK) break;
+            if (!C.out_pinned && k >= kSlots - 1 && (rc = drain_chunk(C, J, k - (kSlots - 1))) != OVL_OK) break;
+        }
+    }
+    for (Job& J : jobs) {
+        if (rc != OVL_OK || C.out_pinned) break;
+        for (int64_t k = std::max<int64_t>(0, J.nchunks - (kSlots - 1)); k < J.nchunks; ++k)
+            if ((rc = drain_chunk(C, J, k)) != OVL_OK) break;
+    }
+    // device error flags (a pair index outside [0, n_reads)) come back behind the results
+    for (Job& J : jobs) {
+        if (rc != OVL_OK || J.nchunks == 0) continue;
+        Dev* d = J.d;
+        if (hipSetDevice(d->device) != hipSuccess ||
+            hipMemcpyAsync(d->h_flag, d->err_flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           C.direct ? d->stream : d->s_out) != hipSuccess)
+            rc = fail(c, OVL_E_HIP, "error-flag readback failed");
+    }
+    if (rc != OVL_OK) {
+        quiesce(jobs);
+        return rc;
+    }
+    for (Job& J : jobs) {
+        if (J.nchunks == 0) continue;
+        HIPCHK(c, hipSetDevice(J.d->device));
+        HIPCHK(c, hipStreamSynchronize(C.direct ? J.d->stream : J.d->s_out));
+    }
+    double kms = 0.0;
+    for (Job& J : jobs) {
+        Dev* d = J.d;
+        if (J.nchunks == 0) continue;
+        if (*d->h_flag) {
+            HIPCHK(c, hipSetDevice(d->device));
+            HIPCHK(c, hipMemset(d->err_flag.p, 0, sizeof(uint32_t)));
+            rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
+        }
+        if (C.timing) {
+            double s = 0.0;
+            for (int64_t k = 0; k < J.nchunks; ++k) {
+                float ms = 0.f;
+                if (hipEventElapsedTime(&ms, d->t_ev[2 * k], d->t_ev[2 * k + 1]) == hipSuccess) s += ms;
+            }
+            kms = std::max(kms, s);
+        }
+    }
+    c->t_kernel_ms = kms;
+    c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+// Host-side shard bounds of a host pair list over the context's devices (cost len[a]*len[b] + 1,
+// the rule of ovl_shard_cut).  Indices are not trusted here: an out-of-range index costs 1.
+std::vector<int64_t> host_cuts(const ovl_ctx* c, const int32_t* a, const int32_t* b, int64_t n, int32_t shards) {
+    std::vector<int64_t> cuts((size_t)shards + 1, 0);
+    cuts[(size_t)shards] = n;
+    if (shards == 1 || n == 0) {
+        for (int32_t r = 1; r < shards; ++r) cuts[(size_t)r] = 0;
+        return cuts;
+    }
+    const int64_t nr = (int64_t)c->h_len.size();
+    auto cost = [&](int64_t p) -> int64_t {
+        const int32_t x = a[p], y = b[p];
+        if (x < 0 || x >= nr || y < 0 || y >= nr) return 1;
+        return (int64_t)c->h_len[(size_t)x] * c->h_len[(size_t)y] + 1;
+    };
+    int64_t total = 0;
+    for (int64_t p = 0; p < n; ++p) total += cost(p);
+    int64_t cum = 0, p = 0;
+    for (int32_t r = 1; r < shards; ++r) {
+        const int64_t want = total * r;
+        while (p < n && (cum + cost(p)) * shards < want) cum += cost(p++);
+        cuts[(size_t)r] = p;  // first p with cum[p] * shards >= want
+    }
+    return cuts;
+}
+
+// Shard bounds of [lo, hi) of device 0's resident candidate list over `shards` (ovl_shard_cut).
+int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int64_t>& cuts) {
+    cuts.assign((size_t)shards + 1, lo);
+    cuts[(size_t)shards] = hi;
+    if (shards == 1 || hi <= lo) return OVL_OK;
+    HIPCHK(d, hipSetDevice(d->device));
+    const int64_t n = d->cand_n;
+    size_t temp = 0;
+    HIPCHK(d, ovl_shard_temp_bytes(n, &temp));
+    HIPCHK(d, ensure(d->sh_temp, temp));
+    HIPCHK(d, ensure(d->sh_cum, (size_t)n * sizeof(int64_t)));
+    HIPCHK(d, ensure(d->sh_cuts, ((size_t)shards + 1) * sizeof(int64_t)));
+    HIPCHK(d, ovl_shard_scan(d->sh_temp.p, d->sh_temp.bytes, as<int32_t>(d->cand_a), as<int32_t>(d->cand_b),
+                             as<int32_t>(d->len), n, as<int64_t>(d->sh_cum), d->stream));
+    HIPCHK(d, ovl_shard_cut(as<int64_t>(d->sh_cum), lo, hi, shards, as<int64_t>(d->sh_cuts), d->stream));
+    HIPCHK(d, hipMemcpyAsync(cuts.data(), d->sh_cuts.p, ((size_t)shards + 1) * sizeof(int64_t), hipMemcpyDeviceToHost,
+                             d->stream));
+    HIPCHK(d, hipStreamSynchronize(d->stream));
+    return OVL_OK;
+}
+
+int check_scoring_args(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* p) {
+    // every device holds the same read set, so device 0 plans for all
+    return make_plan(c->devs[0], match, mismatch, indel, band, p);
+}
+
 }  // namespace
+
+// ----------------------------------------------------------------------------- context
 
 OVL_API int ovl_version(void) { return OVL_ABI_VERSION; }
 
 OVL_API const char* ovl_last_error(const ovl_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
 OVL_API int ovl_device_count(int32_t* out_count) {
-    if (!out_count) return fail(nullptr, OVL_E_ARG, "out_count is NULL");
+    if (!out_count) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "out_count is NULL");
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) {
         *out_count = 0;
-        return fail(nullptr, OVL_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+        return fail((ovl_ctx*)nullptr, OVL_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
     }
     *out_count = n;
     return OVL_OK;
 }
 
-OVL_API int ovl_create(int32_t device, ovl_ctx** out_ctx) {
-    if (!out_ctx) return fail(nullptr, OVL_E_ARG, "out_ctx is NULL");
+OVL_API int ovl_create(int32_t n_devices, ovl_ctx** out_ctx) {
+    if (!out_ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "out_ctx is NULL");
     *out_ctx = nullptr;
-    int n = 0;
-    HIPCHK(nullptr, hipGetDeviceCount(&n));
-    if (n <= 0) return fail(nullptr, OVL_E_HIP, "no HIP device visible");
-    if (device < 0) HIPCHK(nullptr, hipGetDevice(&device));
-    if (device >= n) return fail(nullptr, OVL_E_ARG, "device %d >= device count %d", device, n);
-    HIPCHK(nullptr, hipSetDevice(device));
-    ovl_ctx* c = new ovl_ctx();
-    c->device = device;
-    if (const char* sp = getenv("OVL_SPLIT")) {
-        const int v = atoi(sp);
-        if (v >= 0 && v <= 2) c->split_override = v;
-    }
-    if (const char* e = getenv("OVL_BAND_FORM")) {
-        if (!strcmp(e, "diag")) c->band_form = OVL_BAND_FORM_DIAG;
-        else if (!strcmp(e, "rows")) c->band_form = OVL_BAND_FORM_ROWS;
-        else if (!strcmp(e, "fast")) c->band_form = OVL_BAND_FORM_FAST;
-        else if (!strcmp(e, "strip")) c->band_form = OVL_BAND_FORM_STRIP;
-        else if (!strcmp(e, "lane")) c->band_form = OVL_BAND_FORM_LANE;
-    }
-    if (const char* e = getenv("OVL_DP_CLASSIC")) c->dp_classic = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_DP_LANE")) c->dp_lane = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_CW")) c->lane_cw = atoi(e) == 32 ? 32 : 16;
-    if (const char* e = getenv("OVL_LANE_MIN_PAIRS")) c->lane_min_pairs = atoll(e);
-    if (const char* e = getenv("OVL_LANE_PROF")) c->lane_prof = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_COL16")) c->lane_col16 = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_SFX")) c->lane_sfx = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 1024) c->blocks_per_cu = v;
-    }
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-        c->cu_count = prop.multiProcessorCount;
-    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = ensure(c->err_flag, 16);
-    if (e == hipSuccess) e = hipMemset(c->err_flag.p, 0, 16);
-    if (e != hipSuccess) {
-        int rc = fail(nullptr, OVL_E_HIP, "context setup: %s", hipGetErrorString(e));
-        ovl_destroy(c);
-        return rc;
-    }
-    *out_ctx = c;
+    if (n_devices < 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "n_devices < 0 (0 = all visible devices)");
+    int count = 0, cur = 0;
+    HIPCHK((ovl_ctx*)nullptr, hipGetDeviceCount(&count));
+    if (count <= 0) return fail((ovl_ctx*)nullptr, OVL_E_HIP, "no HIP device visible");
+    if (n_devices == 0) n_devices = count;
+    if (n_devices > count)
+        return fail((ovl_ctx*)nullptr, OVL_E_ARG, "n_devices %d > visible devices %d", n_devices, count);
+    HIPCHK((ovl_ctx*)nullptr, hipGetDevice(&cur));
+    std::vector<int32_t> ids((size_t)n_devices);
+    for (int32_t i = 0; i < n_devices; ++i) ids[(size_t)i] = (cur + i) % count;
+    return create_on(ids.data(), n_devices, out_ctx);
+}
+
+OVL_API int ovl_create_on_devices(const int32_t* devices, int32_t n_devices, ovl_ctx** out_ctx) {
+    if (!out_ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "out_ctx is NULL");
+    *out_ctx = nullptr;
+    if (!devices || n_devices <= 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "empty device list");
+    return create_on(devices, n_devices, out_ctx);
+}
+
+OVL_API int ovl_ctx_devices(const ovl_ctx* c, int32_t* ids, int32_t cap, int32_t* out_n) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (out_n) *out_n = (int32_t)c->devs.size();
+    for (int32_t i = 0; ids && i < cap && i < (int32_t)c->devs.size(); ++i) ids[i] = c->devs[(size_t)i]->device;
     return OVL_OK;
 }
 
 OVL_API int ovl_destroy(ovl_ctx* c) {
     if (!c) return OVL_OK;
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->codes, &c->off, &c->len, &c->sfx, &c->pfx, &c->lut, &c->full, &c->a, &c->b, &c->score, &c->end,
-                      &c->tb, &c->err_flag, &c->k_pre, &c->k_suf, &c->k_sorted, &c->k_iota, &c->k_order, &c->k_lo,
-                      &c->k_hi, &c->k_cnt, &c->k_offs, &c->k_temp, &c->cand_a, &c->cand_b, &c->l_q, &c->l_r, &c->l_row,
-                      &c->l_tb, &c->l_best, &c->lane_col})
-        release(*b);
-    if (c->l_tb_host) (void)hipHostFree(c->l_tb_host);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    DeviceGuard guard;
+    for (Dev* d : c->devs) destroy_dev(d);
     delete c;
     return OVL_OK;
 }
 
-OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
-    if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
-    if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
-    HIPCHK(c, hipSetDevice(c->device));
+// ----------------------------------------------------------------------------- pinned host memory
+
+OVL_API int ovl_host_alloc(int64_t bytes, void** out_ptr) {
+    if (!out_ptr) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "out_ptr is NULL");
+    *out_ptr = nullptr;
+    if (bytes < 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "bytes < 0");
+    // OVL_HOST_COHERENT=1 / 0 forces fine-grained (coherent) / coarse-grained host memory (A/B knob);
+    // unset: the HIP runtime's default
+    unsigned flags = hipHostMallocPortable;
+    if (const char* e = getenv("OVL_HOST_COHERENT"))
+        flags |= atoi(e) ? hipHostMallocCoherent : hipHostMallocNonCoherent;
+    HIPCHK((ovl_ctx*)nullptr, hipHostMalloc(out_ptr, (size_t)std::max<int64_t>(bytes, 64), flags));
+    return OVL_OK;
+}
+
+OVL_API int ovl_host_free(void* ptr) {
+    if (ptr) HIPCHK((ovl_ctx*)nullptr, hipHostFree(ptr));
+    return OVL_OK;
+}
+
+OVL_API int ovl_host_register(void* ptr, int64_t bytes) {
+    if (!ptr || bytes <= 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "NULL pointer or empty range");
+    HIPCHK((ovl_ctx*)nullptr, hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable));
+    return OVL_OK;
+}
+
+OVL_API int ovl_host_unregister(void* ptr) {
+    if (!ptr) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "NULL pointer");
+    HIPCHK((ovl_ctx*)nullptr, hipHostUnregister(ptr));
+    return OVL_OK;
+}
+
+OVL_API int ovl_set_timing(ovl_ctx* c, int32_t on) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    c->timing = on ? 1 : 0;
+    return OVL_OK;
+}
+
+OVL_API int ovl_last_timing(const ovl_ctx* c, double* kernel_ms, double* call_ms) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (kernel_ms) *kernel_ms = c->t_kernel_ms;
+    if (call_ms) *call_ms = c->t_call_ms;
+    return OVL_OK;
+}
+
+// ----------------------------------------------------------------------------- reads
+
+namespace {
+
+struct HostReads {
+    std::vector<int64_t> off;
+    std::vector<int32_t> len;
+    std::vector<uint32_t> full;
+    uint8_t lut[256];
+    const uint8_t* src = nullptr;
+    int64_t total = 0;
+    int32_t n_reads = 0, lmax = 0, planes = 2, wmax = 0, srow = 0, trow = 0;
+};
+
+int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads, HostReads& h) {
     const int64_t base = n_reads > 0 ? offsets[0] : 0;
     if (base < 0) return fail(c, OVL_E_ARG, "offsets[0] < 0");
-    std::vector<int64_t> off((size_t)n_reads + 1, 0);
-    std::vector<int32_t> len((size_t)std::max(n_reads, 1), 0);
-    int32_t lmax = 0;
+    h.n_reads = n_reads;
+    h.off.assign((size_t)n_reads + 1, 0);
+    h.len.assign((size_t)std::max(n_reads, 1), 0);
     for (int32_t r = 0; r < n_reads; ++r) {
         const int64_t l = offsets[r + 1] - offsets[r];
         if (l < 0) return fail(c, OVL_E_ARG, "offsets not non-decreasing at read %d", r);
         if (l > INT32_MAX / 2) return fail(c, OVL_E_UNSUPPORTED, "read %d is too long", r);
-        off[r + 1] = offsets[r + 1] - base;
-        len[r] = (int32_t)l;
-        lmax = std::max(lmax, (int32_t)l);
+        h.off[(size_t)r + 1] = offsets[r + 1] - base;
+        h.len[(size_t)r] = (int32_t)l;
+        h.lmax = std::max(h.lmax, (int32_t)l);
     }
-    const int64_t total = n_reads > 0 ? off[n_reads] : 0;
-    std::vector<uint32_t> full(((size_t)std::max(n_reads, 1) + 31) / 32, 0u);
+    h.total = n_reads > 0 ? h.off[(size_t)n_reads] : 0;
+    h.full.assign(((size_t)std::max(n_reads, 1) + 31) / 32, 0u);
     for (int32_t r = 0; r < n_reads; ++r)
-        if (len[r] == lmax) full[(size_t)r >> 5] |= 1u << (r & 31);
-    if (total > 0 && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
+        if (h.len[(size_t)r] == h.lmax) h.full[(size_t)r >> 5] |= 1u << (r & 31);
+    if (h.total > 0 && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
     // alphabet: dense codes in byte order (equality-preserving)
     bool present[256] = {false};
-    const uint8_t* src = seqs ? seqs + base : nullptr;
-    for (int64_t i = 0; i < total; ++i) present[src[i]] = true;
-    uint8_t lut[256] = {0};
+    h.src = seqs ? seqs + base : nullptr;
+    for (int64_t i = 0; i < h.total; ++i) present[h.src[i]] = true;
+    memset(h.lut, 0, sizeof(h.lut));
     int k = 0;
     for (int v = 0; v < 256; ++v)
-        if (present[v]) lut[v] = (uint8_t)k++;
-    const int planes = k <= 4 ? 2 : (k <= 16 ? 4 : 8);
+        if (present[v]) h.lut[v] = (uint8_t)k++;
+    h.planes = k <= 4 ? 2 : (k <= 16 ? 4 : 8);
     // bit-plane layouts: W = ceil(lmax/32) words of 32 bases, rows padded to 16 bytes
-    int32_t wmax = 0;
-    if (lmax <= kFastMaxLen) wmax = std::max(1, (lmax + 31) / 32);
-    const int32_t srow = wmax ? ((wmax * planes + 3) & ~3) : 0;
-    const int32_t trow = wmax ? ((wmax * planes + 3) & ~3) : 0;
+    h.wmax = 0;
+    if (h.lmax <= kFastMaxLen) h.wmax = std::max(1, (h.lmax + 31) / 32);
+    h.srow = h.wmax ? ((h.wmax * h.planes + 3) & ~3) : 0;
+    h.trow = h.srow;
+    return OVL_OK;
+}
 
-    c->n_reads = -1;  // invalid until fully built
-    c->cand_n = -1;
-    DevBuf raw;
-    HIPCHK(c, ensure(c->off, sizeof(int64_t) * off.size()));
-    HIPCHK(c, ensure(c->len, sizeof(int32_t) * len.size()));
-    HIPCHK(c, ensure(c->codes, (size_t)total + 64));  // tail pad: clamped reads of empty last reads
-    HIPCHK(c, ensure(c->lut, 256));
-    hipError_t e = ensure(raw, (size_t)total);
-    if (e != hipSuccess) return fail(c, OVL_E_OOM, "raw read buffer: %s", hipGetErrorString(e));
-    int rc = OVL_OK;
-    do {
-        e = hipMemcpyAsync(c->off.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, c->stream);
-        if (e != hipSuccess) break;
-        e = hipMemcpyAsync(c->len.p, len.data(), sizeof(int32_t) * len.size(), hipMemcpyHostToDevice, c->stream);
-        if (e != hipSuccess) break;
-        e = hipMemcpyAsync(c->lut.p, lut, 256, hipMemcpyHostToDevice, c->stream);
-        if (e != hipSuccess) break;
-        e = ensure(c->full, sizeof(uint32_t) * full.size());
-        if (e != hipSuccess) break;
-        e = hipMemcpyAsync(c->full.p, full.data(), sizeof(uint32_t) * full.size(), hipMemcpyHostToDevice, c->stream);
-        if (e != hipSuccess) break;
-        if (total > 0) {
-            e = hipMemcpyAsync(raw.p, src, (size_t)total, hipMemcpyHostToDevice, c->stream);
-            if (e != hipSuccess) break;
-            e = ovl_launch_map_codes(as<uint8_t>(raw), as<uint8_t>(c->lut), as<uint8_t>(c->codes), total, c->stream);
-            if (e != hipSuccess) break;
-        }
-        if (wmax > 0) {
-            const size_t rows = (size_t)std::max(n_reads, 1);
-            e = ensure(c->sfx, rows * srow * sizeof(uint32_t));
-            if (e != hipSuccess) break;
-            e = ensure(c->pfx, rows * trow * sizeof(uint32_t));
-            if (e != hipSuccess) break;
-            e = hipMemsetAsync(c->sfx.p, 0, rows * srow * sizeof(uint32_t), c->stream);
-            if (e != hipSuccess) break;
-            e = hipMemsetAsync(c->pfx.p, 0, rows * trow * sizeof(uint32_t), c->stream);
-            if (e != hipSuccess) break;
-            e = ovl_launch_pack(planes, as<uint8_t>(c->codes), as<int64_t>(c->off), as<int32_t>(c->len), n_reads,
-                                wmax, srow, trow, as<uint32_t>(c->sfx), as<uint32_t>(c->pfx), c->stream);
-            if (e != hipSuccess) break;
-        }
-        e = hipStreamSynchronize(c->stream);
-    } while (false);
-    release(raw);
+// Asynchronous upload + pack of one device's copy; the caller synchronises d->stream.
+hipError_t upload_reads(Dev* d, const HostReads& h) {
+    hipError_t e = hipSetDevice(d->device);
+    if (e != hipSuccess) return e;
+    d->n_reads = -1;  // invalid until fully built
+    d->cand_n = -1;
+    const int32_t n_reads = h.n_reads;
+    if ((e = ensure(d->off, sizeof(int64_t) * h.off.size())) != hipSuccess) return e;
+    if ((e = ensure(d->len, sizeof(int32_t) * h.len.size())) != hipSuccess) return e;
+    if ((e = ensure(d->codes, (size_t)h.total + 64)) != hipSuccess) return e;  // tail pad: clamped reads
+    if ((e = ensure(d->lut, 256)) != hipSuccess) return e;
+    if ((e = ensure(d->raw, (size_t)h.total)) != hipSuccess) return e;
+    if ((e = ensure(d->full, sizeof(uint32_t) * h.full.size())) != hipSuccess) return e;
+    hipStream_t s = d->stream;
+    if ((e = hipMemcpyAsync(d->off.p, h.off.data(), sizeof(int64_t) * h.off.size(), hipMemcpyHostToDevice, s)))
+        return e;
+    if ((e = hipMemcpyAsync(d->len.p, h.len.data(), sizeof(int32_t) * h.len.size(), hipMemcpyHostToDevice, s)))
+        return e;
+    if ((e = hipMemcpyAsync(d->lut.p, h.lut, 256, hipMemcpyHostToDevice, s))) return e;
+    if ((e = hipMemcpyAsync(d->full.p, h.full.data(), sizeof(uint32_t) * h.full.size(), hipMemcpyHostToDevice, s)))
+        return e;
+    if (h.total > 0) {
+        if ((e = hipMemcpyAsync(d->raw.p, h.src, (size_t)h.total, hipMemcpyHostToDevice, s))) return e;
+        if ((e = ovl_launch_map_codes(as<uint8_t>(d->raw), as<uint8_t>(d->lut), as<uint8_t>(d->codes), h.total, s)))
+            return e;
+    }
+    if (h.wmax > 0) {
+        const size_t rows = (size_t)std::max(n_reads, 1);
+        if ((e = ensure(d->sfx, rows * h.srow * sizeof(uint32_t)))) return e;
+        if ((e = ensure(d->pfx, rows * h.trow * sizeof(uint32_t)))) return e;
+        if ((e = hipMemsetAsync(d->sfx.p, 0, rows * h.srow * sizeof(uint32_t), s))) return e;
+        if ((e = hipMemsetAsync(d->pfx.p, 0, rows * h.trow * sizeof(uint32_t), s))) return e;
+        if ((e = ovl_launch_pack(h.planes, as<uint8_t>(d->codes), as<int64_t>(d->off), as<int32_t>(d->len), n_reads,
+                                 h.wmax, h.srow, h.trow, as<uint32_t>(d->sfx), as<uint32_t>(d->pfx), s)))
+            return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
+    if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
+    DeviceGuard guard;
+    HostReads h;
+    int rc = prep_reads(c, seqs, offsets, n_reads, h);
+    if (rc != OVL_OK) return rc;
+    c->h_len.clear();
+    hipError_t e = hipSuccess;
+    for (Dev* d : c->devs) {
+        d->n_reads = -1;
+        d->cand_n = -1;
+    }
+    // upload to every device, then wait for all (the uploads and packs overlap across devices)
+    for (Dev* d : c->devs)
+        if ((e = upload_reads(d, h)) != hipSuccess) break;
+    for (Dev* d : c->devs) {
+        (void)hipSetDevice(d->device);
+        hipError_t e2 = hipStreamSynchronize(d->stream);
+        if (e == hipSuccess) e = e2;
+        release(d->raw);
+    }
     if (e != hipSuccess)
         return fail(c, e == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP, "ovl_set_reads: %s", hipGetErrorString(e));
-    c->lmax = lmax;
-    c->codes_bytes = total;
-    c->planes = planes;
-    c->wmax = wmax;
-    c->srow = srow;
-    c->trow = trow;
-    c->n_reads = n_reads;
-    return rc;
+    for (Dev* d : c->devs) {
+        d->lmax = h.lmax;
+        d->codes_bytes = h.total;
+        d->planes = h.planes;
+        d->wmax = h.wmax;
+        d->srow = h.srow;
+        d->trow = h.trow;
+        d->n_reads = n_reads;
+    }
+    c->h_len.assign(h.len.begin(), h.len.begin() + n_reads);
+    return OVL_OK;
 }
 
 OVL_API int ovl_reads_info(const ovl_ctx* c, int32_t* n_reads, int32_t* lmax, int32_t* planes, int64_t* device_bytes) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
-    if (n_reads) *n_reads = c->n_reads;
-    if (lmax) *lmax = c->lmax;
-    if (planes) *planes = c->planes;
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    const Dev* d = c->devs[0];
+    if (n_reads) *n_reads = d->n_reads;
+    if (lmax) *lmax = d->lmax;
+    if (planes) *planes = d->planes;
     if (device_bytes)
-        *device_bytes = (int64_t)(c->codes.bytes + c->off.bytes + c->len.bytes + c->sfx.bytes + c->pfx.bytes);
+        *device_bytes = (int64_t)(d->codes.bytes + d->off.bytes + d->len.bytes + d->sfx.bytes + d->pfx.bytes);
     return OVL_OK;
 }
 
 OVL_API int ovl_plan(const ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
                      int32_t* out_kernel) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (!out_kernel) return fail(c, OVL_E_ARG, "out_kernel is NULL");
     Plan p;
-    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    int rc = make_plan(c->devs[0], match, mismatch, indel, band, &p);
     if (rc != OVL_OK) return rc;
     *out_kernel = p.kernel;
     return OVL_OK;
 }
 
+// ----------------------------------------------------------------------------- scoring
+
 OVL_API int ovl_score_device(ovl_ctx* c, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs, int32_t match,
                              int32_t mismatch, int64_t indel, int32_t band, int32_t* d_score, int32_t* d_end,
                              void* stream) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (n_pairs < 0) return fail(c, OVL_E_ARG, "n_pairs < 0");
     if (n_pairs > 0 && (!d_a || !d_b || !d_score || !d_end)) return fail(c, OVL_E_ARG, "NULL device pointer");
+    Dev* d = c->devs[0];
     Plan p;
-    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    int rc = make_plan(d, match, mismatch, indel, band, &p);
     if (rc != OVL_OK) return rc;
-    if (n_pairs > 0 && c->n_reads == 0) return fail(c, OVL_E_INDEX, "pairs given but the read set is empty");
-    HIPCHK(c, hipSetDevice(c->device));
+    if (n_pairs > 0 && d->n_reads == 0) return fail(c, OVL_E_INDEX, "pairs given but the read set is empty");
+    DeviceGuard guard;
+    HIPCHK(c, hipSetDevice(d->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the default (null) stream
-    return launch_score(c, p, d_a, d_b, n_pairs, match, mismatch, indel, d_score, d_end, s);
+    return launch_score(d, p, d_a, d_b, n_pairs, match, mismatch, indel, d_score, d_end, s);
 }
 
 OVL_API int ovl_check_device_errors(ovl_ctx* c) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipDeviceSynchronize());
-    uint32_t flag = 0;
-    HIPCHK(c, hipMemcpy(&flag, c->err_flag.p, sizeof(flag), hipMemcpyDeviceToHost));
-    if (flag) {
-        HIPCHK(c, hipMemset(c->err_flag.p, 0, sizeof(uint32_t)));
-        return fail(c, OVL_E_INDEX, "a device scoring call saw a pair index outside [0, n_reads)");
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    DeviceGuard guard;
+    int rc = OVL_OK;
+    for (Dev* d : c->devs) {
+        HIPCHK(c, hipSetDevice(d->device));
+        HIPCHK(c, hipDeviceSynchronize());
+        uint32_t flag = 0;
+        HIPCHK(c, hipMemcpy(&flag, d->err_flag.p, sizeof(flag), hipMemcpyDeviceToHost));
+        if (flag) {
+            HIPCHK(c, hipMemset(d->err_flag.p, 0, sizeof(uint32_t)));
+            rc = fail(c, OVL_E_INDEX, "a device scoring call saw a pair index outside [0, n_reads)");
+        }
     }
-    return OVL_OK;
+    return rc;
 }
 
 OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs, int32_t match,
                            int32_t mismatch, int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (n_pairs < 0) return fail(c, OVL_E_ARG, "n_pairs < 0");
-    if (n_pairs > 0 && (!a_idx || !b_idx || !out_score || !out_end)) return fail(c, OVL_E_ARG, "NULL host pointer");
+    if (n_pairs > 0 && (!a_idx || !b_idx || !out_score || !out_end))
+        return fail(c, OVL_E_ARG, "NULL host pointer");
     Plan p;
-    int rc = make_plan(c, match, mismatch, indel, band, &p);
+    int rc = check_scoring_args(c, match, mismatch, indel, band, &p);
     if (rc != OVL_OK) return rc;
     if (n_pairs == 0) return OVL_OK;
-    rc = check_indices(c, a_idx, b_idx, n_pairs);
-    if (rc != OVL_OK) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    if (c->devs[0]->n_reads == 0) return fail(c, OVL_E_INDEX, "pairs given but the read set is empty");
+    DeviceGuard guard;
     const size_t bytes = sizeof(int32_t) * (size_t)n_pairs;
-    HIPCHK(c, ensure(c->a, bytes));
-    HIPCHK(c, ensure(c->b, bytes));
-    HIPCHK(c, ensure(c->score, bytes));
-    HIPCHK(c, ensure(c->end, bytes));
-    HIPCHK(c, hipMemcpyAsync(c->a.p, a_idx, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->b.p, b_idx, bytes, hipMemcpyHostToDevice, c->stream));
-    rc = launch_score(c, p, as<int32_t>(c->a), as<int32_t>(c->b), n_pairs, match, mismatch, indel,
-                      as<int32_t>(c->score), as<int32_t>(c->end), c->stream);
-    if (rc != OVL_OK) return rc;
-    HIPCHK(c, hipMemcpyAsync(out_score, c->score.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out_end, c->end.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    return OVL_OK;
+    Call C;
+    C.plan = &p;
+    C.match = match;
+    C.mismatch = mismatch;
+    C.indel = indel;
+    C.h_a = a_idx;
+    C.h_b = b_idx;
+    C.in_pinned = host_pinned(a_idx, bytes) && host_pinned(b_idx, bytes);
+    C.out_s = out_score;
+    C.out_e = out_end;
+    C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
+    C.timing = c->timing != 0;
+    // banded plans read their seed back from the outputs: those keep device buffers
+    C.direct = C.out_pinned && p.kernel != OVL_KERNEL_BANDED && c->devs[0]->k.pipe_direct;
+    const int32_t S = (int32_t)c->devs.size();
+    const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
+    std::vector<Job> jobs((size_t)S);
+    for (int32_t r = 0; r < S; ++r) {
+        jobs[(size_t)r].d = c->devs[(size_t)r];
+        jobs[(size_t)r].lo = cuts[(size_t)r];
+        jobs[(size_t)r].hi = cuts[(size_t)r + 1];
+    }
+    return run_pipeline(c, C, jobs);
 }
 
 OVL_API int ovl_score_pairs(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
@@ -631,14 +1204,16 @@ OVL_API int ovl_score_pairs(ovl_ctx* c, const uint8_t* seqs, const int64_t* offs
     return ovl_score_host(c, a_idx, b_idx, n_pairs, match, mismatch, indel, band, out_score, out_end);
 }
 
-OVL_API int ovl_align_one(ovl_ctx* c, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
+OVL_API int ovl_align_one(ovl_ctx* ctx, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
                           int32_t* out_score, int32_t* out_end, int8_t* traceback) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    Dev* c = ctx->devs[0];
     if (!out_score || !out_end) return fail(c, OVL_E_ARG, "NULL output pointer");
     if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
     if (a < 0 || a >= c->n_reads || b < 0 || b >= c->n_reads)
         return fail(c, OVL_E_INDEX, "pair (%d, %d) outside [0, %d)", a, b, c->n_reads);
     if (c->lmax > kDpMaxLen) return fail(c, OVL_E_UNSUPPORTED, "DP supports reads up to %d bases", kDpMaxLen);
+    DeviceGuard guard;
     HIPCHK(c, hipSetDevice(c->device));
     // lengths from the host-visible offsets copy
     int64_t offs[2][2];
@@ -687,20 +1262,16 @@ OVL_API int ovl_align_one(ovl_ctx* c, int32_t a, int32_t b, int32_t match, int32
 
 // ----------------------------------------------------------------------------- candidate enumeration
 
-OVL_API int ovl_candidates(ovl_ctx* c, int32_t k, int64_t* out_n_pairs) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
-    if (!out_n_pairs) return fail(c, OVL_E_ARG, "out_n_pairs is NULL");
-    if (k < 0) return fail(c, OVL_E_ARG, "k-mer length must be non-negative (k=%d)", k);
-    if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
-    const int32_t bits = c->planes;  // symbol codes are dense: < 2^planes
-    if (k > 0 && (int64_t)k * bits > 58)
-        return fail(c, OVL_E_UNSUPPORTED, "k=%d with %d-bit symbols does not fit a 64-bit key (k * bits <= 58)", k,
-                    bits);
+namespace {
+
+// Keys, sort, per-read groups and their offsets; the list length comes back in d->cand_tail.
+int cand_count(Dev* c, int32_t k) {
     HIPCHK(c, hipSetDevice(c->device));
     c->cand_n = -1;
     const int32_t n = c->n_reads;
     const size_t nr = (size_t)std::max(n, 1);
     const int all = k == 0 ? 1 : 0;
+    const int32_t bits = c->planes;  // symbol codes are dense: < 2^planes
     hipStream_t s = c->stream;
     HIPCHK(c, ensure(c->k_lo, nr * sizeof(int64_t)));
     HIPCHK(c, ensure(c->k_hi, nr * sizeof(int64_t)));
@@ -723,29 +1294,73 @@ OVL_API int ovl_candidates(ovl_ctx* c, int32_t k, int64_t* out_n_pairs) {
     HIPCHK(c, ovl_cand_count(as<uint64_t>(c->k_sorted), as<uint64_t>(c->k_pre), as<uint64_t>(c->k_suf), n, all,
                              as<int64_t>(c->k_lo), as<int64_t>(c->k_hi), as<int64_t>(c->k_cnt), s));
     HIPCHK(c, ovl_cand_scan(c->k_temp.p, c->k_temp.bytes, as<int64_t>(c->k_cnt), as<int64_t>(c->k_offs), n, s));
-    int64_t tail[2] = {0, 0};
+    c->cand_tail[0] = c->cand_tail[1] = 0;
     if (n > 0) {
-        HIPCHK(c, hipMemcpyAsync(&tail[0], as<int64_t>(c->k_offs) + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(&tail[1], as<int64_t>(c->k_cnt) + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(&c->cand_tail[0], as<int64_t>(c->k_offs) + (n - 1), sizeof(int64_t),
+                                 hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(&c->cand_tail[1], as<int64_t>(c->k_cnt) + (n - 1), sizeof(int64_t),
+                                 hipMemcpyDeviceToHost, s));
     }
-    HIPCHK(c, hipStreamSynchronize(s));
-    const int64_t total = tail[0] + tail[1];
+    return OVL_OK;
+}
+
+int cand_emit(Dev* c, int32_t k) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t total = c->cand_tail[0] + c->cand_tail[1];
     HIPCHK(c, ensure(c->cand_a, (size_t)total * sizeof(int32_t)));
     HIPCHK(c, ensure(c->cand_b, (size_t)total * sizeof(int32_t)));
     if (total > 0)
         HIPCHK(c, ovl_cand_emit(as<int32_t>(c->k_order), as<int64_t>(c->k_lo), as<int64_t>(c->k_hi),
-                                as<int64_t>(c->k_offs), n, all, as<int32_t>(c->cand_a), as<int32_t>(c->cand_b), s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    c->cand_n = total;
+                                as<int64_t>(c->k_offs), c->n_reads, k == 0 ? 1 : 0, as<int32_t>(c->cand_a),
+                                as<int32_t>(c->cand_b), c->stream));
+    return OVL_OK;
+}
+
+}  // namespace
+
+OVL_API int ovl_candidates(ovl_ctx* ctx, int32_t k, int64_t* out_n_pairs) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!out_n_pairs) return fail(ctx, OVL_E_ARG, "out_n_pairs is NULL");
+    if (k < 0) return fail(ctx, OVL_E_ARG, "k-mer length must be non-negative (k=%d)", k);
+    Dev* d0 = ctx->devs[0];
+    if (d0->n_reads < 0) return fail(ctx, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
+    const int32_t bits = d0->planes;
+    if (k > 0 && (int64_t)k * bits > 58)
+        return fail(ctx, OVL_E_UNSUPPORTED, "k=%d with %d-bit symbols does not fit a 64-bit key (k * bits <= 58)", k,
+                    bits);
+    DeviceGuard guard;
+    // every device enumerates the same list from its own copy of the reads (no list broadcast); the
+    // phases overlap across devices
+    int rc = OVL_OK;
+    for (Dev* d : ctx->devs)
+        if ((rc = cand_count(d, k)) != OVL_OK) break;
+    for (Dev* d : ctx->devs) {
+        (void)hipSetDevice(d->device);
+        hipError_t e = hipStreamSynchronize(d->stream);
+        if (rc == OVL_OK && e != hipSuccess) rc = fail(ctx, OVL_E_HIP, "ovl_candidates: %s", hipGetErrorString(e));
+    }
+    if (rc != OVL_OK) return rc;
+    for (Dev* d : ctx->devs)
+        if ((rc = cand_emit(d, k)) != OVL_OK) break;
+    for (Dev* d : ctx->devs) {
+        (void)hipSetDevice(d->device);
+        hipError_t e = hipStreamSynchronize(d->stream);
+        if (rc == OVL_OK && e != hipSuccess) rc = fail(ctx, OVL_E_HIP, "ovl_candidates: %s", hipGetErrorString(e));
+    }
+    if (rc != OVL_OK) return rc;
+    const int64_t total = d0->cand_tail[0] + d0->cand_tail[1];
+    for (Dev* d : ctx->devs) d->cand_n = total;
     *out_n_pairs = total;
     return OVL_OK;
 }
 
-OVL_API int ovl_candidates_copy(ovl_ctx* c, int32_t* a_idx, int32_t* b_idx) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+OVL_API int ovl_candidates_copy(ovl_ctx* ctx, int32_t* a_idx, int32_t* b_idx) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    Dev* c = ctx->devs[0];
     if (c->cand_n < 0) return fail(c, OVL_E_STATE, "no candidate list: call ovl_candidates first");
     if (c->cand_n == 0) return OVL_OK;
     if (!a_idx || !b_idx) return fail(c, OVL_E_ARG, "NULL host pointer");
+    DeviceGuard guard;
     HIPCHK(c, hipSetDevice(c->device));
     const size_t bytes = (size_t)c->cand_n * sizeof(int32_t);
     HIPCHK(c, hipMemcpyAsync(a_idx, c->cand_a.p, bytes, hipMemcpyDeviceToHost, c->stream));
@@ -754,9 +1369,10 @@ OVL_API int ovl_candidates_copy(ovl_ctx* c, int32_t* a_idx, int32_t* b_idx) {
     return OVL_OK;
 }
 
-OVL_API int ovl_candidates_device(const ovl_ctx* c, const int32_t** d_a_idx, const int32_t** d_b_idx,
+OVL_API int ovl_candidates_device(const ovl_ctx* ctx, const int32_t** d_a_idx, const int32_t** d_b_idx,
                                   int64_t* n_pairs) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    const Dev* c = ctx->devs[0];
     if (c->cand_n < 0) return fail(c, OVL_E_STATE, "no candidate list: call ovl_candidates first");
     if (d_a_idx) *d_a_idx = reinterpret_cast<const int32_t*>(c->cand_a.p);
     if (d_b_idx) *d_b_idx = reinterpret_cast<const int32_t*>(c->cand_b.p);
@@ -764,36 +1380,79 @@ OVL_API int ovl_candidates_device(const ovl_ctx* c, const int32_t** d_a_idx, con
     return OVL_OK;
 }
 
-OVL_API int ovl_score_candidates(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
-                                 int32_t* out_score, int32_t* out_end) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
-    if (c->cand_n < 0) return fail(c, OVL_E_STATE, "no candidate list: call ovl_candidates first");
-    Plan p;
-    int rc = make_plan(c, match, mismatch, indel, band, &p);
+OVL_API int ovl_candidates_shards(ovl_ctx* ctx, int32_t n_shards, int64_t* bounds) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (n_shards <= 0 || !bounds) return fail(ctx, OVL_E_ARG, "n_shards <= 0 or bounds is NULL");
+    Dev* d = ctx->devs[0];
+    if (d->cand_n < 0) return fail(ctx, OVL_E_STATE, "no candidate list: call ovl_candidates first");
+    DeviceGuard guard;
+    std::vector<int64_t> cuts;
+    int rc = device_cuts(d, 0, d->cand_n, n_shards, cuts);
     if (rc != OVL_OK) return rc;
-    const int64_t n = c->cand_n;
-    if (n == 0) return OVL_OK;
-    if (!out_score || !out_end) return fail(c, OVL_E_ARG, "NULL host pointer");
-    HIPCHK(c, hipSetDevice(c->device));
-    const size_t bytes = sizeof(int32_t) * (size_t)n;
-    HIPCHK(c, ensure(c->score, bytes));
-    HIPCHK(c, ensure(c->end, bytes));
-    rc = launch_score(c, p, as<int32_t>(c->cand_a), as<int32_t>(c->cand_b), n, match, mismatch, indel,
-                      as<int32_t>(c->score), as<int32_t>(c->end), c->stream);
-    if (rc != OVL_OK) return rc;
-    HIPCHK(c, hipMemcpyAsync(out_score, c->score.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(out_end, c->end.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::copy(cuts.begin(), cuts.end(), bounds);
     return OVL_OK;
+}
+
+OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t match, int32_t mismatch,
+                                       int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    Dev* d0 = ctx->devs[0];
+    if (d0->cand_n < 0) return fail(ctx, OVL_E_STATE, "no candidate list: call ovl_candidates first");
+    if (lo < 0 || hi < lo || hi > d0->cand_n)
+        return fail(ctx, OVL_E_ARG, "range [%lld, %lld) outside the candidate list [0, %lld)", (long long)lo,
+                    (long long)hi, (long long)d0->cand_n);
+    Plan p;
+    int rc = check_scoring_args(ctx, match, mismatch, indel, band, &p);
+    if (rc != OVL_OK) return rc;
+    if (hi == lo) return OVL_OK;
+    if (!out_score || !out_end) return fail(ctx, OVL_E_ARG, "NULL host pointer");
+    DeviceGuard guard;
+    const size_t bytes = sizeof(int32_t) * (size_t)(hi - lo);
+    Call C;
+    C.plan = &p;
+    C.match = match;
+    C.mismatch = mismatch;
+    C.indel = indel;
+    C.out_s = out_score;
+    C.out_e = out_end;
+    C.out_base = lo;
+    C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
+    C.timing = ctx->timing != 0;
+    // banded plans read their seed back from the outputs: those keep device buffers
+    C.direct = C.out_pinned && p.kernel != OVL_KERNEL_BANDED && ctx->devs[0]->k.pipe_direct;
+    const int32_t S = (int32_t)ctx->devs.size();
+    std::vector<int64_t> cuts;
+    rc = device_cuts(d0, lo, hi, S, cuts);
+    if (rc != OVL_OK) return rc;
+    std::vector<Job> jobs((size_t)S);
+    for (int32_t r = 0; r < S; ++r) {
+        Job& J = jobs[(size_t)r];
+        J.d = ctx->devs[(size_t)r];
+        J.lo = cuts[(size_t)r];
+        J.hi = cuts[(size_t)r + 1];
+        J.dev_a = as<int32_t>(J.d->cand_a);
+        J.dev_b = as<int32_t>(J.d->cand_b);
+    }
+    return run_pipeline(ctx, C, jobs);
+}
+
+OVL_API int ovl_score_candidates(ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
+                                 int32_t* out_score, int32_t* out_end) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    const int64_t n = ctx->devs[0]->cand_n;
+    if (n < 0) return fail(ctx, OVL_E_STATE, "no candidate list: call ovl_candidates first");
+    return ovl_score_candidates_range(ctx, 0, n, match, mismatch, indel, band, out_score, out_end);
 }
 
 // ----------------------------------------------------------------------------- local alignment
 
-OVL_API int ovl_local_align(ovl_ctx* c, const uint8_t* query, int32_t n, const uint8_t* ref, int32_t m,
+OVL_API int ovl_local_align(ovl_ctx* ctx, const uint8_t* query, int32_t n, const uint8_t* ref, int32_t m,
                             int32_t match, int32_t mismatch, int64_t indel, int32_t* out_score, int32_t* out_end_i,
                             int32_t* out_end_j, int32_t* out_start_i, int32_t* out_start_j, int8_t* ops,
                             int64_t ops_cap, int64_t* out_n_ops) {
-    if (!c) return fail(nullptr, OVL_E_ARG, "ctx is NULL");
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    Dev* c = ctx->devs[0];
+    DeviceGuard guard;
     if (n < 0 || m < 0) return fail(c, OVL_E_ARG, "negative length");
     if ((n > 0 && !query) || (m > 0 && !ref)) return fail(c, OVL_E_ARG, "NULL sequence");
     if (!out_score || !out_end_i || !out_end_j || !out_start_i || !out_start_j || !out_n_ops)

@@ -173,3 +173,66 @@ extern "C" hipError_t ovl_cand_emit(const int32_t* order, const int64_t* lo, con
                                                                                     all_pairs, out_a, out_b);
     return hipGetLastError();
 }
+
+// ----------------------------------------------------------------------------- shard bounds
+// Contiguous shards of a pair list balanced by cost(p) = len[a]*len[b] + 1 (the
+// DP work of a pair is n*m cells), the cut rule of ovlgraph/sharded.py:shard_bounds: inside
+// [lo, hi), cut_r = the first p with (cum[p] - base) * S >= total * r, where cum is the inclusive
+// prefix sum of the costs, base = cum[lo - 1] and total = cum[hi - 1] - base; cuts are made
+// non-decreasing, cut_0 = lo and cut_S = hi.  cum fits int64 (<= 2^31 pairs x 2^30 + 1).
+namespace ovl_cand {
+
+struct PairCost {
+    const int32_t* a;
+    const int32_t* b;
+    const int32_t* len;
+    __host__ __device__ int64_t operator()(const int64_t& p) const {
+        return (int64_t)len[a[p]] * (int64_t)len[b[p]] + 1;
+    }
+};
+
+__global__ void cut_kernel(const int64_t* __restrict__ cum, int64_t lo, int64_t hi, int32_t shards,
+                           int64_t* __restrict__ cuts) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t base = lo > 0 ? cum[lo - 1] : 0;
+    const int64_t total = hi > lo ? cum[hi - 1] - base : 0;
+    int64_t prev = lo;
+    cuts[0] = lo;
+    for (int32_t r = 1; r < shards; ++r) {
+        int64_t a = lo, b = hi;
+        const int64_t want = total * r;
+        while (a < b) {
+            const int64_t mid = (a + b) >> 1;
+            if ((cum[mid] - base) * shards >= want) b = mid;
+            else a = mid + 1;
+        }
+        prev = a > prev ? a : prev;
+        cuts[r] = prev;
+    }
+    cuts[shards] = hi;
+}
+
+}  // namespace ovl_cand
+
+using ovl_cand::PairCost;
+typedef hipcub::TransformInputIterator<int64_t, PairCost, hipcub::CountingInputIterator<int64_t>> CostIter;
+
+extern "C" hipError_t ovl_shard_temp_bytes(int64_t n_pairs, size_t* bytes) {
+    PairCost f{nullptr, nullptr, nullptr};
+    CostIter it(hipcub::CountingInputIterator<int64_t>(0), f);
+    return hipcub::DeviceScan::InclusiveSum(nullptr, *bytes, it, (int64_t*)nullptr, n_pairs);
+}
+
+extern "C" hipError_t ovl_shard_scan(void* temp, size_t temp_bytes, const int32_t* a, const int32_t* b,
+                                     const int32_t* len, int64_t n_pairs, int64_t* cum, hipStream_t stream) {
+    if (n_pairs <= 0) return hipSuccess;
+    PairCost f{a, b, len};
+    CostIter it(hipcub::CountingInputIterator<int64_t>(0), f);
+    return hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, it, cum, n_pairs, stream);
+}
+
+extern "C" hipError_t ovl_shard_cut(const int64_t* cum, int64_t lo, int64_t hi, int32_t shards, int64_t* cuts,
+                                    hipStream_t stream) {
+    ovl_cand::cut_kernel<<<1, 64, 0, stream>>>(cum, lo, hi, shards, cuts);
+    return hipGetLastError();
+}

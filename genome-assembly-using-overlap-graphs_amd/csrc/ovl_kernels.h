@@ -109,3 +109,11 @@ extern "C" hipError_t ovl_launch_local(const uint8_t* q, int32_t n, const uint8_
                                        int64_t mismatch, int64_t indel, int32_t wide, uint64_t* rowbuf, int8_t* tb,
                                        unsigned long long* best, uint32_t* err_flag, int32_t blocks, uint32_t epoch,
                                        hipStream_t stream);
+
+// shard bounds of a pair list balanced by len[a]*len[b] + 1 (ovl_candidates.hip): ovl_shard_scan writes
+// the inclusive prefix sum of the costs (n_pairs int64), ovl_shard_cut the shards + 1 cuts of [lo, hi)
+extern "C" hipError_t ovl_shard_temp_bytes(int64_t n_pairs, size_t* bytes);
+extern "C" hipError_t ovl_shard_scan(void* temp, size_t temp_bytes, const int32_t* a, const int32_t* b,
+                                     const int32_t* len, int64_t n_pairs, int64_t* cum, hipStream_t stream);
+extern "C" hipError_t ovl_shard_cut(const int64_t* cum, int64_t lo, int64_t hi, int32_t shards, int64_t* cuts,
+                                    hipStream_t stream);

@@ -16,7 +16,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_ROOT, "build", "libovl.so")
 CSRC = os.path.join(PKG_ROOT, "csrc")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OVL_OK = 0
 ERRORS = {
@@ -35,7 +35,15 @@ SIGNATURES = {
     "ovl_version": (ctypes.c_int, []),
     "ovl_device_count": (ctypes.c_int, [_pi32]),
     "ovl_create": (ctypes.c_int, [_i32, ctypes.POINTER(_P)]),
+    "ovl_create_on_devices": (ctypes.c_int, [_P, _i32, ctypes.POINTER(_P)]),
+    "ovl_ctx_devices": (ctypes.c_int, [_P, _P, _i32, _pi32]),
     "ovl_destroy": (ctypes.c_int, [_P]),
+    "ovl_host_alloc": (ctypes.c_int, [_i64, ctypes.POINTER(_P)]),
+    "ovl_host_free": (ctypes.c_int, [_P]),
+    "ovl_host_register": (ctypes.c_int, [_P, _i64]),
+    "ovl_host_unregister": (ctypes.c_int, [_P]),
+    "ovl_set_timing": (ctypes.c_int, [_P, _i32]),
+    "ovl_last_timing": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "ovl_last_error": (ctypes.c_char_p, [_P]),
     "ovl_score_pairs": (ctypes.c_int, [_P, _P, _P, _i32, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P]),
     "ovl_set_reads": (ctypes.c_int, [_P, _P, _P, _i32]),
@@ -49,6 +57,8 @@ SIGNATURES = {
     "ovl_candidates_copy": (ctypes.c_int, [_P, _P, _P]),
     "ovl_candidates_device": (ctypes.c_int, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), _pi64]),
     "ovl_score_candidates": (ctypes.c_int, [_P, _i32, _i32, _i64, _i32, _P, _P]),
+    "ovl_score_candidates_range": (ctypes.c_int, [_P, _i64, _i64, _i32, _i32, _i64, _i32, _P, _P]),
+    "ovl_candidates_shards": (ctypes.c_int, [_P, _i32, _P]),
     "ovl_local_align": (ctypes.c_int, [_P, _P, _i32, _P, _i32, _i32, _i32, _i64, _pi32, _pi32, _pi32, _pi32,
                                        _pi32, _P, _i64, _pi64]),
     "ovl_remove_cycles": (ctypes.c_int, [_P, _P, _P, _i32, _P, _pi64]),

@@ -1,20 +1,25 @@
-"""OverlapEngine — Python face of libovl.so (one context per GPU, one GPU per process).
+"""OverlapEngine — Python face of libovl.so (one context on one or more GPUs).
 
 The engine keeps a read set resident in HBM (bit-plane packed by a gfx950
 kernel) and scores candidate pairs in one batched call, replacing the
-per-pair Python->Numba call of overlapGraphs.py:53.  It never computes on the
-CPU: a missing library or GPU raises ``OvlError``.
+per-pair Python->Numba call of overlapGraphs.py:53.  A multi-GPU engine
+(``OverlapEngine(devices=[...])`` or ``devices="all"``) shards every host-array
+call over its GPUs from this one thread.  Results come back in
+pinned host arrays (``hostmem.PinnedPool``) unless ``out=`` is given.  It never
+computes on the CPU: a missing library or GPU raises ``OvlError``.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
-from typing import Dict, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 
 from . import _lib
 from ._lib import OvlError, check
+from .hostmem import pinned_empty
 
 INDEL_DEFAULT = -(2 ** 31)  # aligners.py:7 default indel (the report's "-inf", REPORT p.3)
 
@@ -51,10 +56,29 @@ def _ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
-class OverlapEngine:
-    """A libovl context bound to one HIP device."""
+def _outputs(n: int, out) -> Tuple[np.ndarray, np.ndarray]:
+    """Result arrays: the caller's ``out=(score, end)`` (int32, contiguous, >= n) or pinned ones."""
+    if out is None:
+        return pinned_empty(n), pinned_empty(n)
+    sc, en = out
+    for x in (sc, en):
+        if not (isinstance(x, np.ndarray) and x.dtype == np.int32 and x.flags.c_contiguous and x.ndim == 1
+                and x.shape[0] >= n and x.flags.writeable):
+            raise OvlError(-1, "out must be two writeable contiguous 1-D int32 arrays of >= n_pairs elements")
+    return sc[:n], en[:n]
 
-    def __init__(self, device: int = -1):
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    rc = _lib.load().ovl_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class OverlapEngine:
+    """A libovl context on one HIP device (``device``; -1 = the current one) or on several
+    (``devices``: a list of ordinals, or "all")."""
+
+    def __init__(self, device: int = -1, devices: Union[None, str, Sequence[int]] = None):
         self._L = _lib.load()
         n = ctypes.c_int32(0)
         rc = self._L.ovl_device_count(ctypes.byref(n))
@@ -62,9 +86,36 @@ class OverlapEngine:
             raise OvlError(-2, "no HIP device visible to libovl: the overlap engine has no CPU fallback "
                                f"({_lib.last_error()})")
         ctx = ctypes.c_void_p()
-        check(self._L.ovl_create(int(device), ctypes.byref(ctx)))
+        if devices == "all":
+            check(self._L.ovl_create(0, ctypes.byref(ctx)))
+        elif devices is not None:
+            ids = np.ascontiguousarray(list(devices), dtype=np.int32)
+            check(self._L.ovl_create_on_devices(_ptr(ids), int(ids.shape[0]), ctypes.byref(ctx)))
+        elif int(device) < 0:
+            check(self._L.ovl_create(1, ctypes.byref(ctx)))
+        else:
+            ids = np.array([int(device)], dtype=np.int32)
+            check(self._L.ovl_create_on_devices(_ptr(ids), 1, ctypes.byref(ctx)))
         self._ctx = ctx
         self._reads_key = None
+
+    @property
+    def devices(self) -> List[int]:
+        """Device ordinals of this context (results are sharded over them in this order)."""
+        n = ctypes.c_int32()
+        ids = np.zeros(64, dtype=np.int32)
+        check(self._L.ovl_ctx_devices(self._ctx, _ptr(ids), 64, ctypes.byref(n)), self._ctx)
+        return ids[: n.value].tolist()
+
+    def set_timing(self, on: bool = True) -> None:
+        """Record kernel time inside host-array scoring calls (HIP events; see ``last_timing``)."""
+        check(self._L.ovl_set_timing(self._ctx, 1 if on else 0), self._ctx)
+
+    def last_timing(self) -> Dict[str, float]:
+        """{kernel_ms: summed kernel time of the busiest device, call_ms: wall time} of the last call."""
+        k, w = ctypes.c_double(), ctypes.c_double()
+        check(self._L.ovl_last_timing(self._ctx, ctypes.byref(k), ctypes.byref(w)), self._ctx)
+        return {"kernel_ms": k.value, "call_ms": w.value}
 
     # ---------------------------------------------------------------- lifecycle
     def close(self) -> None:
@@ -112,8 +163,8 @@ class OverlapEngine:
         the list also stays resident for ``score_candidates``.
         """
         n = self.enumerate_candidates(k)
-        a = np.empty(n, dtype=np.int32)
-        b = np.empty(n, dtype=np.int32)
+        a = pinned_empty(n)
+        b = pinned_empty(n)
         if n:
             check(self._L.ovl_candidates_copy(self._ctx, _ptr(a), _ptr(b)), self._ctx)
         return a, b
@@ -134,14 +185,30 @@ class OverlapEngine:
         return pa.value or 0, pb.value or 0, int(n.value)
 
     def score_candidates(self, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
-                         band: int = -1) -> Tuple[np.ndarray, np.ndarray]:
-        """Score the resident candidate list (no pair upload) -> (score, end) host arrays."""
+                         band: int = -1, out=None) -> Tuple[np.ndarray, np.ndarray]:
+        """Score the resident candidate list (no pair upload) -> (score, end) host arrays.
+
+        Sharded over the engine's devices; each device's results land in its slice of the
+        arrays by DMA (pinned arrays unless ``out=(score, end)`` is given)."""
         n = self.candidates_device()[2]
-        sc = np.empty(n, dtype=np.int32)
-        en = np.empty(n, dtype=np.int32)
+        sc, en = _outputs(n, out)
         check(self._L.ovl_score_candidates(self._ctx, match, mismatch, indel, band, _ptr(sc), _ptr(en)),
               self._ctx)
         return sc, en
+
+    def score_candidates_range(self, lo: int, hi: int, match: int = 10, mismatch: int = -1,
+                               indel: int = INDEL_DEFAULT, band: int = -1, out=None) -> Tuple[np.ndarray, np.ndarray]:
+        """(score, end) of candidate pairs [lo, hi) (a shard of a multi-process job)."""
+        sc, en = _outputs(int(hi) - int(lo), out)
+        check(self._L.ovl_score_candidates_range(self._ctx, int(lo), int(hi), match, mismatch, indel, band,
+                                                 _ptr(sc), _ptr(en)), self._ctx)
+        return sc, en
+
+    def candidate_shards(self, n_shards: int) -> List[int]:
+        """Shard bounds of the resident candidate list balanced by sum len(a)*len(b) + 1 (on the device)."""
+        bounds = np.zeros(int(n_shards) + 1, dtype=np.int64)
+        check(self._L.ovl_candidates_shards(self._ctx, int(n_shards), _ptr(bounds)), self._ctx)
+        return bounds.tolist()
 
     # ---------------------------------------------------------------- local alignment
     def local_align(self, query: str, reference: str, match: int = 10, mismatch: int = -1, indel: int = -1,
@@ -167,14 +234,14 @@ class OverlapEngine:
 
     # ---------------------------------------------------------------- scoring
     def score(self, a_idx, b_idx, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
-              band: int = -1) -> Tuple[np.ndarray, np.ndarray]:
-        """Score pairs (host arrays) against the resident reads -> (score, end) int32 arrays."""
+              band: int = -1, out=None) -> Tuple[np.ndarray, np.ndarray]:
+        """Score pairs (host arrays) against the resident reads -> (score, end) int32 arrays
+        (pinned unless ``out=(score, end)`` is given); sharded over the engine's devices."""
         a = np.ascontiguousarray(a_idx, dtype=np.int32)
         b = np.ascontiguousarray(b_idx, dtype=np.int32)
         if a.shape != b.shape or a.ndim != 1:
             raise OvlError(-1, "a_idx and b_idx must be 1-D arrays of equal length")
-        sc = np.empty(a.shape[0], dtype=np.int32)
-        en = np.empty(a.shape[0], dtype=np.int32)
+        sc, en = _outputs(a.shape[0], out)
         check(self._L.ovl_score_host(self._ctx, _ptr(a), _ptr(b), a.shape[0], match, mismatch, indel, band,
                                      _ptr(sc), _ptr(en)), self._ctx)
         return sc, en
@@ -250,12 +317,48 @@ _default: Optional[OverlapEngine] = None
 _default_lock = threading.Lock()
 
 
+def placement(count: int, env=None, pid: Optional[int] = None) -> Union[int, str, List[int]]:
+    """Which device(s) the process-wide engine uses, given ``count`` visible devices.
+
+    1. ``OVL_DEVICES``: "all" or a comma list -> one engine over several GPUs (single process);
+    2. ``OVL_DEVICE``: that ordinal;
+    3. ``LOCAL_RANK`` (torch.distributed.run and similar launchers): local_rank % count;
+    4. otherwise the process id modulo count, so the reference's joblib workers
+       (experiments.py:537, n_jobs=-1: one process each) spread over the visible GPUs.
+    """
+    env = os.environ if env is None else env
+    if count <= 0:
+        raise OvlError(-2, "no HIP device visible to libovl")
+    many = env.get("OVL_DEVICES")
+    if many:
+        if many.strip().lower() == "all":
+            return "all"
+        ids = [int(x) for x in many.split(",") if x.strip()]
+        if not ids or any(not 0 <= i < count for i in ids):
+            raise OvlError(-1, f"OVL_DEVICES={many!r}: ordinals must lie in [0, {count})")
+        return ids
+    one = env.get("OVL_DEVICE")
+    if one not in (None, ""):
+        d = int(one)
+        if not 0 <= d < count:
+            raise OvlError(-1, f"OVL_DEVICE={d} outside [0, {count})")
+        return d
+    lr = env.get("LOCAL_RANK")
+    if lr not in (None, ""):
+        return int(lr) % count
+    return (os.getpid() if pid is None else pid) % count
+
+
 def default_engine() -> OverlapEngine:
-    """Process-wide engine on the current HIP device (created on first use)."""
+    """Process-wide engine (created on first use) on the device(s) ``placement`` picks."""
     global _default
     with _default_lock:
         if _default is None:
-            _default = OverlapEngine(-1)
+            where = placement(device_count())
+            if isinstance(where, int):
+                _default = OverlapEngine(where)
+            else:
+                _default = OverlapEngine(devices=where)
         return _default
 
 

@@ -241,19 +241,36 @@ class OverlapEdges:
                                      self.min_score)
 
 
+_engines: Dict[Tuple[int, ...], OverlapEngine] = {}
+
+
+def engine_on(devices) -> OverlapEngine:
+    """A cached engine over ``devices`` ("all" or a list of ordinals): one process, several GPUs."""
+    key = ("all",) if devices == "all" else tuple(int(d) for d in devices)
+    if key not in _engines:
+        _engines[key] = OverlapEngine(devices="all" if key == ("all",) else list(key))
+    return _engines[key]
+
+
 def overlap_edges_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
-                    candidates: str = "auto") -> OverlapEdges:
+                    candidates: str = "auto", devices=None) -> OverlapEdges:
     """Scored k-mer candidates of ``construct_overlap_graph_nx_k`` as columns (no networkx)."""
     assert k >= 0, "k-mer length must be non-negative"
+    if engine is None and devices is not None:
+        engine = engine_on(devices)
     distinct, counts = dedup_reads(reads)
     a, b, sc, en = candidates_and_scores(distinct, k, engine, scorer, candidates)
     return OverlapEdges(distinct, counts, a, b, sc, en)
 
 
 def construct_overlap_graph_nx_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
-                                 candidates: str = "auto"):
-    """Overlap graph over k-mer-filtered candidates (overlapGraphs.py:5-61)."""
-    edges = overlap_edges_k(reads, k, engine, scorer, candidates)
+                                 candidates: str = "auto", devices=None):
+    """Overlap graph over k-mer-filtered candidates (overlapGraphs.py:5-61).
+
+    ``devices`` ("all" or ordinals) scores on several GPUs from this one process: every
+    device enumerates the same list, scores its Σ n·m-balanced shard and copies its
+    results into its slice of the host result arrays."""
+    edges = overlap_edges_k(reads, k, engine, scorer, candidates, devices)
     return edges.to_digraph(), edges.read_copies()
 
 

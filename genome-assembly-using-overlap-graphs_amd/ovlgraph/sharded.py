@@ -1,17 +1,29 @@
-"""Multi-GPU scoring: one process per GPU, candidate pairs sharded contiguously.
+"""Multi-process multi-GPU scoring: one process per GPU, candidate pairs sharded contiguously.
 
-SURVEY.md §8e: pairs are independent, so each rank scores a contiguous range
-of the ordered candidate list with no exchange during compute.  The only
-collective is the final gather of ``(score, end)`` (8 bytes per pair) so the
-caller sees the reference's order; on GPUs it is an RCCL ``all_gather`` over
-xGMI (backend "nccl" is RCCL on ROCm), on CPU test runs it is gloo.
+SURVEY.md §8e: pairs are independent, so each rank scores a contiguous range of
+the ordered candidate list (balanced by Σ len(a)·len(b)) with no exchange during
+compute.  The results are gathered to ONE destination, in reference order:
 
-Every rank enumerates the same candidate list deterministically, so the read
-set and pair list need no broadcast.
+* ``dest="host"`` (the default of ``ShardedStep``): every rank DMA-copies its
+  ``(score, end)`` slice from its GPU straight into a shared host buffer that
+  rank 0 owns (POSIX shared memory, pinned per rank with ``ovl_host_register``).
+  Each GPU uses its own PCIe link, so the copies run in parallel; no collective
+  moves data, only a barrier orders the step.  This is SURVEY.md §8e's "per-device
+  D2H into pinned host slices".
+* ``dest="rank0"``: the slices stay in HBM and one ``dist.gather`` (RCCL
+  send/recv over xGMI on backend "nccl", gloo on CPU) collects them on rank 0's GPU.
+
+The single-process form of the same thing is ``OverlapEngine(devices=...)``: one
+context drives every GPU and the per-device copies land in the caller's arrays.
+
+Every rank enumerates (or receives) the same candidate list deterministically, so
+the read set and pair list need no broadcast.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional, Sequence, Tuple
+import ctypes
+import os
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -19,25 +31,65 @@ from .engine import INDEL_DEFAULT, OverlapEngine
 
 
 def shard_bounds(n_pairs: int, world: int, rank: int, cost: Optional[np.ndarray] = None) -> Tuple[int, int]:
-    """Contiguous [lo, hi) of rank `rank`; balanced by per-pair `cost` (e.g. n*m) when given."""
+    """Contiguous [lo, hi) of rank `rank`; balanced by per-pair `cost` (e.g. n*m + 1) when given.
+
+    Cut r is the first pair p whose inclusive cost prefix c[p] satisfies c[p]·world >= total·r,
+    the rule ``ovl_candidates_shards`` applies on the device.
+    """
     if world <= 0 or not (0 <= rank < world):
         raise ValueError("bad world/rank")
     if cost is None or n_pairs == 0:
         return (n_pairs * rank) // world, (n_pairs * (rank + 1)) // world
-    c = np.cumsum(np.asarray(cost, dtype=np.float64))
-    total = c[-1]
-    cuts = [0] + [int(np.searchsorted(c, total * r / world, side="left")) for r in range(1, world)] + [n_pairs]
+    c = np.cumsum(np.asarray(cost, dtype=np.int64))
+    total = int(c[-1])
+    cuts = [0] + [int(np.searchsorted(c * world, total * r, side="left")) for r in range(1, world)] + [n_pairs]
     cuts = np.maximum.accumulate(np.minimum(cuts, n_pairs))
     return int(cuts[rank]), int(cuts[rank + 1])
 
 
+def pair_costs(reads: Sequence[str], a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
+    return lens[a] * lens[b] + 1
+
+
+def _device(dist, group):
+    import torch
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _gather_rows(packed, bounds, n_pairs: int, dst: Optional[int], group):
+    """Gather every rank's padded (2, width) rows to `dst` (None: to every rank) -> (score, end) or None."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if dst is None:
+        rows = [torch.empty_like(packed) for _ in range(world)]
+        dist.all_gather(rows, packed, group=group)
+    else:
+        rows = [torch.empty_like(packed) for _ in range(world)] if rank == dst else None
+        dist.gather(packed, rows, dst=dst, group=group)
+        if rank != dst:
+            return None
+    score = np.empty(n_pairs, dtype=np.int32)
+    end = np.empty(n_pairs, dtype=np.int32)
+    for r, (lo, hi) in enumerate(bounds):
+        g = rows[r].cpu().numpy()
+        score[lo:hi] = g[0, : hi - lo]
+        end[lo:hi] = g[1, : hi - lo]
+    return score, end
+
+
 def score_pairs_sharded(reads: Sequence[str], a_idx, b_idx, match: int = 10, mismatch: int = -1,
                         indel: int = INDEL_DEFAULT, group=None, engine: Optional[OverlapEngine] = None,
-                        local_scorer: Optional[Callable] = None, balance: bool = True) -> Tuple[np.ndarray, np.ndarray]:
-    """Score the whole pair list across the ranks of `group`; every rank gets all results.
+                        local_scorer: Optional[Callable] = None, balance: bool = True, dst: Optional[int] = 0):
+    """Score the whole pair list across the ranks of `group`; results gathered to rank `dst`.
 
-    ``local_scorer(reads, a, b) -> (score, end)`` overrides the GPU engine for
-    the local shard (used by CPU multi-process tests with the oracle).
+    Returns ``(score, end)`` in reference order on rank ``dst`` and ``None`` on the others
+    (``dst=None``: every rank gets them, an all_gather).  ``local_scorer(reads, a, b) ->
+    (score, end)`` overrides the GPU engine for the local shard (CPU multi-process tests).
     """
     import torch
     import torch.distributed as dist
@@ -46,123 +98,222 @@ def score_pairs_sharded(reads: Sequence[str], a_idx, b_idx, match: int = 10, mis
     b = np.ascontiguousarray(b_idx, dtype=np.int32)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    cost = None
-    if balance and a.shape[0]:
-        lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
-        cost = lens[a] * lens[b] + 1
+    cost = pair_costs(reads, a, b) if balance and a.shape[0] else None
     bounds = [shard_bounds(a.shape[0], world, r, cost) for r in range(world)]
     lo, hi = bounds[rank]
-    width = max(h - l for l, h in bounds) if bounds else 0
-    backend = dist.get_backend(group)
-    on_gpu = backend == "nccl"
-    device = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
-
-    packed = torch.full((2, max(width, 1)), -1, dtype=torch.int32, device=device)
+    width = max(1, max(h - l for l, h in bounds))
+    device = _device(dist, group)
+    packed = torch.full((2, width), -1, dtype=torch.int32, device=device)
     if hi > lo:
         if local_scorer is not None:
             sc, en = local_scorer(reads, a[lo:hi], b[lo:hi])
-            packed[0, : hi - lo] = torch.as_tensor(np.asarray(sc, dtype=np.int32), device=device)
-            packed[1, : hi - lo] = torch.as_tensor(np.asarray(en, dtype=np.int32), device=device)
-        elif on_gpu:
-            eng = engine or OverlapEngine(-1)
-            eng.set_reads(reads)
-            ta = torch.as_tensor(a[lo:hi], device=device)
-            tb = torch.as_tensor(b[lo:hi], device=device)
-            eng.score_tensors(ta, tb, packed[0], packed[1], match, mismatch, indel)
         else:
-            eng = engine or OverlapEngine(-1)
+            eng = engine or OverlapEngine(torch.cuda.current_device() if device.type == "cuda" else -1)
             eng.set_reads(reads)
             sc, en = eng.score(a[lo:hi], b[lo:hi], match, mismatch, indel)
-            packed[0, : hi - lo] = torch.as_tensor(sc)
-            packed[1, : hi - lo] = torch.as_tensor(en)
-    gathered = [torch.empty_like(packed) for _ in range(world)]
-    dist.all_gather(gathered, packed, group=group)
-    score = np.empty(a.shape[0], dtype=np.int32)
-    end = np.empty(a.shape[0], dtype=np.int32)
-    for r, (l, h) in enumerate(bounds):
-        g = gathered[r].cpu().numpy()
-        score[l:h] = g[0, : h - l]
-        end[l:h] = g[1, : h - l]
-    return score, end
+        packed[0, : hi - lo] = torch.as_tensor(np.asarray(sc, dtype=np.int32)).to(device)
+        packed[1, : hi - lo] = torch.as_tensor(np.asarray(en, dtype=np.int32)).to(device)
+    return _gather_rows(packed, bounds, a.shape[0], dst, group)
+
+
+class SharedResults:
+    """A (score, end) host buffer of n pairs shared by the ranks of one node (POSIX shm).
+
+    Rank 0 creates it, the others attach by name; each rank pins only the pages of its own
+    slices (``ovl_host_register``), so its GPU's D2H copies land in place.
+    """
+
+    def __init__(self, n_pairs: int, group=None, tag: str = ""):
+        import torch.distributed as dist
+        from multiprocessing import resource_tracker, shared_memory
+
+        self.n = int(n_pairs)
+        self.rank = dist.get_rank(group)
+        size = max(8, 8 * self.n)
+        name = [f"ovl_{os.getpid()}_{tag}"[:30] if self.rank == 0 else None]
+        if self.rank == 0:
+            self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=size)
+        dist.broadcast_object_list(name, src=0, group=group)
+        if self.rank != 0:
+            self.shm = shared_memory.SharedMemory(name=name[0], create=False)
+            # an attaching process must not unlink the segment at exit (CPython < 3.13 tracker)
+            try:
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
+        self.buf = np.frombuffer(self.shm.buf, dtype=np.int32, count=2 * self.n)
+        self.score = self.buf[: self.n]
+        self.end = self.buf[self.n:]
+        self._pinned: List[int] = []
+
+    def pin(self, lo: int, hi: int) -> None:
+        """Pin the pages that hold pairs [lo, hi) of both columns in this process."""
+        if hi <= lo:
+            return
+        from . import _lib
+        L = _lib.load()
+        base = self.buf.ctypes.data
+        page = 4096
+        for first, last in ((lo, hi), (self.n + lo, self.n + hi)):
+            s = (base + 4 * first) // page * page
+            e = -(-(base + 4 * last) // page) * page
+            s = max(s, base // page * page)
+            rc = L.ovl_host_register(ctypes.c_void_p(s), e - s)
+            if rc != 0:
+                raise _lib.OvlError(rc, _lib.last_error())
+            self._pinned.append(s)
+
+    def close(self) -> None:
+        from . import _lib
+        if self._pinned:
+            L = _lib.load()
+            for s in self._pinned:
+                L.ovl_host_unregister(ctypes.c_void_p(s))
+            self._pinned = []
+        self.score = self.end = self.buf = None
+        try:
+            self.shm.close()
+        except BufferError:
+            return
+        if self.rank == 0:
+            try:
+                self.shm.unlink()
+            except FileNotFoundError:
+                pass
 
 
 class ShardedStep:
-    """Repeated sharded scoring of one candidate list with the RCCL gather, device-resident.
+    """Repeated sharded scoring of one candidate list, results gathered to one destination.
 
-    The same contract as ``score_pairs_sharded`` (every rank holds the same ordered list, each scores
-    its contiguous shard, one ``all_gather`` restores reference order), split into a one-time setup
-    and a ``step()`` that issues the shard's scoring launch and the gather with no host copies: the
-    shard's indices and the packed ``(score, end)`` rows stay in HBM.  ``bench.py`` times it at N > 1.
-    On the gloo backend (CPU tests, one-GPU rehearsal) the gather runs on host copies, and
-    ``local_scorer(reads, a, b) -> (score, end)`` may replace the engine.
+    Setup once: the read set on this rank's GPU, the candidate list (``a_idx``/``b_idx`` host
+    arrays, or ``k`` to enumerate it on the device, identical on every rank), this rank's
+    Σ n·m-balanced shard, and the destination.  ``step()`` scores the shard and gathers:
+
+    * ``dest="host"``: the shard's results DMA into rank 0's shared host arrays; ``step()``
+      returns after this rank's copies are done and a barrier (every slice has landed);
+    * ``dest="rank0"``: the shard's results stay in HBM and ``dist.gather`` collects them on
+      rank 0 (RCCL send/recv on "nccl").
+
+    ``results()`` gives rank 0 the reference-ordered ``(score, end)``.  On CPU tests
+    ``local_scorer(reads, a, b) -> (score, end)`` replaces the engine (host lists only).
     """
 
-    def __init__(self, reads: Sequence[str], a_idx, b_idx, match: int = 10, mismatch: int = -1,
-                 indel: int = INDEL_DEFAULT, group=None, engine: Optional[OverlapEngine] = None,
-                 local_scorer: Optional[Callable] = None, balance: bool = True):
+    def __init__(self, reads: Sequence[str], a_idx=None, b_idx=None, k: Optional[int] = None,
+                 match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT, group=None,
+                 engine: Optional[OverlapEngine] = None, local_scorer: Optional[Callable] = None,
+                 dest: str = "host", balance: bool = True):
         import torch
         import torch.distributed as dist
 
-        self.reads = reads
-        self.a = np.ascontiguousarray(a_idx, dtype=np.int32)
-        self.b = np.ascontiguousarray(b_idx, dtype=np.int32)
+        if dest not in ("host", "rank0"):
+            raise ValueError("dest must be 'host' or 'rank0'")
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        cost = None
-        if balance and self.a.shape[0]:
-            lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
-            cost = lens[self.a] * lens[self.b] + 1
-        self.bounds = [shard_bounds(self.a.shape[0], self.world, r, cost) for r in range(self.world)]
-        self.width = max(1, max(h - l for l, h in self.bounds))
-        self.on_gpu = dist.get_backend(group) == "nccl"
-        self.local_scorer = local_scorer
+        self.dest = dest
         self.scoring = (match, mismatch, indel)
-        lo, hi = self.bounds[self.rank]
-        self.n_local = hi - lo
-        self._launch = None
+        self.local_scorer = local_scorer
+        self.reads = reads
+        self.device = _device(dist, group)
+        self.eng = None
+        self.a = self.b = None
         if local_scorer is None:
-            dev = torch.device("cuda", torch.cuda.current_device())
-            self.eng = engine or OverlapEngine(dev.index)
+            self.eng = engine or OverlapEngine(torch.cuda.current_device())
             self.eng.set_reads(reads)
-            self.packed = torch.full((2, self.width), -1, dtype=torch.int32, device=dev)
-            if self.n_local:
-                self.ta = torch.as_tensor(self.a[lo:hi], device=dev)
-                self.tb = torch.as_tensor(self.b[lo:hi], device=dev)
-                self._launch = self.eng.launcher(self.ta, self.tb, self.packed[0], self.packed[1],
-                                                 match, mismatch, indel)
+        if a_idx is None:
+            if self.eng is None or k is None:
+                raise ValueError("give a_idx/b_idx, or k with the GPU engine")
+            n = self.eng.enumerate_candidates(k)
+            self.n_pairs = n
+            cuts = self.eng.candidate_shards(self.world) if balance else \
+                [(n * r) // self.world for r in range(self.world + 1)]
+            self.bounds = [(cuts[r], cuts[r + 1]) for r in range(self.world)]
+            self.on_device_list = True
         else:
-            self.packed = torch.full((2, self.width), -1, dtype=torch.int32)
-        gdev = self.packed.device if self.on_gpu else torch.device("cpu")
-        self.out = torch.empty((self.world, 2, self.width), dtype=torch.int32, device=gdev)
+            self.a = np.ascontiguousarray(a_idx, dtype=np.int32)
+            self.b = np.ascontiguousarray(b_idx, dtype=np.int32)
+            self.n_pairs = int(self.a.shape[0])
+            cost = pair_costs(reads, self.a, self.b) if balance and self.n_pairs else None
+            self.bounds = [shard_bounds(self.n_pairs, self.world, r, cost) for r in range(self.world)]
+            self.on_device_list = False
+        lo, hi = self.bounds[self.rank]
+        self.lo, self.hi = lo, hi
+        self.width = max(1, max(h - l for l, h in self.bounds))
+        self.shared = None
+        self._launch = None
+        if dest == "host":
+            self.shared = SharedResults(self.n_pairs, group, tag=str(os.environ.get("MASTER_PORT", "")))
+            if self.eng is not None:
+                self.shared.pin(lo, hi)
+        else:
+            self.packed = torch.full((2, self.width), -1, dtype=torch.int32, device=self.device)
+            self.rows = ([torch.empty_like(self.packed) for _ in range(self.world)] if self.rank == 0 else None)
+            if self.eng is not None and hi > lo:
+                if self.on_device_list:
+                    pa, pb, _ = self.eng.candidates_device()
+                    self._launch = lambda: self.eng.score_device(
+                        pa + 4 * lo, pb + 4 * lo, hi - lo, self.packed[0].data_ptr(), self.packed[1].data_ptr(),
+                        match, mismatch, indel, stream=torch.cuda.current_stream(self.device).cuda_stream)
+                else:
+                    self.ta = torch.as_tensor(self.a[lo:hi], device=self.device)
+                    self.tb = torch.as_tensor(self.b[lo:hi], device=self.device)
+                    self._launch = self.eng.launcher(self.ta, self.tb, self.packed[0], self.packed[1],
+                                                     match, mismatch, indel)
+
+    def _local(self):
+        lo, hi = self.lo, self.hi
+        return self.local_scorer(self.reads, self.a[lo:hi], self.b[lo:hi])
 
     def step(self) -> None:
-        """Score this rank's shard, then gather every shard (asynchronous on the GPU path)."""
+        """Score this rank's shard and gather it to the destination."""
         import torch
         import torch.distributed as dist
 
+        lo, hi = self.lo, self.hi
+        if self.dest == "host":
+            if hi > lo:
+                out = (self.shared.score[lo:hi], self.shared.end[lo:hi])
+                if self.eng is None:
+                    sc, en = self._local()
+                    out[0][:] = sc
+                    out[1][:] = en
+                elif self.on_device_list:
+                    self.eng.score_candidates_range(lo, hi, *self.scoring, out=out)
+                else:
+                    self.eng.score(self.a[lo:hi], self.b[lo:hi], *self.scoring, out=out)
+            dist.barrier(group=self.group)
+            return
         if self._launch is not None:
             self._launch()
-        elif self.local_scorer is not None and self.n_local:
-            lo, hi = self.bounds[self.rank]
-            sc, en = self.local_scorer(self.reads, self.a[lo:hi], self.b[lo:hi])
-            self.packed[0, :hi - lo] = torch.as_tensor(np.asarray(sc, dtype=np.int32))
-            self.packed[1, :hi - lo] = torch.as_tensor(np.asarray(en, dtype=np.int32))
-        if self.on_gpu:
-            dist.all_gather_into_tensor(self.out.view(-1), self.packed.view(-1), group=self.group)
-        else:
-            dist.all_gather(list(self.out.unbind(0)), self.packed.cpu(), group=self.group)
+        elif self.eng is None and hi > lo:
+            sc, en = self._local()
+            self.packed[0, : hi - lo] = torch.as_tensor(np.asarray(sc, dtype=np.int32))
+            self.packed[1, : hi - lo] = torch.as_tensor(np.asarray(en, dtype=np.int32))
+        dist.gather(self.packed, self.rows, dst=0, group=self.group)
 
     def gather_bytes(self) -> int:
-        """Bytes every rank receives per step (the padded (score, end) rows of all shards)."""
-        return int(self.out.numel()) * 4
+        """Result bytes that cross to the destination per step (8 B per pair; padded rows for rank0)."""
+        if self.dest == "host":
+            return 8 * self.n_pairs
+        return self.world * 2 * self.width * 4
 
-    def results(self) -> Tuple[np.ndarray, np.ndarray]:
-        """(score, end) of the whole list in reference order, from the last step's gather."""
-        g = self.out.cpu().numpy()
-        score = np.empty(self.a.shape[0], dtype=np.int32)
-        end = np.empty(self.a.shape[0], dtype=np.int32)
+    def results(self) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+        """Rank 0: (score, end) of the whole list in reference order, from the last step; else None."""
+        if self.rank != 0:
+            return None
+        if self.dest == "host":
+            return self.shared.score.copy(), self.shared.end.copy()
+        score = np.empty(self.n_pairs, dtype=np.int32)
+        end = np.empty(self.n_pairs, dtype=np.int32)
         for r, (l, h) in enumerate(self.bounds):
-            score[l:h] = g[r, 0, : h - l]
-            end[l:h] = g[r, 1, : h - l]
+            g = self.rows[r].cpu().numpy()
+            score[l:h] = g[0, : h - l]
+            end[l:h] = g[1, : h - l]
         return score, end
+
+    def close(self) -> None:
+        import torch.distributed as dist
+        if self.shared is not None:
+            dist.barrier(group=self.group)  # rank 0 unlinks only after every rank is done
+            self.shared.close()
+            self.shared = None

@@ -11,8 +11,16 @@
  *  - Plain C types only; the caller owns every pointer it passes in.
  *  - Return value 0 (OVL_OK) on success, a negative OVL_E_* code on failure;
  *    ovl_last_error() then describes it.  Nothing throws or aborts across the ABI.
- *  - One call at a time per ovl_ctx.  Contexts are independent; a process
- *    drives one GPU through one context (one process per GPU).
+ *  - One call at a time per ovl_ctx.  Contexts are independent.  A context
+ *    drives one or more GPUs from the calling thread: host-array
+ *    scoring calls shard the pair list over its devices (contiguous ranges
+ *    balanced by sum len(a)*len(b)) and every device writes its range of the
+ *    results straight into the caller's arrays.  joblib-style multi-process
+ *    callers create one single-device context per process.
+ *  - Host arrays may be pageable or pinned (ovl_host_alloc / ovl_host_register /
+ *    hipHostMalloc).  Pinned arrays are read and written by DMA in place;
+ *    pageable ones go through pinned staging.  Either way copies, kernels and
+ *    result copies of consecutive chunks overlap.
  *  - Read i is the byte string seqs[offsets[i] .. offsets[i+1]).  Bytes are
  *    symbols compared for equality only (any alphabet of <= 256 symbols).
  *  - Semantics are the reference's: DP fill of aligners.py:27-48 with int64
@@ -28,7 +36,7 @@
 extern "C" {
 #endif
 
-#define OVL_ABI_VERSION 2
+#define OVL_ABI_VERSION 3
 
 enum {
     OVL_OK = 0,
@@ -56,9 +64,30 @@ int ovl_version(void);
 /* Number of visible HIP devices. */
 int ovl_device_count(int32_t* out_count);
 
-/* Create a context on `device` (-1 = the current device). */
-int ovl_create(int32_t device, ovl_ctx** out_ctx);
+/*
+ * Create a context on n_devices GPUs: 0 = every visible device;
+ * otherwise the n_devices consecutive devices starting at the calling thread's
+ * current device (so 1 = the current device).  The caller's current device is
+ * never changed by any entry point.
+ */
+int ovl_create(int32_t n_devices, ovl_ctx** out_ctx);
+/* Create a context on an explicit list of distinct device ordinals (device 0 of the context = devices[0]). */
+int ovl_create_on_devices(const int32_t* devices, int32_t n_devices, ovl_ctx** out_ctx);
+/* The context's device ordinals: *out_n = count, ids[0 .. min(cap, count)) = ordinals. */
+int ovl_ctx_devices(const ovl_ctx* ctx, int32_t* ids, int32_t cap, int32_t* out_n);
 int ovl_destroy(ovl_ctx* ctx);
+
+/* Pinned host memory for result / pair arrays (DMA in place, visible to every device). */
+int ovl_host_alloc(int64_t bytes, void** out_ptr);
+int ovl_host_free(void* ptr);
+/* Pin (register) / unpin an existing host range, e.g. a shared-memory result buffer. */
+int ovl_host_register(void* ptr, int64_t bytes);
+int ovl_host_unregister(void* ptr);
+
+/* Per-call timing of host-array scoring calls (off by default; on adds HIP timing events):
+ * kernel_ms = summed kernel time of the busiest device, call_ms = wall time of the call. */
+int ovl_set_timing(ovl_ctx* ctx, int32_t on);
+int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 
 /* Last error message of `ctx`, or of the calling thread when ctx is NULL. */
 const char* ovl_last_error(const ovl_ctx* ctx);
@@ -92,14 +121,16 @@ int ovl_reads_info(const ovl_ctx* ctx, int32_t* n_reads, int32_t* lmax, int32_t*
 int ovl_plan(const ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
              int32_t* out_kernel);
 
-/* Score against the resident reads; host pair/result arrays; synchronous. */
+/* Score against the resident reads; host pair/result arrays; synchronous.  Sharded over the
+ * context's devices; chunked H2D / kernel / D2H pipeline per device.  A pair index outside
+ * [0, n_reads) makes the call return OVL_E_INDEX (checked on the device, its results are -1). */
 int ovl_score_host(ovl_ctx* ctx, const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
                    int32_t match, int32_t mismatch, int64_t indel, int32_t band,
                    int32_t* out_score, int32_t* out_end);
 
 /*
- * Score against the resident reads with DEVICE pointers, asynchronously on
- * `stream` (a hipStream_t; NULL = the default stream, as in the HIP API).  Pairs with an index
+ * Score against the resident reads with DEVICE pointers (on the context's first device),
+ * asynchronously on `stream` (a hipStream_t; NULL = the default stream, as in the HIP API).  Pairs with an index
  * outside [0, n_reads) get score = end = -1 and set a device error flag that
  * ovl_check_device_errors() reports.
  */
@@ -137,9 +168,21 @@ int ovl_candidates_copy(ovl_ctx* ctx, int32_t* a_idx, int32_t* b_idx);
 /* Device pointers (and length) of the context's candidate list, for ovl_score_device. */
 int ovl_candidates_device(const ovl_ctx* ctx, const int32_t** d_a_idx, const int32_t** d_b_idx, int64_t* n_pairs);
 
-/* Score the context's candidate list (no pair upload); host outputs; synchronous. */
+/* Score the context's candidate list (no pair upload); host outputs; synchronous.  Every device
+ * of the context enumerated the same list, each scores its shard and copies its results into its
+ * slice of out_score / out_end (the "gather" of SURVEY.md §8e is these per-device D2H copies). */
 int ovl_score_candidates(ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t indel, int32_t band,
                          int32_t* out_score, int32_t* out_end);
+
+/* The same for pairs [lo, hi) of the candidate list: out_score[p - lo], out_end[p - lo].  A
+ * process of a multi-process job scores its shard this way (bounds from ovl_candidates_shards). */
+int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t match, int32_t mismatch,
+                               int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end);
+
+/* Contiguous shard bounds of the candidate list, balanced by sum len(a)*len(b) + 1:
+ * bounds[0] = 0 <= bounds[1] <= ... <= bounds[n_shards] = n_pairs (the rule of
+ * ovlgraph/sharded.py:shard_bounds, computed on the device). */
+int ovl_candidates_shards(ovl_ctx* ctx, int32_t n_shards, int64_t* bounds);
 
 /*
  * local_alignment (aligners.py:85-167) of query[0..n) against reference[0..m) on the whole GPU:

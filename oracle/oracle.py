@@ -127,6 +127,8 @@ def lib():
         L.oracle_batch_dp.restype = ctypes.c_int
         L.oracle_batch_ungapped.argtypes = [P, P, i32, P, P, i64, i64, i64, P, P, i32]
         L.oracle_batch_ungapped.restype = ctypes.c_int
+        L.oracle_batch_closed_form.argtypes = [P, P, i32, P, P, i64, i64, i64, P, P, i32]
+        L.oracle_batch_closed_form.restype = ctypes.c_int
         L.oracle_batch_banded.argtypes = [P, P, i32, P, P, i64, i64, i64, i64, i32, P, P, i32]
         L.oracle_batch_banded.restype = ctypes.c_int
         L.oracle_local_align.argtypes = [P, i32, P, i32, i64, i64, i64, P, P, P, P, P, P, i64, P]
@@ -188,6 +190,24 @@ def batch_ungapped(reads: Sequence[str], a_idx, b_idx, match=10, mismatch=-1,
                                      a.shape[0], match, mismatch, _ptr(sc), _ptr(en), threads)
     if rc != 0:
         raise RuntimeError(f"oracle_batch_ungapped failed rc={rc}")
+    return sc, en
+
+
+def batch_closed_form(reads: Sequence[str], a_idx, b_idx, match=10, mismatch=-1,
+                      threads: int = 0, encoded=None) -> Tuple[np.ndarray, np.ndarray]:
+    """The optimised CPU closed form (64 bases per popcount; ACGT reads <= 256 bases): bench.py's
+    second CPU-baseline line.  Equal to batch_ungapped, which tests check."""
+    seqs, offs = encoded if encoded is not None else encode(reads)
+    a = np.ascontiguousarray(a_idx, dtype=np.int32)
+    b = np.ascontiguousarray(b_idx, dtype=np.int32)
+    sc = np.zeros(a.shape[0], np.int32)
+    en = np.zeros(a.shape[0], np.int32)
+    if seqs.size == 0:
+        seqs = np.zeros(1, np.uint8)
+    rc = lib().oracle_batch_closed_form(_ptr(seqs), _ptr(offs), len(offs) - 1, _ptr(a), _ptr(b),
+                                        a.shape[0], match, mismatch, _ptr(sc), _ptr(en), threads)
+    if rc != 0:
+        raise RuntimeError(f"oracle_batch_closed_form failed rc={rc}")
     return sc, en
 
 

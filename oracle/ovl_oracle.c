@@ -232,6 +232,100 @@ static int batch_common(int mode, const uint8_t* seqs, const int64_t* offsets, i
     return err ? -1 : 0;
 }
 
+/* ---------------------------------------------------------------------------
+ * Optimised CPU closed form (bench.py's second CPU-baseline line, SURVEY.md §8d:
+ * "the build's optimized closed-form CPU path").  Same result as
+ * oracle_overlap_ungapped -- exact when gaps cannot win --
+ * computed 64 bases at a time: reads are packed once into two bit planes
+ * (2 bits per base, ACGT only, base i at bit i), and the mismatch count of the
+ * diagonal ending at (n, j) is popcount((s0 ^ t0) | (s1 ^ t1)) over the aligned
+ * windows, so dp[n][j] = match * L + (mismatch - match) * X(j).
+ * ------------------------------------------------------------------------- */
+#define CF_MAXW 5  /* words per plane: reads up to 256 bases (+ one spill word) */
+
+static inline uint64_t cf_window(const uint64_t* w, int32_t start, int32_t k) {
+    const int32_t q = (start >> 6) + k, r = start & 63;
+    return r ? (w[q] >> r) | (w[q + 1] << (64 - r)) : w[q];
+}
+
+/* pack read bytes (ACGT -> 0..3 by byte order A<C<G<T) into planes[2][CF_MAXW] */
+static int cf_pack(const uint8_t* x, int32_t n, uint64_t planes[2][CF_MAXW]) {
+    memset(planes, 0, sizeof(uint64_t) * 2 * CF_MAXW);
+    for (int32_t i = 0; i < n; ++i) {
+        uint64_t c;
+        switch (x[i]) {
+            case 'A': c = 0; break;
+            case 'C': c = 1; break;
+            case 'G': c = 2; break;
+            case 'T': c = 3; break;
+            default: return -1;
+        }
+        planes[0][i >> 6] |= (c & 1) << (i & 63);
+        planes[1][i >> 6] |= (c >> 1) << (i & 63);
+    }
+    return 0;
+}
+
+static void cf_pair(const uint64_t S[2][CF_MAXW], int32_t n, const uint64_t T[2][CF_MAXW], int32_t m,
+                    int64_t match, int64_t mismatch, int32_t* out_score, int32_t* out_end) {
+    int64_t best = 0;  /* j = 0 scores 0 and is scanned first */
+    int32_t end = 0;
+    const int64_t dms = mismatch - match;
+    for (int32_t j = 1; j <= m; ++j) {
+        const int32_t L = n < j ? n : j;
+        const int32_t a = n - L, b = j - L;  /* s[a .. a+L) against t[b .. b+L) */
+        int64_t x = 0;
+        const int32_t words = (L + 63) >> 6;
+        for (int32_t k = 0; k < words; ++k) {
+            uint64_t d = (cf_window(S[0], a, k) ^ cf_window(T[0], b, k)) |
+                         (cf_window(S[1], a, k) ^ cf_window(T[1], b, k));
+            const int32_t rem = L - 64 * k;
+            if (rem < 64) d &= (((uint64_t)1) << rem) - 1;
+            x += __builtin_popcountll(d);
+        }
+        const int64_t sum = match * L + dms * x;
+        if (sum > best) { best = sum; end = j; }
+    }
+    *out_score = (int32_t)best;
+    *out_end = end;
+}
+
+/* Closed form over a pair list of ACGT reads up to 256 bases; -3 when a read is longer or has
+ * another symbol (callers use oracle_batch_ungapped then).  threads <= 0: all OpenMP threads. */
+int oracle_batch_closed_form(const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
+                             const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,
+                             int64_t match, int64_t mismatch,
+                             int32_t* out_score, int32_t* out_end, int32_t threads)
+{
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        if (a_idx[p] < 0 || a_idx[p] >= n_reads || b_idx[p] < 0 || b_idx[p] >= n_reads) return -2;
+    }
+    uint64_t (*pk)[2][CF_MAXW] = (uint64_t (*)[2][CF_MAXW])malloc(sizeof(*pk) * (size_t)(n_reads > 0 ? n_reads : 1));
+    if (!pk) return -1;
+    int err = 0;
+#ifdef _OPENMP
+    if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(threads) reduction(| : err)
+#endif
+    for (int32_t r = 0; r < n_reads; ++r) {
+        const int64_t len = offsets[r + 1] - offsets[r];
+        if (len > 64 * (CF_MAXW - 1) || cf_pack(seqs + offsets[r], (int32_t)len, pk[r])) err |= 1;
+    }
+    if (err) { free(pk); return -3; }
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(threads)
+#endif
+    for (int64_t p = 0; p < n_pairs; ++p) {
+        const int32_t a = a_idx[p], b = b_idx[p];
+        cf_pair((const uint64_t (*)[CF_MAXW])pk[a], (int32_t)(offsets[a + 1] - offsets[a]),
+                (const uint64_t (*)[CF_MAXW])pk[b], (int32_t)(offsets[b + 1] - offsets[b]),
+                match, mismatch, out_score + p, out_end + p);
+    }
+    (void)threads;
+    free(pk);
+    return 0;
+}
+
 /* Batch over a pair list; threads <= 0 means all OpenMP threads. */
 int oracle_batch_dp(const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
                     const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs,

@@ -1,0 +1,319 @@
+"""GPU: the host-array pipeline, multi-device contexts, sharding and gathers, full-size cfg5.
+
+Every result is compared bit for bit with the oracle (oracle/ovl_oracle.c, the restatement of
+aligners.py:27-57) or with another path already checked against it.
+
+* ovl_score_host / ovl_score_candidates: chunked H2D / kernel / D2H pipeline, pinned and pageable
+  caller arrays, many chunks (staging-slot reuse), device-side index errors.
+* ovl_create(0) / ovl_create_on_devices: one context over the visible GPUs (one on this box),
+  Σ n·m shard bounds on the device (ovl_candidates_shards) == ovlgraph.sharded.shard_bounds,
+  ovl_score_candidates_range shards reassemble the whole list.
+* ovlgraph.sharded at world 1 on backend "nccl" (RCCL): score_pairs_sharded, ShardedStep with
+  dest="host" (shared pinned host buffer) and dest="rank0" (dist.gather).
+* dp_lane_kernel launches on two streams share the hand-off buffer safely.
+* cfg5 (BASELINE configs[4], 3.39 M pairs, l = 250) at full size: default scoring vs the oracle's
+  closed form; gapped (indel -2) lane kernel == wavefront kernel on the whole list, and both ==
+  the oracle's full DP on a 50k-pair strided sample.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine_env(env, **kw):
+    from ovlgraph import OverlapEngine
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return OverlapEngine(**kw) if kw else OverlapEngine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def cfg2():
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("cfg2", seed=0))
+    a, b = enumerate_candidates(reads, 5)
+    return reads, a, b
+
+
+@pytest.fixture(scope="module")
+def cfg2_ref(oracle_mod, cfg2):
+    reads, a, b = cfg2
+    return oracle_mod.batch_ungapped(reads, a, b)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from ovlgraph import OverlapEngine
+    eng = OverlapEngine(0)
+    yield eng
+    eng.close()
+
+
+@pytest.mark.parametrize("chunk", ["0", "64", "1000", "65536"])
+def test_pipeline_host_list_pinned_and_pageable(oracle_mod, cfg2, cfg2_ref, chunk):
+    from ovlgraph.hostmem import is_pinned_array, pinned_empty
+    reads, a, b = cfg2
+    eng = _engine_env({"OVL_PIPE_CHUNK": chunk})
+    try:
+        eng.set_reads(reads)
+        # pageable inputs, pinned outputs (the default)
+        sc, en = eng.score(a, b)
+        assert is_pinned_array(sc) and is_pinned_array(en)
+        np.testing.assert_array_equal(sc, cfg2_ref[0])
+        np.testing.assert_array_equal(en, cfg2_ref[1])
+        # pageable outputs (staging ring)
+        out = (np.full(a.shape[0], 7, np.int32), np.full(a.shape[0], 7, np.int32))
+        eng.score(a, b, out=out)
+        np.testing.assert_array_equal(out[0], cfg2_ref[0])
+        np.testing.assert_array_equal(out[1], cfg2_ref[1])
+        # pinned inputs too
+        pa, pb = pinned_empty(a.shape[0]), pinned_empty(a.shape[0])
+        pa[:] = a
+        pb[:] = b
+        sc2, en2 = eng.score(pa, pb)
+        np.testing.assert_array_equal(sc2, cfg2_ref[0])
+        np.testing.assert_array_equal(en2, cfg2_ref[1])
+        # resident device list -> pinned and pageable outputs
+        da, db = eng.candidates(5)
+        np.testing.assert_array_equal(da, a)
+        np.testing.assert_array_equal(db, b)
+        cs, ce = eng.score_candidates()
+        np.testing.assert_array_equal(cs, cfg2_ref[0])
+        np.testing.assert_array_equal(ce, cfg2_ref[1])
+        out = (np.zeros(a.shape[0] + 5, np.int32), np.zeros(a.shape[0] + 5, np.int32))
+        eng.score_candidates(out=out)
+        np.testing.assert_array_equal(out[0][: a.shape[0]], cfg2_ref[0])
+        assert out[0][a.shape[0]:].tolist() == [0] * 5  # nothing past n_pairs is written
+    finally:
+        eng.close()
+
+
+def test_pipeline_gapped_and_banded(oracle_mod, cfg2):
+    """The pipeline around the DP kernels (lane kernel above 65,536 pairs) and the band knob."""
+    reads, a, b = cfg2
+    eng = _engine_env({"OVL_PIPE_CHUNK": "40000"})
+    try:
+        eng.set_reads(reads)
+        sc, en = eng.score(a, b, 10, -1, -2)
+        rs, re_ = oracle_mod.batch_dp(reads, a, b, 10, -1, -2)
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
+        sc, en = eng.score(a, b, 10, -1, -2, 8)
+        rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, 8)
+        np.testing.assert_array_equal(sc, rs)
+        np.testing.assert_array_equal(en, re_)
+    finally:
+        eng.close()
+
+
+def test_pipeline_index_error_then_recovery(engine, cfg2, cfg2_ref):
+    from ovlgraph import OvlError
+    reads, a, b = cfg2
+    engine.set_reads(reads)
+    bad = b.copy()
+    bad[len(bad) // 2] = len(reads)  # one index past the read set, in the middle of a chunk
+    with pytest.raises(OvlError, match="OVL_E_INDEX"):
+        engine.score(a, bad)
+    sc, en = engine.score(a, b)  # the flag was consumed: the next call is clean
+    np.testing.assert_array_equal(sc, cfg2_ref[0])
+    np.testing.assert_array_equal(en, cfg2_ref[1])
+
+
+def test_pipeline_timing(engine, cfg2):
+    reads, a, b = cfg2
+    engine.set_reads(reads)
+    engine.set_timing(True)
+    engine.score(a, b)
+    t = engine.last_timing()
+    engine.set_timing(False)
+    assert 0.0 < t["kernel_ms"] < t["call_ms"]
+
+
+def test_registered_host_memory_is_used_in_place(engine, cfg2, cfg2_ref):
+    """Results land in an ovl_host_register'ed (pinned) slice of an ordinary buffer."""
+    from ovlgraph import _lib
+    reads, a, b = cfg2
+    engine.set_reads(reads)
+    n = a.shape[0]
+    L = _lib.load()
+    buf = np.zeros(2 * n + 4096, np.int32)
+    base = buf.ctypes.data
+    _lib.check(L.ovl_host_register(ctypes.c_void_p(base), buf.nbytes))
+    try:
+        engine.score(a, b, out=(buf[:n], buf[n:2 * n]))
+    finally:
+        _lib.check(L.ovl_host_unregister(ctypes.c_void_p(base)))
+    np.testing.assert_array_equal(buf[:n], cfg2_ref[0])
+    np.testing.assert_array_equal(buf[n:2 * n], cfg2_ref[1])
+
+
+def test_multi_device_context(oracle_mod, cfg2, cfg2_ref):
+    """ovl_create(0) = every visible GPU (one on a 1-GPU box); same results as a one-GPU engine,
+    through the host list and the resident device list."""
+    from ovlgraph import OverlapEngine, OvlError, _lib
+    reads, a, b = cfg2
+    import torch
+    n_dev = torch.cuda.device_count()
+    eng = OverlapEngine(devices="all")
+    try:
+        assert eng.devices == list(range(n_dev))
+        eng.set_reads(reads)
+        sc, en = eng.score(a, b)
+        np.testing.assert_array_equal(sc, cfg2_ref[0])
+        np.testing.assert_array_equal(en, cfg2_ref[1])
+        assert eng.enumerate_candidates(5) == a.shape[0]
+        cs, ce = eng.score_candidates()
+        np.testing.assert_array_equal(cs, cfg2_ref[0])
+        np.testing.assert_array_equal(ce, cfg2_ref[1])
+    finally:
+        eng.close()
+    with pytest.raises(OvlError, match="OVL_E_ARG"):
+        OverlapEngine(devices=[0, 0])
+    with pytest.raises(OvlError, match="OVL_E_ARG"):
+        OverlapEngine(devices=[n_dev])
+    ctx = ctypes.c_void_p()
+    L = _lib.load()
+    assert L.ovl_create(n_dev + 1, ctypes.byref(ctx)) == -1
+
+
+def test_device_shard_bounds_and_ranges(engine, cfg2, cfg2_ref):
+    from ovlgraph.sharded import pair_costs, shard_bounds
+    reads, a, b = cfg2
+    engine.set_reads(reads)
+    n = engine.enumerate_candidates(5)
+    cost = pair_costs(reads, a, b)
+    for shards in (1, 2, 3, 8):
+        bounds = engine.candidate_shards(shards)
+        want = [0] + [shard_bounds(n, shards, r, cost)[1] for r in range(shards)]
+        assert bounds == want
+        parts = [engine.score_candidates_range(bounds[r], bounds[r + 1]) for r in range(shards)]
+        np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), cfg2_ref[0])
+        np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), cfg2_ref[1])
+    sc, en = engine.score_candidates_range(10, 10)
+    assert sc.size == 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def nccl_world1():
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+def test_sharded_paths_on_rccl_world1(nccl_world1, engine, cfg2, cfg2_ref):
+    """The multi-process drop-in's GPU branches: RCCL world 1, real engine."""
+    from ovlgraph.sharded import ShardedStep, score_pairs_sharded
+    reads, a, b = cfg2
+    sc, en = score_pairs_sharded(reads, a, b, engine=engine)
+    np.testing.assert_array_equal(sc, cfg2_ref[0])
+    np.testing.assert_array_equal(en, cfg2_ref[1])
+    for dest in ("host", "rank0"):
+        for kw in ({"a_idx": a, "b_idx": b}, {"k": 5}):
+            st = ShardedStep(reads, engine=engine, dest=dest, **kw)
+            st.step()
+            st.step()
+            got = st.results()
+            st.close()
+            np.testing.assert_array_equal(got[0], cfg2_ref[0])
+            np.testing.assert_array_equal(got[1], cfg2_ref[1])
+
+
+def test_lane_kernel_on_two_streams(oracle_mod, cfg2):
+    """dp_lane_kernel launches on different streams are ordered on the shared hand-off buffer."""
+    import torch
+    reads, a, b = cfg2
+    eng = _engine_env({"OVL_DP_LANE": "1"})
+    try:
+        eng.set_reads(reads)
+        ta = torch.as_tensor(a, device="cuda")
+        tb = torch.as_tensor(b, device="cuda")
+        outs = []
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        for _ in range(3):
+            for s in streams:
+                so = torch.empty_like(ta)
+                eo = torch.empty_like(ta)
+                eng.score_tensors(ta, tb, so, eo, 10, -1, -2, stream=s)
+                outs.append((so, eo))
+        torch.cuda.synchronize()
+        eng.check_device_errors()
+        rs, re_ = oracle_mod.batch_dp(reads, a, b, 10, -1, -2)
+        for so, eo in outs:
+            np.testing.assert_array_equal(so.cpu().numpy(), rs)
+            np.testing.assert_array_equal(eo.cpu().numpy(), re_)
+    finally:
+        eng.close()
+
+
+# ----------------------------------------------------------------------------- cfg5 at full size
+
+@pytest.fixture(scope="module")
+def cfg5():
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("cfg5", seed=0))
+    a, b = enumerate_candidates(reads, 5)
+    return reads, a, b
+
+
+def test_cfg5_full_default_scoring_vs_oracle(engine, oracle_mod, cfg5):
+    """Every one of cfg5's pairs (default scoring: the W = 8 uniform sweep) == the oracle."""
+    reads, a, b = cfg5
+    assert a.shape[0] > 3_000_000
+    engine.set_reads(reads)
+    assert engine.plan() == "ungapped"
+    sc, en = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+    n = engine.enumerate_candidates(5)
+    assert n == a.shape[0]
+    cs, ce = engine.score_candidates()
+    np.testing.assert_array_equal(cs, rs)
+    np.testing.assert_array_equal(ce, re_)
+
+
+def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
+    """Gapped (indel -2) on the whole cfg5 list: dp_lane_kernel (the planner's choice) ==
+    dp_fast_kernel (OVL_DP_LANE=0) pair for pair; both == the oracle's full DP on a strided
+    50k-pair sample."""
+    reads, a, b = cfg5
+    lane = _engine_env({"OVL_DP_LANE": "1"})
+    fast = _engine_env({"OVL_DP_LANE": "0"})
+    try:
+        lane.set_reads(reads)
+        fast.set_reads(reads)
+        ls, le = lane.score(a, b, 10, -1, -2)
+        fs, fe = fast.score(a, b, 10, -1, -2)
+    finally:
+        lane.close()
+        fast.close()
+    np.testing.assert_array_equal(ls, fs)
+    np.testing.assert_array_equal(le, fe)
+    idx = np.linspace(0, a.shape[0] - 1, 50_000).astype(np.int64)
+    rs, re_ = oracle_mod.batch_dp(reads, a[idx], b[idx], 10, -1, -2)
+    np.testing.assert_array_equal(ls[idx], rs)
+    np.testing.assert_array_equal(le[idx], re_)

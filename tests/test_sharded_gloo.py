@@ -1,4 +1,5 @@
-"""N>1 path on CPU: world_size-2 gloo ranks shard the pair list and gather results in order."""
+"""N>1 path on CPU: world_size-2 gloo ranks shard the pair list and gather results, in reference
+order, to ONE destination: rank 0 (dist.gather) or rank 0's shared host buffer (per-rank copies)."""
 import os
 import socket
 
@@ -19,6 +20,19 @@ def test_shard_bounds_cover_exactly():
             c = [shard_bounds(n, w, r, cost) for r in range(w)]
             assert c[0][0] == 0 and c[-1][1] == n
             assert all(c[i][1] == c[i + 1][0] and c[i][0] <= c[i][1] for i in range(w - 1))
+
+
+def test_shard_bounds_integer_rule():
+    """c[p]*world >= total*r: the device rule of ovl_candidates_shards (cut = first such p)."""
+    rng = np.random.default_rng(5)
+    for n in (1, 5, 300):
+        cost = rng.integers(1, 70000, size=n)
+        c = np.cumsum(cost)
+        for w in (2, 3, 8):
+            for r in range(1, w):
+                lo, _ = shard_bounds(n, w, r, cost)
+                first = next((p for p in range(n) if c[p] * w >= c[-1] * r), n)
+                assert lo >= first and (lo == first or lo == shard_bounds(n, w, r - 1, cost)[1])
 
 
 def _free_port():
@@ -43,16 +57,29 @@ def _worker(rank, world, port, q):
     reads = simulate_reads(read_genome_from_fasta(), 60, 600, 0.02, seed=11)
     distinct, _ = dedup_reads(reads)
     a, b = enumerate_candidates(distinct, 3)
-    sc, en = score_pairs_sharded(distinct, a, b, local_scorer=lambda r, x, y: oracle.batch_ungapped(r, x, y))
-    # the repeated-step form bench.py times at N > 1: setup once, step twice, gather in reference order
+    scorer = lambda r, x, y: oracle.batch_ungapped(r, x, y)  # noqa: E731
+    got = score_pairs_sharded(distinct, a, b, local_scorer=scorer)
+    assert (got is None) == (rank != 0)  # gathered to rank 0 only
+    everyone = score_pairs_sharded(distinct, a, b, local_scorer=scorer, dst=None)
+    assert everyone is not None
+    # the repeated-step form bench.py times at N > 1: setup once, step twice, one destination
     from ovlgraph.sharded import ShardedStep
-    st = ShardedStep(distinct, a, b, local_scorer=lambda r, x, y: oracle.batch_ungapped(r, x, y))
-    st.step()
-    st.step()
-    sc2, en2 = st.results()
-    assert st.gather_bytes() == world * 2 * st.width * 4
+    out = {}
+    for dest in ("host", "rank0"):
+        st = ShardedStep(distinct, a, b, local_scorer=scorer, dest=dest)
+        assert st.bounds[0][0] == 0 and st.bounds[-1][1] == len(a)
+        st.step()
+        st.step()
+        res = st.results()
+        assert (res is None) == (rank != 0)
+        out[dest] = res
+        if dest == "host":
+            assert st.gather_bytes() == 8 * len(a)
+        else:
+            assert st.gather_bytes() == world * 2 * st.width * 4
+        st.close()
     if rank == 0:
-        q.put((a, b, sc, en, distinct, sc2, en2))
+        q.put((a, b, got[0], got[1], distinct, out["host"], out["rank0"], everyone))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -64,7 +91,7 @@ def test_gloo_world2_matches_single_process(oracle_mod):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    a, b, sc, en, distinct, sc2, en2 = q.get(timeout=240)
+    a, b, sc, en, distinct, host, rank0, everyone = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -72,5 +99,6 @@ def test_gloo_world2_matches_single_process(oracle_mod):
     assert len(a) > 100
     np.testing.assert_array_equal(sc, ref_sc)
     np.testing.assert_array_equal(en, ref_en)
-    np.testing.assert_array_equal(sc2, ref_sc)
-    np.testing.assert_array_equal(en2, ref_en)
+    for got_sc, got_en in (host, rank0, everyone):
+        np.testing.assert_array_equal(got_sc, ref_sc)
+        np.testing.assert_array_equal(got_en, ref_en)
