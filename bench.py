@@ -140,26 +140,35 @@ def cpu_baseline(reads, a, b, gpu_score, gpu_end, budget_s: float = 10.0):
     n = a.shape[0]
 
     def run(fn, t, secs):
-        cal = min(n, max(256, 64 * t))
+        # size an evenly strided sample from a calibration pass, then whole passes over it until `secs`
+        cal = min(n, max(1024, 256 * t))
         idx = np.linspace(0, n - 1, cal).astype(np.int64)
         t0 = time.perf_counter()
         fn(reads, a[idx], b[idx], threads=t, encoded=enc)
         per = (time.perf_counter() - t0) / cal
         m = int(min(n, max(cal, secs / max(per, 1e-12))))
         idx = np.linspace(0, n - 1, m).astype(np.int64)
+        sa, sb = a[idx], b[idx]
+        ok, passes = True, 0
         t0 = time.perf_counter()
-        sc, en = fn(reads, a[idx], b[idx], threads=t, encoded=enc)
+        while True:
+            sc, en = fn(reads, sa, sb, threads=t, encoded=enc)
+            passes += 1
+            if passes == 1:
+                ok = bool(np.array_equal(sc, gpu_score[idx]) and np.array_equal(en, gpu_end[idx]))
+            if time.perf_counter() - t0 >= secs:
+                break
         dt = time.perf_counter() - t0
-        ok = bool(np.array_equal(sc, gpu_score[idx]) and np.array_equal(en, gpu_end[idx]))
-        return {"value": m / dt, "pairs": m, "seconds": round(dt, 2), "threads": t, "matches_gpu": ok}
+        return {"value": m * passes / dt, "pairs": m, "passes": passes, "seconds": round(dt, 2), "threads": t,
+                "matches_gpu": ok}
 
     full = run(oracle.batch_dp, threads, budget_s)
     one = run(oracle.batch_dp, 1, budget_s / 2)
     cf = run(oracle.batch_closed_form, threads, 2.0)
     cf1 = run(oracle.batch_closed_form, 1, 2.0)
     return {"value": full["value"], "unit": "overlap-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{full['pairs']} of {n} candidate pairs of the same list (evenly strided), "
-                      f"{full['seconds']} s, through oracle/ovl_oracle.c oracle_batch_dp: the full int32 DP + "
+            "sample": f"{full['pairs']} of {n} candidate pairs of the same list (evenly strided) x "
+                      f"{full['passes']} passes, {full['seconds']} s, through oracle/ovl_oracle.c oracle_batch_dp: the full int32 DP + "
                       f"int8 traceback table per pair of aligners.py:27-57, OpenMP {threads} threads (the box's "
                       f"CPU share per GPU; cpu below lists the machine)",
             "matches_gpu": full["matches_gpu"],

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -94,9 +95,10 @@ struct Dev {
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
     DevBuf lane_col;      // lane-per-pair DP: per-wavefront strip hand-off columns
-    hipEvent_t lane_evt = nullptr;        // last launch that used lane_col ...
-    hipStream_t lane_stream = nullptr;    // ... and its stream (launches on other streams wait for it)
-    bool lane_used = false;
+    DevBuf seed_s, seed_e;  // band knob: the ungapped seed (score, j*) of each pair
+    hipEvent_t scratch_evt = nullptr;     // last launch that used lane_col / seed_* ...
+    hipStream_t scratch_stream = nullptr; // ... and its stream (launches on other streams wait for it)
+    bool scratch_used = false;
     int64_t codes_bytes = 0;
     // device candidate enumeration (ovl_candidates): per-read keys / groups and the pair list
     DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
@@ -267,6 +269,31 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s);
 
+// Per-device scratch (lane_col, seed_*) is shared by every launch of the device.  A launch on stream s
+// first waits for the previous user on another stream; growing a buffer first waits for that user.
+struct ScratchNeed {
+    DevBuf* buf;
+    size_t bytes;
+};
+
+hipError_t scratch_acquire(Dev* c, hipStream_t s, std::initializer_list<ScratchNeed> needs) {
+    hipError_t e = hipSuccess;
+    for (const ScratchNeed& n : needs) {
+        if (n.buf->bytes >= n.bytes) continue;
+        if (c->scratch_used && (e = hipEventSynchronize(c->scratch_evt)) != hipSuccess) return e;
+        if ((e = ensure(*n.buf, n.bytes)) != hipSuccess) return e;
+    }
+    if (c->scratch_used && c->scratch_stream != s) e = hipStreamWaitEvent(s, c->scratch_evt, 0);
+    return e;
+}
+
+hipError_t scratch_release(Dev* c, hipStream_t s) {
+    hipError_t e = hipEventRecord(c->scratch_evt, s);
+    c->scratch_stream = s;
+    c->scratch_used = true;
+    return e;
+}
+
 // Lane-per-pair full DP (ovl_dp_lane.hip): one lane per pair, so it needs many pairs to fill the
 // chip (below that the one-wavefront-per-pair dp_fast_kernel is faster), reads short enough for
 // the per-wavefront hand-off columns, and G = dp - indel*(i+j) inside int32.
@@ -296,14 +323,19 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s) {
     if (n_pairs == 0) return OVL_OK;
+    const int32_t* seed_end = nullptr;
     if (pl.kernel == OVL_KERNEL_BANDED) {
-        // seed j* into d_end, then the banded DP reads it and overwrites (score, end)
+        // seed j* into device scratch (the outputs may be host memory), then the banded DP reads it
+        const size_t sb = sizeof(int32_t) * (size_t)n_pairs;
+        HIPCHK(c, scratch_acquire(c, s, {{&c->seed_s, sb}, {&c->seed_e, sb}}));
         Plan seed;
         seed.kernel = pl.seed_kernel;
         seed.key64 = pl.seed_key64;
         seed.wide = pl.seed_wide;
-        int rc = launch_score_chunk(c, seed, d_a, d_b, n_pairs, match, mismatch, INT32_MIN, d_score, d_end, s);
+        int rc = launch_score_chunk(c, seed, d_a, d_b, n_pairs, match, mismatch, INT32_MIN, as<int32_t>(c->seed_s),
+                                    as<int32_t>(c->seed_e), s);
         if (rc != OVL_OK) return rc;
+        seed_end = as<int32_t>(c->seed_e);
     }
     if (pl.kernel == OVL_KERNEL_UNGAPPED) {
         OvlUngappedArgs g{};
@@ -358,19 +390,14 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.err_flag = as<uint32_t>(c->err_flag);
         g.wide = pl.wide ? 1 : 0;
         g.band = pl.kernel == OVL_KERNEL_BANDED ? pl.band : -1;
+        g.seed = seed_end;
         g.classic = c->dp_classic;
         if (g.band < 0 && !g.wide && !g.classic && use_dp_lane(c, match, mismatch, indel, n_pairs)) {
             OvlLaneArgs k{};
             k.cw = c->lane_cw;
             k.slots = (int64_t)c->cu_count * 4 * ovl_dp_lane_waves_per_simd(k.cw);
             const size_t col_bytes = (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t);
-            if (c->lane_col.bytes < col_bytes) {
-                // reallocation frees the buffer a launch on another stream may still use
-                if (c->lane_used) HIPCHK(c, hipEventSynchronize(c->lane_evt));
-                HIPCHK(c, ensure(c->lane_col, col_bytes));
-            }
-            // one hand-off buffer per device: launches on different streams must not overlap on it
-            if (c->lane_used && c->lane_stream != s) HIPCHK(c, hipStreamWaitEvent(s, c->lane_evt, 0));
+            HIPCHK(c, scratch_acquire(c, s, {{&c->lane_col, col_bytes}}));
             const int64_t L = std::max<int32_t>(c->lmax, 1);
             const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
             const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
@@ -384,9 +411,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
             k.wsfx = c->wmax;
             k.colbuf = as<uint32_t>(c->lane_col);
             HIPCHK(c, ovl_launch_dp_lane(&g, &k, s));
-            HIPCHK(c, hipEventRecord(c->lane_evt, s));
-            c->lane_stream = s;
-            c->lane_used = true;
+            HIPCHK(c, scratch_release(c, s));
             return OVL_OK;
         }
         if (g.band >= 0) {
@@ -428,10 +453,12 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                 k.srow = c->srow;
                 k.wsfx = c->wmax;
                 HIPCHK(c, ovl_launch_band_lane(&g, &k, s));
+                HIPCHK(c, scratch_release(c, s));
                 return OVL_OK;
             }
         }
         HIPCHK(c, ovl_launch_dp(&g, s));
+        if (seed_end) HIPCHK(c, scratch_release(c, s));
     }
     return OVL_OK;
 }
@@ -495,7 +522,7 @@ void destroy_dev(Dev* d) {
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
                       &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
                       &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
-                      &d->lane_col})
+                      &d->lane_col, &d->seed_s, &d->seed_e})
         release(*b);
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
@@ -506,7 +533,7 @@ void destroy_dev(Dev* d) {
             if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : d->t_ev)
         if (e) (void)hipEventDestroy(e);
-    if (d->lane_evt) (void)hipEventDestroy(d->lane_evt);
+    if (d->scratch_evt) (void)hipEventDestroy(d->scratch_evt);
     for (hipStream_t s : {d->stream, d->s_in, d->s_out})
         if (s) (void)hipStreamDestroy(s);
     delete d;
@@ -527,7 +554,7 @@ hipError_t init_dev(Dev* d) {
             e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
             if (e != hipSuccess) return e;
         }
-    e = hipEventCreateWithFlags(&d->lane_evt, hipEventDisableTiming);
+    e = hipEventCreateWithFlags(&d->scratch_evt, hipEventDisableTiming);
     if (e != hipSuccess) return e;
     e = hipHostMalloc((void**)&d->h_flag, 64, hipHostMallocDefault);
     if (e != hipSuccess) return e;
@@ -1183,8 +1210,7 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.out_e = out_end;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = c->timing != 0;
-    // banded plans read their seed back from the outputs: those keep device buffers
-    C.direct = C.out_pinned && p.kernel != OVL_KERNEL_BANDED && c->devs[0]->k.pipe_direct;
+    C.direct = C.out_pinned && c->devs[0]->k.pipe_direct;
     const int32_t S = (int32_t)c->devs.size();
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);
@@ -1418,8 +1444,7 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.out_base = lo;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = ctx->timing != 0;
-    // banded plans read their seed back from the outputs: those keep device buffers
-    C.direct = C.out_pinned && p.kernel != OVL_KERNEL_BANDED && ctx->devs[0]->k.pipe_direct;
+    C.direct = C.out_pinned && ctx->devs[0]->k.pipe_direct;
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);

@@ -321,6 +321,7 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
                                                              int32_t lcap, int32_t match, int32_t mismatch,
                                                              int32_t indel, int32_t* __restrict__ out_score,
                                                              int32_t* __restrict__ out_end,
+                                                             const int32_t* __restrict__ seed,
                                                              uint32_t* __restrict__ err_flag) {
     constexpr int W = (NB - 1) / 2;
     constexpr int NBW = (NB + 3) / 4;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
         if (!live || bad) { a = 0; b = 0; }
         int32_t n = (live && !bad) ? len[a] : 0;
         int32_t m = (live && !bad) ? len[b] : 0;
-        int32_t jstar = (live && !bad) ? out_end[p] : 0;
+        int32_t jstar = (live && !bad) ? seed[p] : 0;
         if (n > lcap || m > lcap || jstar < 0 || jstar > m) { bad = bad || live; n = 0; m = 0; jstar = 0; }
         const uint32_t sa = (uint32_t)off[a];
         const uint32_t tb = (uint32_t)off[b];
@@ -535,7 +536,7 @@ hipError_t launch_band_lane_w(const OvlDpArgs* g, const OvlLaneArgs* k, int64_t 
     ovl::band_lane_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
         g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx,
         g->n_pairs, g->mcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,
-        g->err_flag);
+        g->seed, g->err_flag);
     return hipGetLastError();
 }
 

@@ -51,7 +51,8 @@ struct OvlDpArgs {
     int8_t* tb;          // optional traceback (single pair)
     uint32_t* err_flag;
     int32_t wide;        // int64 arithmetic (else int32, when magnitudes allow)
-    int32_t band;        // < 0: full DP; >= 0: banded around the seed diagonal n - out_end[pair]
+    int32_t band;        // < 0: full DP; >= 0: banded around the seed diagonal n - seed[pair]
+    const int32_t* seed; // banded: the seed ends j* (device memory, never aliases out_*)
     int32_t band_form;   // banded: OVL_BAND_FORM_* -- the host checks each form's limits
     int32_t classic;     // full DP without traceback: use dp_kernel instead of dp_fast_kernel (tests)
 };

@@ -761,8 +761,8 @@ __device__ __forceinline__ int64_t shr1<int64_t>(int64_t v) {
 // Cell rule of aligners.py:35-48 with Acc-width arithmetic; the stored value
 // is narrowed to int32 as the reference's int32 table does.
 // BANDED (the build's band knob, oracle_overlap_banded; not a reference mode):
-// out_end[pair] holds the seed end j* on entry (the ungapped closed form's
-// first argmax, written by the launch before); only cells with
+// seed[pair] holds the seed end j* (the ungapped closed form's first argmax,
+// written by the launch before into a separate buffer, so out_* may be host memory); only cells with
 // |(i - j) - d*| <= band, d* = n - j*, are filled, out-of-band predecessors
 // count as -inf, and only strips and anti-diagonal steps that meet the band are
 // swept.  A cell's diagonal predecessor is always in the band; "up" leaves it
@@ -772,8 +772,8 @@ __global__ __launch_bounds__(64) void dp_kernel(
     const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx,
     int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel, int32_t band,
-    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, int8_t* __restrict__ tb,
-    uint32_t* __restrict__ err_flag) {
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, const int32_t* __restrict__ seed,
+    int8_t* __restrict__ tb, uint32_t* __restrict__ err_flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int32_t* row0 = reinterpret_cast<int32_t*>(smem);
     int32_t* row1 = row0 + (mcap + 1);
@@ -795,7 +795,7 @@ __global__ __launch_bounds__(64) void dp_kernel(
         const uint8_t* s = codes + off[a];
         const uint8_t* t = codes + off[b];
         // band: seed diagonal d* and the rows [rlo, rhi] that hold band cells
-        const int32_t dstar = BANDED ? n - out_end[pair] : 0;
+        const int32_t dstar = BANDED ? n - seed[pair] : 0;
         const int32_t W = BANDED ? band : 0;
         const int32_t rlo = BANDED ? (dstar - W + 1 > 1 ? dstar - W + 1 : 1) : 1;
         __syncthreads();  // previous pair's LDS readers are done
@@ -866,7 +866,7 @@ __global__ __launch_bounds__(64) void dp_kernel(
         const int owner = (n - 1) & 63;
         const int32_t bs = __shfl(best, owner, 64);
         const int32_t be = __shfl(bend, owner, 64);
-        __syncthreads();  // every lane has read out_end[pair] (banded seed) before it is overwritten
+        __syncthreads();  // every lane is done with this pair's LDS rows
         if (lane == 0) {
             out_score[pair] = n > 0 && m > 0 ? bs : 0;
             out_end[pair] = n > 0 && m > 0 ? be : 0;
@@ -900,7 +900,8 @@ __global__ __launch_bounds__(64) void dp_fast_kernel(
     const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx,
     int64_t n_pairs, int32_t mcap, int64_t match, int64_t mismatch, int64_t indel, int32_t band,
-    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, const int32_t* __restrict__ seed,
+    uint32_t* __restrict__ err_flag) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // rows hold columns 0 .. 64*nch + 64 (hand-off chunks of 64 columns); t codes padded likewise
     const int32_t pitch = ((mcap + 126) / 64) * 64 + 64;
@@ -924,10 +925,10 @@ __global__ __launch_bounds__(64) void dp_fast_kernel(
         const uint8_t* s = codes + off[a];
         const uint8_t* t = codes + off[b];
         const int32_t nch = (m + 126) / 64;  // chunks covering tau = 0 .. m + 62
-        // band: seed diagonal d* (out_end holds the ungapped seed end j*) and the first row with
+        // band: seed diagonal d* (seed holds the ungapped seed end j*) and the first row with
         // a band cell of column >= 1; the band of row i is columns [i - d* - W, i - d* + W]
         const int32_t W = BANDED ? band : 0;
-        const int32_t dstar = BANDED ? n - out_end[pair] : 0;
+        const int32_t dstar = BANDED ? n - seed[pair] : 0;
         const int32_t rlo = BANDED ? (dstar - W + 1 > 1 ? dstar - W + 1 : 1) : 1;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // previous pair's LDS readers are done
         for (int j = lane; j < pitch; j += 64) row0[j] = 0;
@@ -1069,7 +1070,7 @@ __global__ __launch_bounds__(256) void band_row_kernel(
     const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
     int32_t lcap, int32_t match, int32_t mismatch, int32_t indel, int32_t band, int32_t* __restrict__ out_score,
-    int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    int32_t* __restrict__ out_end, const int32_t* __restrict__ seed, uint32_t* __restrict__ err_flag) {
     constexpr int PPW = 64 / SEG;  // pairs per wavefront
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
@@ -1093,7 +1094,7 @@ __global__ __launch_bounds__(256) void band_row_kernel(
             out_score[p] = -1;
             out_end[p] = -1;
         }
-        const int32_t jstar = ok ? out_end[p] : 0;  // seed from the ungapped launch
+        const int32_t jstar = ok ? seed[p] : 0;  // seed from the ungapped launch
         const int32_t dstar = n - jstar;
         // stage s and t of this pair in LDS (the segment's lanes copy them)
         if (ok) {
@@ -1322,7 +1323,8 @@ __global__ __launch_bounds__(64, (D <= 4 ? 8 : 6)) void band_diag_kernel(
     const uint8_t* __restrict__ codes, const int64_t* __restrict__ off, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
     int32_t lcap, int32_t match, int32_t mismatch, int32_t indel, int32_t W, int32_t nseg,
-    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, const int32_t* __restrict__ seed,
+    uint32_t* __restrict__ err_flag) {
     constexpr int U = 8;       // iterations (2 anti-diagonal steps each) per unrolled block
     constexpr int H = D / 2;   // slots of one parity
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1355,7 +1357,7 @@ __global__ __launch_bounds__(64, (D <= 4 ? 8 : 6)) void band_diag_kernel(
             if (!bad) {
                 n = len[a];
                 m = len[b];
-                jstar = out_end[pair];
+                jstar = seed[pair];
                 bad = n > lcap || m > lcap || jstar < 0 || jstar > m;
                 sg = codes + off[a];
                 tg = codes + off[b];
@@ -1515,7 +1517,7 @@ template <typename Acc, bool BANDED>
 static void launch_dp_t(const OvlDpArgs* g, unsigned blocks, size_t lds, hipStream_t stream) {
     dp_kernel<Acc, BANDED><<<blocks, 64, lds, stream>>>(g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx,
                                                          g->n_pairs, g->mcap, g->match, g->mismatch, g->indel,
-                                                         g->band, g->out_score, g->out_end, g->tb, g->err_flag);
+                                                         g->band, g->out_score, g->out_end, g->seed, g->tb, g->err_flag);
 }
 
 template <int SEG, int NC>
@@ -1527,7 +1529,7 @@ static void launch_band_row_t(const OvlDpArgs* g, hipStream_t stream) {
     const size_t lds = (size_t)4 * PPW * 2 * g->mcap;
     band_row_kernel<SEG, NC><<<(unsigned)blocks, 256, lds, stream>>>(
         g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, (int32_t)g->match,
-        (int32_t)g->mismatch, (int32_t)g->indel, g->band, g->out_score, g->out_end, g->err_flag);
+        (int32_t)g->mismatch, (int32_t)g->indel, g->band, g->out_score, g->out_end, g->seed, g->err_flag);
 }
 
 template <int D, int KW>
@@ -1540,7 +1542,7 @@ static void launch_band_diag_t(const OvlDpArgs* g, int nseg, hipStream_t stream)
     if (blocks > 32768) blocks = 32768;
     band_diag_kernel<D, KW><<<(unsigned)blocks, 64, lds, stream>>>(
         g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, (int32_t)lcap, (int32_t)g->match,
-        (int32_t)g->mismatch, (int32_t)g->indel, W, nseg, g->out_score, g->out_end, g->err_flag);
+        (int32_t)g->mismatch, (int32_t)g->indel, W, nseg, g->out_score, g->out_end, g->seed, g->err_flag);
 }
 
 // Slots per lane for the anti-diagonal form: the VALU cost per pair-iteration is about
@@ -1612,7 +1614,7 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
                 const size_t lds2 = (size_t)2 * pitch * sizeof(int32_t) + (size_t)pitch;
                 dp_fast_kernel<int32_t, true><<<nb, 64, lds2, stream>>>(
                     g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
-                    g->mismatch, g->indel, g->band, g->out_score, g->out_end, g->err_flag);
+                    g->mismatch, g->indel, g->band, g->out_score, g->out_end, g->seed, g->err_flag);
                 return hipGetLastError();
             }
             default:
@@ -1626,11 +1628,11 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* g, hipStream_t stream) {
         if (g->wide)
             dp_fast_kernel<int64_t, false><<<nb, 64, lds2, stream>>>(
                 g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
-                g->mismatch, g->indel, -1, g->out_score, g->out_end, g->err_flag);
+                g->mismatch, g->indel, -1, g->out_score, g->out_end, g->seed, g->err_flag);
         else
             dp_fast_kernel<int32_t, false><<<nb, 64, lds2, stream>>>(
                 g->codes, g->off, g->len, g->n_reads, g->a_idx, g->b_idx, g->n_pairs, g->mcap, g->match,
-                g->mismatch, g->indel, -1, g->out_score, g->out_end, g->err_flag);
+                g->mismatch, g->indel, -1, g->out_score, g->out_end, g->seed, g->err_flag);
     } else if (g->wide) {
         launch_dp_t<int64_t, false>(g, nb, lds, stream);
     } else {

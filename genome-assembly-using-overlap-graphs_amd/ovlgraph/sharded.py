@@ -248,7 +248,16 @@ class ShardedStep:
         else:
             self.packed = torch.full((2, self.width), -1, dtype=torch.int32, device=self.device)
             self.rows = ([torch.empty_like(self.packed) for _ in range(self.world)] if self.rank == 0 else None)
-            if self.eng is not None and hi > lo:
+            if self.eng is not None and hi > lo and self.device.type != "cuda":
+                # gloo (one-GPU rehearsal): the rows live in host memory, so score through the host API
+                rows = self.packed.numpy()
+                if self.on_device_list:
+                    self._launch = lambda: self.eng.score_candidates_range(
+                        lo, hi, match, mismatch, indel, out=(rows[0], rows[1]))
+                else:
+                    self._launch = lambda: self.eng.score(self.a[lo:hi], self.b[lo:hi], match, mismatch, indel,
+                                                          out=(rows[0], rows[1]))
+            elif self.eng is not None and hi > lo:
                 if self.on_device_list:
                     pa, pb, _ = self.eng.candidates_device()
                     self._launch = lambda: self.eng.score_device(
