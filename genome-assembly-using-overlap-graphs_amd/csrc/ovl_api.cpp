@@ -52,6 +52,7 @@ struct Knobs {
     int64_t lane_min_pairs = 65536;  // OVL_LANE_MIN_PAIRS env: auto threshold (one tile per SIMD)
     int32_t lane_prof = 1;        // OVL_LANE_PROF=0: compare/select scores instead of the byte profile (tests)
     int32_t lane_col16 = 1;       // OVL_LANE_COL16=0: int32 hand-off column even when int16 holds (tests)
+    int32_t lane_lds = 1;         // OVL_LANE_LDS=0: hand-off column in HBM even when the LDS form holds (tests)
     int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
     int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
                                   // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
@@ -81,6 +82,7 @@ struct Dev {
     int64_t& lane_min_pairs = k.lane_min_pairs;
     int32_t& lane_prof = k.lane_prof;
     int32_t& lane_col16 = k.lane_col16;
+    int32_t& lane_lds = k.lane_lds;
     int32_t& lane_sfx = k.lane_sfx;
     int32_t& blocks_per_cu = k.blocks_per_cu;
     // resident reads
@@ -403,8 +405,13 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
             const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
             k.prof = c->lane_prof && c->planes == 2 && indel <= 0 && sma >= -128 && sma <= 127 && smm >= -128 &&
                      smm <= 127;
-            k.col16 = c->lane_col16 && (4 * L + 4) * M < (int64_t(1) << 15);
+            k.ho = c->lane_col16 && (4 * L + 4) * M < (int64_t(1) << 15) ? 1 : 0;
             k.sfx = k.prof && c->lane_sfx && c->wmax > 0;
+            // column steps G[i][j] - G[i-1][j] lie in [0, max(match, mismatch) - 2*indel]: 4 bits in LDS
+            const int64_t step_max = std::max<int64_t>(match, mismatch) - 2 * indel;
+            if (c->lane_lds && k.sfx && k.cw != 16 && indel <= 0 && std::max<int64_t>(match, mismatch) >= indel &&
+                step_max <= 15 && g.mcap <= 256)
+                k.ho = 2;
             k.sfx_words = as<uint32_t>(c->sfx);
             k.pfx_words = as<uint32_t>(c->pfx);
             k.srow = c->srow;
@@ -495,6 +502,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_LANE_MIN_PAIRS")) k.lane_min_pairs = atoll(e);
     if (const char* e = getenv("OVL_LANE_PROF")) k.lane_prof = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_LANE_COL16")) k.lane_col16 = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LANE_LDS")) k.lane_lds = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_LANE_SFX")) k.lane_sfx = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
         const int v = atoi(e);

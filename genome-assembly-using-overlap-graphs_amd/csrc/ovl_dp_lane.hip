@@ -34,6 +34,8 @@
 namespace ovl {
 namespace {
 
+constexpr int32_t kLaneLdsMaxLen = 256;  // HO 2: 32 KiB of hand-off words per block, 4 blocks per CU
+
 __device__ __forceinline__ int32_t wave_max(int32_t v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
@@ -54,12 +56,17 @@ __device__ __forceinline__ int32_t wave_min(int32_t v) {
 //          (2 VALU per cell); virtual rows select an all-zero profile, which reproduces row 0
 //          exactly (row 0 rises by -indel per column, so neither the diagonal nor the left move
 //          can exceed it), so no cell needs a mask
-//   COL16  |G| < 2^15: the hand-off column as int16, two rows per dword (half the traffic)
+//   HO     hand-off column: 0 = int32 in HBM; 1 = int16 in HBM, two rows per dword (|G| < 2^15);
+//          2 = 4-bit row differences in LDS, eight rows per dword.  The column's steps
+//          G[i][j] - G[i-1][j] lie in [0, max(match, mismatch) - 2*indel] (up move: >= 0; by
+//          induction over j the diagonal and left moves stay below it), so when that is <= 15 a
+//          lane's 256-row column is 128 bytes and a wavefront's fits LDS beside 15 others: no
+//          hand-off traffic leaves the CU
 //   SFX    (PROF) the row symbols come from the resident bit-plane rows (sfx, right-aligned):
 //          with the row count a multiple of 32, row iteration `it` reads bit it % 32 of word
 //          it / 32 + W - R / 32 on every lane, so a lane loads 8 bytes per 32 rows instead of
 //          a byte gather per row
-template <int CW, int OCC, bool PROF, bool COL16, bool SFX>
+template <int CW, int OCC, bool PROF, int HO, bool SFX>
 __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __restrict__ codes,
                                                            const int64_t* __restrict__ off,
                                                            const int32_t* __restrict__ len, int32_t n_reads,
@@ -73,7 +80,12 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                                                            int32_t* __restrict__ out_end,
                                                            uint32_t* __restrict__ err_flag) {
     static_assert(!SFX || PROF, "bit-plane row symbols need the byte profile");
+    static_assert(HO != 2 || SFX, "the LDS hand-off works on 8-row words (row count a multiple of 32)");
+    constexpr bool COL16 = HO == 1;
+    constexpr bool LH = HO == 2;
     const int lane = threadIdx.x & 63;
+    extern __shared__ uint32_t lds_hand[];  // LH: [row / 8][wavefront in block][lane]
+    uint32_t* __restrict__ hcol = lds_hand + (threadIdx.x >> 6) * 64 + lane;
     const int64_t wslot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t nslots = (int64_t)gridDim.x * 4;
     uint32_t* __restrict__ col = colbuf + wslot * (int64_t)rcap * 64 + lane;
@@ -152,6 +164,12 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
             constexpr int NCW = COL16 ? 2 : 4;
             constexpr int NQS = SFX ? 1 : 4;
             uint32_t qs[NQS], qc[NCW];
+            // LH: the hand-off words of rows it..it+7 (read) and the next 8 (prefetched), the word being
+            // written, and the running values the 4-bit steps start from: the left column's value of the
+            // row before `it` and this strip's last column in that row (row 0's values carry through the
+            // virtual rows, whose steps are 0)
+            uint32_t hr = 0, hn = 0, hw = 0;
+            int32_t lprev = -g * j0, vprev = -g * (j0 + CW);
             uint32_t S0 = 0, S1 = 0, S0n = 0, S1n = 0;  // SFX: bit planes of the current / next 32 rows
             auto fetch4 = [&](int32_t it4) {
                 if constexpr (!SFX) {
@@ -162,7 +180,7 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                         qs[k] = (uint32_t)codes[sa + (uint32_t)ic];
                     }
                 }
-                if constexpr (!FIRST) {
+                if constexpr (!FIRST && !LH) {
 #pragma unroll
                     for (int k = 0; k < NCW; ++k) qc[k] = col[(int64_t)((COL16 ? it4 / 2 : it4) + k) * 64];
                 }
@@ -242,6 +260,41 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
                     }
                 }
                 if (it + 4 < R) fetch4(it + 4);
+                if constexpr (LH) {
+                    const uint32_t sh = (uint32_t)(it & 4) * 4u;  // this body's half of the 8-row word
+                    if constexpr (!FIRST) {
+                        if ((it & 4) == 0) {
+                            hr = hn;
+                            if (it + 8 < R) hn = hcol[(int64_t)(it / 8 + 1) * 256];
+                        }
+                    }
+                    int32_t lf[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if constexpr (FIRST) {
+                            lf[k] = -g * (it + k - sk + 1);
+                        } else {
+                            lprev += (int32_t)__builtin_amdgcn_ubfe(hr, sh + 4u * k, 4u);
+                            lf[k] = lprev;
+                        }
+                    }
+                    const int32_t v0 = row(it, A, B, s4[0], lf[0], masked_tag);
+                    const int32_t v1 = row(it + 1, B, A, s4[0], lf[1], masked_tag);
+                    const int32_t v2 = row(it + 2, A, B, s4[0], lf[2], masked_tag);
+                    const int32_t v3 = row(it + 3, B, A, s4[0], lf[3], masked_tag);
+                    // steps of this strip's last column (also after the last strip: never read, no branch)
+                    uint32_t h = (uint32_t)(v0 - vprev);
+                    h |= (uint32_t)(v1 - v0) << 4;
+                    h |= (uint32_t)(v2 - v1) << 8;
+                    h |= (uint32_t)(v3 - v2) << 12;
+                    vprev = v3;
+                    if ((it & 4) == 0) {
+                        hw = h;
+                    } else {
+                        hcol[(int64_t)(it / 8) * 256] = hw | (h << 16);
+                    }
+                    return;
+                }
                 const int32_t v0 = row(it, A, B, s4[0], left(it, c4, 0), masked_tag);
                 const int32_t v1 = row(it + 1, B, A, s4[SFX ? 0 : 1], left(it + 1, c4, 1), masked_tag);
                 const int32_t v2 = row(it + 2, A, B, s4[SFX ? 0 : 2], left(it + 2, c4, 2), masked_tag);
@@ -259,6 +312,7 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
             };
             if constexpr (SFX) fetch_planes(0);
             fetch4(0);
+            if constexpr (LH && !FIRST) hn = hcol[0];
             int32_t it = 0;
             for (; it < mcut; it += 4) body(it, std::true_type{});
             for (; it < R; it += 4) body(it, std::false_type{});
@@ -488,8 +542,12 @@ using ovl::dp_lane_kernel;
 
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap) { return ((lcap + 31) & ~31) + 4; }
 
-// strip width per lane-kernel variant: 16 columns at 6 waves/SIMD, 32 columns at 4 waves/SIMD
-extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw) { return cw == 32 ? 4 : 6; }
+// waves per SIMD each strip width is compiled for: 16 columns at 6, 32 columns at 4 (64 columns spill even
+// at 3 waves per SIMD: the 4-row body keeps two rows of the strip live)
+extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw) { return cw == 16 ? 6 : 4; }
+
+// the LDS hand-off (HO 2): rows rounded to 32, 4 bits per row, a dword per 8 rows, per wavefront of the block
+extern "C" int32_t ovl_dp_lane_lds_bytes(int32_t lcap) { return ((lcap + 31) & ~31) / 8 * 4 * 64 * 4; }
 
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* k, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
@@ -499,26 +557,29 @@ extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* 
     const int32_t lcap = g->mcap;
     const int32_t rcap = ovl_dp_lane_rcap(lcap);
     if (k->sfx && (!k->prof || !k->sfx_words || k->wsfx * 32 < lcap)) return hipErrorInvalidValue;
-#define OVL_LANE(CW, OCC, PR, C16, SX)                                                                        \
-    dp_lane_kernel<CW, OCC, PR, C16, SX><<<(unsigned)blocks, 256, 0, stream>>>(                             \
+    if (k->ho == 2 && (!k->sfx || k->cw == 16 || lcap > ovl::kLaneLdsMaxLen)) return hipErrorInvalidValue;
+    const size_t shmem = k->ho == 2 ? (size_t)ovl_dp_lane_lds_bytes(lcap) : 0;
+#define OVL_LANE(CW, OCC, PR, HO, SX)                                                                         \
+    dp_lane_kernel<CW, OCC, PR, HO, SX><<<(unsigned)blocks, 256, shmem, stream>>>(                           \
         g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx, g->n_pairs, \
         lcap, rcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, k->colbuf, g->out_score,     \
         g->out_end, g->err_flag)
-    const int key = (k->cw == 32 ? 8 : k->cw == 16 ? 0 : 64) | (k->prof ? 4 : 0) | (k->col16 ? 2 : 0) |
-                    (k->sfx ? 1 : 0);
+    const int cwk = k->cw == 32 ? 1 : (k->cw == 16 ? 0 : 3);
+    const int key = cwk << 5 | (k->prof ? 8 : 0) | (k->ho & 3) << 1 | (k->sfx ? 1 : 0);
     switch (key) {
-        case 0: OVL_LANE(16, 6, false, false, false); break;
-        case 2: OVL_LANE(16, 6, false, true, false); break;
-        case 4: OVL_LANE(16, 6, true, false, false); break;
-        case 5: OVL_LANE(16, 6, true, false, true); break;
-        case 6: OVL_LANE(16, 6, true, true, false); break;
-        case 7: OVL_LANE(16, 6, true, true, true); break;
-        case 8: OVL_LANE(32, 4, false, false, false); break;
-        case 10: OVL_LANE(32, 4, false, true, false); break;
-        case 12: OVL_LANE(32, 4, true, false, false); break;
-        case 13: OVL_LANE(32, 4, true, false, true); break;
-        case 14: OVL_LANE(32, 4, true, true, false); break;
-        case 15: OVL_LANE(32, 4, true, true, true); break;
+        case 0x00: OVL_LANE(16, 6, false, 0, false); break;
+        case 0x02: OVL_LANE(16, 6, false, 1, false); break;
+        case 0x08: OVL_LANE(16, 6, true, 0, false); break;
+        case 0x09: OVL_LANE(16, 6, true, 0, true); break;
+        case 0x0A: OVL_LANE(16, 6, true, 1, false); break;
+        case 0x0B: OVL_LANE(16, 6, true, 1, true); break;
+        case 0x20: OVL_LANE(32, 4, false, 0, false); break;
+        case 0x22: OVL_LANE(32, 4, false, 1, false); break;
+        case 0x28: OVL_LANE(32, 4, true, 0, false); break;
+        case 0x29: OVL_LANE(32, 4, true, 0, true); break;
+        case 0x2A: OVL_LANE(32, 4, true, 1, false); break;
+        case 0x2B: OVL_LANE(32, 4, true, 1, true); break;
+        case 0x2D: OVL_LANE(32, 4, true, 2, true); break;
         default: return hipErrorInvalidValue;
     }
 #undef OVL_LANE

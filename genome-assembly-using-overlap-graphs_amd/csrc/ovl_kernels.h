@@ -70,7 +70,8 @@ extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out
 struct OvlLaneArgs {
     int32_t cw;                 // strip width: 16 or 32 columns
     int32_t prof;               // byte score profile (<= 4 symbols, diagonal scores in int8, indel <= 0)
-    int32_t col16;              // int16 hand-off column (|G| < 2^15)
+    int32_t ho;                 // hand-off column: 0 int32 in HBM, 1 int16 in HBM (|G| < 2^15), 2 4-bit steps
+                                // in LDS (sfx, cw 32, max(match, mismatch) - 2*indel <= 15, lmax <= 256)
     int32_t sfx;                // (prof) row symbols from the resident suffix bit planes
     const uint32_t* sfx_words;  // sfx / pfx layouts of ovl_set_reads (2 planes), srow words per read, wsfx words
     const uint32_t* pfx_words;
@@ -81,6 +82,7 @@ struct OvlLaneArgs {
 };
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);
+extern "C" int32_t ovl_dp_lane_lds_bytes(int32_t lcap);
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
 // band knob, a lane per pair (ovl_dp_lane.hip): ovl_band_lane_ok(band), <= 4 symbols, scores in int8;
 // uses lane->slots, and lane->sfx (row symbols and t codes from the bit planes) with sfx/pfx_words

@@ -293,10 +293,18 @@ __device__ __forceinline__ typename Key<KM>::T sweep_shifts(const uint32_t* Sw, 
 // branch.  Per block q the running max is kept without its q-constant
 // (key = keyq + 32q*M', M' = (match << 16) - 1), so an end position costs one
 // v_mad_i32_i24 and one v_max.
+//
+// t-truncated pairs (n = lw, m < lw: read b cut at the genome end, generateErrorFreeReads.py:45-46) ride
+// the same sweep: their end positions j <= m compare only real t bases, so their keys are the uniform
+// keys, and only j > m must be dropped.  Blocks q < m/32 are always valid, blocks above m/32 never;
+// block qm = m/32 is valid for r <= m % 32, so the lane snapshots best[qm] right after shift r = m % 32.
+// tmask (scalar) has bit r set iff some lane of the wavefront snapshots at shift r, so a step takes the
+// snapshot branch only on those shifts; tm = m for a t-truncated lane, -1 otherwise.
 template <int W, int KM>
 __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw, const uint32_t* Tw, int32_t lw,
                                                              int32_t match, int32_t dms, uint32_t r_lo,
-                                                             uint32_t r_hi) {
+                                                             uint32_t r_hi, uint32_t tmask = 0u,
+                                                             int32_t tm = -1) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int TW = W + 1;
@@ -390,6 +398,22 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     // r = 0 (t unshifted, block W when lw = 32W) through keys; r >= 1 through keys_s for W <= 4 (A/B on
     // one box: cfg2 -0.7 %, target -0.4 %; at W = 5, cfg3, +1.3 %, so W >= 5 keeps the t shift)
     constexpr bool SHIFT_S = W <= 4;
+    // t-truncated lanes: the best key of blocks 0..qm as they stand after shift m % 32 (block qm's last
+    // valid end position).  A max under "q <= qm" masks, not a select on "q == qm": the compiler turns
+    // an equality select chain into an indexed table, and the block maxima into an LDS array.
+    T snap = 0;
+    auto snapshot = [&](uint32_t r) {
+        if (tm >= 0 && (uint32_t)(tm & 31) == r) {
+            const int32_t qm = tm >> 5;
+            T v = best[0] + qoff[0];
+#pragma unroll
+            for (int q = 1; q < W; ++q) {
+                const T k = best[q] + qoff[q];
+                v = q <= qm && k > v ? k : v;
+            }
+            snap = v;
+        }
+    };
     auto body = [&](uint32_t r, uint32_t vt, T rm, auto nq_tag) {
         constexpr int NQ = decltype(nq_tag)::value;
         T kq[W + 1];
@@ -401,6 +425,7 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) best[q] = kq[q] > best[q] ? kq[q] : best[q];
+        if ((tmask >> r) & 1u) snapshot(r);  // scalar branch
     };
     // two consecutive r per step: per block one 3-way max (v_max3_i32) for both keys
     auto body2 = [&](uint32_t r, T rm, auto nq_tag) {
@@ -412,6 +437,26 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
         } else {
             keys(r, (uint32_t)((int32_t)0x80000000 >> (r - 1)), rm, nq_tag, k0);
             keys(r + 1, (uint32_t)((int32_t)0x80000000 >> r), rm + mq, nq_tag, k1);
+        }
+        // scalar branch: a lane snapshots after r or r + 1, from the block maxima before this step's
+        // update (kept apart from it, so the update stays one v_max3_i32 per block)
+        if ((tmask >> r) & 3u) {
+            const uint32_t d = (uint32_t)(tm & 31) - r;
+            if (tm >= 0 && d <= 1u) {
+                const int32_t qm = tm >> 5;
+                T v = 0;
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    T k = best[q];
+                    if (q < NQ) {
+                        const T kk = d ? (k0[q] > k1[q] ? k0[q] : k1[q]) : k0[q];
+                        k = kk > k ? kk : k;
+                    }
+                    k += qoff[q];
+                    v = q <= qm && k > v ? k : v;
+                }
+                snap = v;
+            }
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -464,6 +509,16 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     for (int q = 0; q <= W; ++q) {
         const T k = best[q] + qoff[q];
         out = k > out ? k : out;
+    }
+    if (tm >= 0) {  // t-truncated: blocks below qm whole, block qm up to its snapshot
+        const int32_t qm = tm >> 5;
+        T t = snap > 0 ? snap : 0;
+#pragma unroll
+        for (int q = 0; q < W - 1; ++q) {
+            const T k = best[q] + qoff[q];
+            t = q < qm && k > t ? k : t;
+        }
+        out = t;
     }
     return out;
 }
@@ -544,6 +599,10 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = (W * P + 3) & ~3;
+    // t-truncated pairs in the sweep (snapshot): throughput mode with int32 keys.  Not in latency mode,
+    // where the side wave scores them concurrently and the sweep is the critical path (A/B, cfg2:
+    // 8.2 -> 9.0 us with them in the sweep)
+    constexpr bool TT = KM == 0 && !LAT;
     constexpr int RING = 128;                      // >= 15 left over + 64 from one tile
     constexpr int ROWQ = (SROW + TROW) / 4;        // uint4 per staged side pair (latency mode)
     __shared__ int4 ring_all[LAT ? 1 : 4][RING];   // throughput mode: 8 KiB per block
@@ -603,7 +662,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
                 out_score[p] = -1;
                 out_end[p] = -1;
             }
-            const bool push = ok && !(n == lw && m == lw);
+            // (n = lw, m <= lw) pairs are the sweeping wave's: uniform and (TT) t-truncated alike
+            const bool push = ok && (TT ? n != lw : !(n == lw && m == lw));
             const uint64_t pm = __ballot(push);
             int4* ent = side_ent[LAT ? grp : 0];
             uint4* rows = side_rows + (LAT ? grp * 64 * ROWQ : 0);
@@ -660,12 +720,20 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         uint32_t Sw[SROW], Tw[TROW];
         load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
         load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
-        // both reads of length lw? one bit per read (L1-resident bitmap) instead of two len gathers
-        const bool uni = ok && ((full[a >> 5] >> (a & 31)) & (full[b >> 5] >> (b & 31)) & 1u);
+        // read a of length lw? one bit per read (L1-resident bitmap); b's length decides uniform (m = lw)
+        // or t-truncated (m < lw, scored by this sweep with a snapshot); a shorter read a is a side pair
+        const bool fa = ok && ((full[a >> 5] >> (a & 31)) & 1u);
+        const int32_t mb = len[b];
+        const bool uni = fa && mb == lw;
+        const bool tt = TT && fa && mb < lw;
+        const int32_t tm = tt ? mb : -1;
+        uint32_t tmask = 0;
+        for (uint64_t bm = __ballot(tt); bm; bm &= bm - 1)  // scalar loop over the t-truncated lanes
+            tmask |= 1u << (__builtin_amdgcn_readlane(mb, (int)__builtin_ctzll(bm)) & 31);
         OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
         if constexpr (!LAT) {
             if (mine && !ok) atomicOr(err_flag, 1u);
-            const bool push = ok && !uni;
+            const bool push = ok && !uni && !tt;
             const uint64_t pm = __ballot(push);
             if (push)
                 ring[(tail + __popcll(pm & ((1ull << lane) - 1ull))) & (RING - 1)] = make_int4((int32_t)p, a, b, 0);
@@ -675,10 +743,10 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         T best = (T)(Sw[0] ^ Tw[0] ^ Sw[SROW - 1] ^ Tw[TROW - 1]) & 0;
         asm volatile("" ::"v"(Sw[0]), "v"(Tw[0]), "v"(Sw[SROW - 1]), "v"(Tw[TROW - 1]));
 #else
-        T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, 0u, 32u);
+        T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, 0u, 32u, tmask, tm);
 #endif
         OVL_TR_CLOCK(3, (uint32_t)best);
-        if (mine && (uni || (!LAT && !ok))) {
+        if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
             out_score[p] = ok ? sc : -1;

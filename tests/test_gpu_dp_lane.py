@@ -36,20 +36,26 @@ def _engine_env(env):
 LENS = [0, 1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 47, 63, 64, 65, 100, 127, 128, 129, 250, 251, 255]
 
 
-@pytest.fixture(scope="module")
-def mixed_set():
-    rng = random.Random(2024)
-    reads = [_rand(rng, rng.choice(LENS)) for _ in range(150)] + [_rand(rng, rng.randint(1, 260)) for _ in range(150)]
+@pytest.fixture(scope="module", params=[256, 260])
+def mixed_set(request):
+    """lmax 256: bit-plane layouts exist (row symbols from the planes, the LDS hand-off); 260: they do not."""
+    lmax = request.param
+    rng = random.Random(2024 + lmax)
+    reads = [_rand(rng, rng.choice(LENS)) for _ in range(150)] + [_rand(rng, rng.randint(1, lmax)) for _ in range(150)]
+    reads[0] = _rand(rng, lmax)
     n = len(reads)
     a = np.array([rng.randrange(n) for _ in range(3001)], dtype=np.int32)
     b = np.array([rng.randrange(n) for _ in range(3001)], dtype=np.int32)
     return reads, a, b
 
 
-VARIANTS = {  # strip width x byte score profile x int16 hand-off column x bit-plane row symbols
-    f"cw{cw}-prof{pr}-col16{c16}-sfx{sx}": {"OVL_LANE_CW": cw, "OVL_LANE_PROF": pr, "OVL_LANE_COL16": c16,
-                                             "OVL_LANE_SFX": sx}
-    for cw in ("16", "32") for pr in ("0", "1") for c16 in ("0", "1") for sx in ("0", "1") if pr == "1" or sx == "0"}
+# strip width x byte score profile x int16 hand-off column x bit-plane row symbols x LDS hand-off (4-bit column
+# steps; taken when the scoring bounds them by 15, the profile and planes are on and lmax <= 256)
+VARIANTS = {
+    f"cw{cw}-prof{pr}-col16{c16}-sfx{sx}-lds{ld}": {"OVL_LANE_CW": cw, "OVL_LANE_PROF": pr, "OVL_LANE_COL16": c16,
+                                                    "OVL_LANE_SFX": sx, "OVL_LANE_LDS": ld}
+    for cw in ("16", "32") for pr in ("0", "1") for c16 in ("0", "1") for sx in ("0", "1") for ld in ("0", "1")
+    if (pr == "1" or sx == "0") and (ld == "0" or (cw == "32" and pr == "1" and sx == "1"))}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -64,7 +70,8 @@ def test_lane_vs_oracle_mixed_lengths(oracle_mod, mixed_set, params, variant):
     rs, re_ = oracle_mod.batch_dp(reads, a, b, *params)
     with _engine_env(dict(VARIANTS[variant], OVL_DP_LANE="1")) as eng:
         eng.set_reads(reads)
-        assert eng.plan(*params) == "dp"
+        # (0, 0, -1) over bit-plane reads is the closed form (gaps cannot win): still checked
+        assert eng.plan(*params) == "dp" or params == (0, 0, -1)
         sc, en = eng.score(a, b, *params)
         eng.check_device_errors()
     np.testing.assert_array_equal(sc, rs)

@@ -389,6 +389,45 @@ def test_split_knob_equivalence(oracle_mod):
         np.testing.assert_array_equal(en, re_)
 
 
+@pytest.mark.parametrize("lw", [31, 32, 64, 100, 128, 150, 250])
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_t_truncated_pairs_in_sweep(oracle_mod, lw, split):
+    """Pairs (full-length a, truncated b) are scored inside the uniform sweep (snapshot of block m/32
+    after shift m % 32): every m in 0..lw-1, b cut from a's continuation so that the best end sits at
+    or next to m, in throughput (OVL_SPLIT=0) and latency mode (1), several truncated lanes per
+    wavefront with equal and distinct m % 32."""
+    import os
+    from ovlgraph import OverlapEngine
+    rng = random.Random(lw * 3 + int(split))
+    genome = _rand(rng, 40 * lw)
+    starts = list(range(0, 30 * lw, max(1, lw // 5)))
+    full = [genome[i:i + lw] for i in starts]
+    short = []
+    for m in range(1, lw):
+        st = rng.choice(starts)
+        short.append(genome[st:st + m])                     # prefix of a full read: overlaps end at or near m
+        short.append(_rand(rng, m))                          # unrelated
+    reads = full + short
+    n_full, n = len(full), len(reads)
+    nr = np.random.default_rng(lw)
+    a = nr.integers(0, n_full, 120_000, dtype=np.int32)
+    b = np.where(nr.random(120_000) < 0.3, nr.integers(n_full, n, 120_000), nr.integers(0, n, 120_000)).astype(np.int32)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
+    os.environ["OVL_SPLIT"] = split
+    try:
+        with OverlapEngine(0) as eng:
+            eng.set_reads(reads)
+            assert eng.plan() == "ungapped"
+            sc, en = eng.score(a, b)
+            sc_small, en_small = eng.score(a[:3000], b[:3000])
+    finally:
+        del os.environ["OVL_SPLIT"]
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+    np.testing.assert_array_equal(sc_small, rs[:3000])
+    np.testing.assert_array_equal(en_small, re_[:3000])
+
+
 @pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (2 ** 28, -(2 ** 28), -(2 ** 27))])
 def test_dp_fast_and_classic_agree_with_oracle(oracle_mod, params):
     """Scores-only full DP runs dp_fast_kernel (chunked, unrolled); OVL_DP_CLASSIC=1 forces dp_kernel.
