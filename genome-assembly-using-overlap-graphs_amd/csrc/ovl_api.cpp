@@ -118,7 +118,9 @@ struct Dev {
     int32_t* st_in = nullptr;
     int32_t* st_out = nullptr;
     int64_t st_cap = 0;
-    uint32_t* h_flag = nullptr;  // pinned error-flag readback
+    uint32_t* h_flag = nullptr;      // pinned error flag of host-array calls (the kernels store into it)
+    uint32_t* h_flag_dev = nullptr;  // its device address
+    uint32_t* cur_flag = nullptr;    // the flag the next launches write: err_flag (device calls) or h_flag_dev
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
 };
 
@@ -367,7 +369,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.mismatch = mismatch;
         g.out_score = d_score;
         g.out_end = d_end;
-        g.err_flag = as<uint32_t>(c->err_flag);
+        g.err_flag = c->cur_flag;
         g.planes = c->planes;
         g.wmax = c->wmax;
         g.key64 = pl.key64 ? 1 : 0;
@@ -389,7 +391,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.out_score = d_score;
         g.out_end = d_end;
         g.tb = nullptr;
-        g.err_flag = as<uint32_t>(c->err_flag);
+        g.err_flag = c->cur_flag;
         g.wide = pl.wide ? 1 : 0;
         g.band = pl.kernel == OVL_KERNEL_BANDED ? pl.band : -1;
         g.seed = seed_end;
@@ -566,8 +568,12 @@ hipError_t init_dev(Dev* d) {
     if (e != hipSuccess) return e;
     e = hipHostMalloc((void**)&d->h_flag, 64, hipHostMallocDefault);
     if (e != hipSuccess) return e;
+    *d->h_flag = 0;
+    e = hipHostGetDevicePointer((void**)&d->h_flag_dev, d->h_flag, 0);
+    if (e != hipSuccess) return e;
     e = ensure(d->err_flag, 16);
     if (e != hipSuccess) return e;
+    d->cur_flag = as<uint32_t>(d->err_flag);
     return hipMemset(d->err_flag.p, 0, 16);
 }
 
@@ -791,9 +797,25 @@ void quiesce(std::vector<Job>& jobs) {
     }
 }
 
+// Host-array calls: the kernels flag a bad pair index by storing into the device's pinned host flag, which
+// the host reads after the call's synchronisation (no flag copy behind the results).
+struct HostFlag {
+    std::vector<Job>& jobs;
+    explicit HostFlag(std::vector<Job>& j) : jobs(j) {
+        for (Job& J : jobs) {
+            *(volatile uint32_t*)J.d->h_flag = 0;
+            J.d->cur_flag = J.d->h_flag_dev;
+        }
+    }
+    ~HostFlag() {
+        for (Job& J : jobs) J.d->cur_flag = as<uint32_t>(J.d->err_flag);
+    }
+};
+
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
     int rc = OVL_OK;
+    HostFlag host_flag(jobs);
     for (Job& J : jobs)
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
     int64_t maxch = 0;
@@ -810,15 +832,6 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         for (int64_t k = std::max<int64_t>(0, J.nchunks - (kSlots - 1)); k < J.nchunks; ++k)
             if ((rc = drain_chunk(C, J, k)) != OVL_OK) break;
     }
-    // device error flags (a pair index outside [0, n_reads)) come back behind the results
-    for (Job& J : jobs) {
-        if (rc != OVL_OK || J.nchunks == 0) continue;
-        Dev* d = J.d;
-        if (hipSetDevice(d->device) != hipSuccess ||
-            hipMemcpyAsync(d->h_flag, d->err_flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           C.direct ? d->stream : d->s_out) != hipSuccess)
-            rc = fail(c, OVL_E_HIP, "error-flag readback failed");
-    }
     if (rc != OVL_OK) {
         quiesce(jobs);
         return rc;
@@ -832,9 +845,8 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         Dev* d = J.d;
         if (J.nchunks == 0) continue;
-        if (*d->h_flag) {
-            HIPCHK(c, hipSetDevice(d->device));
-            HIPCHK(c, hipMemset(d->err_flag.p, 0, sizeof(uint32_t)));
+        if (*(volatile uint32_t*)d->h_flag) {
+            *d->h_flag = 0;
             rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
         }
         if (C.timing) {

@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
         for (int32_t j0 = CW; j0 < mmax; j0 += CW) strip(j0, std::false_type{});
         if (live) {
             if (bad) {
-                atomicOr(err_flag, 1u);
+                ovl_flag_error(err_flag);
                 out_score[p] = -1;
                 out_end[p] = -1;
             } else {
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
         }
         if (live) {
             if (bad) {
-                atomicOr(err_flag, 1u);
+                ovl_flag_error(err_flag);
                 out_score[p] = -1;
                 out_end[p] = -1;
             } else {

@@ -3,6 +3,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Scoring kernels flag a pair index outside [0, n_reads): a relaxed system-scope store of 1 (idempotent,
+// so no read-modify-write), because for host-array calls the flag is pinned host memory that the host
+// reads after the call's synchronisation.
+__device__ __forceinline__ void ovl_flag_error(uint32_t* flag) {
+    __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct OvlUngappedArgs {
     const uint32_t* sfx;
     const uint32_t* pfx;

@@ -559,7 +559,7 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
     if (!ok) { a = 0; b = 0; }
     int32_t n = len[a], m = len[b];
     ok = ok && n <= 32 * W && m <= 32 * W;
-    if (mine && !ok && r0 == 0) atomicOr(err_flag, 1u);
+    if (mine && !ok && r0 == 0) ovl_flag_error(err_flag);
     uint32_t Sw[SROW], Tw[TROW];
     load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
     load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
             OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
             if (mine && !ok) {
-                atomicOr(err_flag, 1u);
+                ovl_flag_error(err_flag);
                 out_score[p] = -1;
                 out_end[p] = -1;
             }
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             tmask |= 1u << (__builtin_amdgcn_readlane(mb, (int)__builtin_ctzll(bm)) & 31);
         OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
         if constexpr (!LAT) {
-            if (mine && !ok) atomicOr(err_flag, 1u);
+            if (mine && !ok) ovl_flag_error(err_flag);
             const bool push = ok && !uni && !tt;
             const uint64_t pm = __ballot(push);
             if (push)
@@ -852,7 +852,7 @@ __global__ __launch_bounds__(64) void dp_kernel(
         const int32_t b = b_idx[pair];
         if (a < 0 || a >= n_reads || b < 0 || b >= n_reads || len[b] > mcap) {
             if (lane == 0) {
-                atomicOr(err_flag, 1u);
+                ovl_flag_error(err_flag);
                 out_score[pair] = -1;
                 out_end[pair] = -1;
             }
@@ -982,7 +982,7 @@ __global__ __launch_bounds__(64) void dp_fast_kernel(
         const int32_t b = b_idx[pair];
         if (a < 0 || a >= n_reads || b < 0 || b >= n_reads || len[b] > mcap) {
             if (lane == 0) {
-                atomicOr(err_flag, 1u);
+                ovl_flag_error(err_flag);
                 out_score[pair] = -1;
                 out_end[pair] = -1;
             }
@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(256) void band_row_kernel(
         const int32_t n = ok ? len[a] : 0, m = ok ? len[b] : 0;
         ok = ok && n <= lcap && m <= lcap;
         if (mine && !ok && t0 == 0) {
-            atomicOr(err_flag, 1u);
+            ovl_flag_error(err_flag);
             out_score[p] = -1;
             out_end[p] = -1;
         }
@@ -1569,7 +1569,7 @@ __global__ __launch_bounds__(64, (D <= 4 ? 8 : 6)) void band_diag_kernel(
                 key = kx > key ? kx : key;
             }
             if (bad) {
-                atomicOr(err_flag, 1u);
+                ovl_flag_error(err_flag);
                 out_score[pair] = -1;
                 out_end[pair] = -1;
             } else {

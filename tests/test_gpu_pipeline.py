@@ -130,6 +130,15 @@ def test_pipeline_index_error_then_recovery(engine, cfg2, cfg2_ref):
     sc, en = engine.score(a, b)  # the flag was consumed: the next call is clean
     np.testing.assert_array_equal(sc, cfg2_ref[0])
     np.testing.assert_array_equal(en, cfg2_ref[1])
+    # the kernels store the flag into pinned host memory: pageable outputs (staged copies), the gapped
+    # lane kernel and the band knob report it the same way, and a clean call follows each
+    pageable = (np.empty(len(a), np.int32), np.empty(len(a), np.int32))
+    for args in ((10, -1, -(2 ** 31), -1), (10, -1, -2, -1), (10, -1, -2, 8)):
+        with pytest.raises(OvlError, match="OVL_E_INDEX"):
+            engine.score(a, bad, *args, out=pageable)
+        sc, en = engine.score(a, b, *args, out=pageable)
+        assert sc[len(bad) // 2] >= 0
+    engine.check_device_errors()  # the device API's own flag never saw these
 
 
 def test_pipeline_timing(engine, cfg2):
