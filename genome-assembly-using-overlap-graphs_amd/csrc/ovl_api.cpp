@@ -13,14 +13,20 @@
 // else a DP kernel.  Never falls back to the CPU.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <initializer_list>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ovl.h"
@@ -57,7 +63,8 @@ struct Knobs {
     int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
                                   // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic)
-    int32_t pipe_direct = 1;      // OVL_PIPE_DIRECT=0: pinned outputs through D2H copies instead of kernel stores
+    int32_t pipe_direct = 1;      // OVL_PIPE_DIRECT=0: copy-engine H2D / D2H transfers instead of kernels reading
+                                  // and storing host memory through its device mapping (A/B knob)
 };
 
 }  // namespace
@@ -117,6 +124,8 @@ struct Dev {
     hipEvent_t ev_h2d[kSlots] = {}, ev_in[kSlots] = {}, ev_k[kSlots] = {}, ev_out[kSlots] = {};
     int32_t* st_in = nullptr;
     int32_t* st_out = nullptr;
+    int32_t* st_in_dev = nullptr;   // device addresses of the staging rings (kernels read / store them)
+    int32_t* st_out_dev = nullptr;
     int64_t st_cap = 0;
     uint32_t* h_flag = nullptr;      // pinned error flag of host-array calls (the kernels store into it)
     uint32_t* h_flag_dev = nullptr;  // its device address
@@ -518,6 +527,76 @@ Knobs read_knobs() {
     return k;
 }
 
+// Host copies between pageable caller arrays and the pinned staging rings, split over a few worker threads
+// (one thread copies ~10 GB/s; a 16 MB result column is ~1.5 ms alone).  The pool is created on first
+// use in each process (a forked joblib worker builds its own) and sized by OVL_HOST_THREADS (default:
+// min(8, hardware threads)).
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static CopyPool* pool = nullptr;
+        static std::mutex mu;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!pool || pool->pid_ != getpid()) pool = new CopyPool();  // a forked child starts a fresh pool
+        return *pool;
+    }
+    // dst[i] = src[i] for [0, bytes), on the workers and the calling thread
+    void copy(void* dst, const void* src, size_t bytes) {
+        const size_t parts = std::min<size_t>(workers_.size() + 1, bytes / kMinPart);
+        if (parts <= 1) {
+            memcpy(dst, src, bytes);
+            return;
+        }
+        const size_t step = (bytes / parts + 63) & ~size_t(63);
+        std::lock_guard<std::mutex> one_call(call_mu_);  // calls from several host threads take turns
+        std::unique_lock<std::mutex> lk(mu_);
+        pending_ = 0;
+        for (size_t i = 1; i < parts; ++i) {
+            const size_t lo = i * step, hi = std::min(bytes, lo + step);
+            if (lo >= hi) break;
+            tasks_.push_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, hi - lo); });
+            ++pending_;
+        }
+        lk.unlock();
+        cv_.notify_all();
+        memcpy(dst, src, std::min(step, bytes));
+        lk.lock();
+        done_.wait(lk, [&] { return pending_ == 0; });
+    }
+
+  private:
+    static constexpr size_t kMinPart = size_t(1) << 19;
+    CopyPool() : pid_(getpid()) {
+        int n = (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char* e = getenv("OVL_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
+        for (int i = 0; i + 1 < n; ++i) {
+            std::thread t([this] { run(); });
+            t.detach();  // lives with the process; never joined at exit
+            workers_.push_back(0);
+        }
+    }
+    void run() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return !tasks_.empty(); });
+            auto f = std::move(tasks_.back());
+            tasks_.pop_back();
+            lk.unlock();
+            f();
+            lk.lock();
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    pid_t pid_;
+    std::vector<int> workers_;
+    std::vector<std::function<void()>> tasks_;
+    size_t pending_ = 0;
+    std::mutex mu_, call_mu_;
+    std::condition_variable cv_, done_;
+};
+
+void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
+
 void free_staging(int32_t*& p) {
     if (p) (void)hipHostFree(p);
     p = nullptr;
@@ -632,15 +711,19 @@ bool host_pinned(const void* p, size_t bytes) {
 // Pairs per pipeline chunk.  Measured on MI355X (tools/pipe_ab.py, profiles/r02_pipe_ab_*.json): every
 // chunk's D2H copy costs ~0.1 ms of fixed overhead, which is more than the kernel time a chunk hides, so
 // copies of pinned arrays run as one chunk; only pageable arrays, which go through pinned staging slots,
-// are cut into 4 M-pair chunks (the slot size).  Direct kernel stores need no chunks at all.
-int64_t pick_chunk(const Dev* d, int64_t n, bool staged) {
+// are cut into chunks (the slot size): 4 M pairs with copy-engine transfers, 512 K pairs when the kernels
+// read and store the staging slots themselves (the host copy of chunk k+1 overlaps the kernel of chunk k).
+// Direct kernel stores into pinned arrays need no chunks at all.
+int64_t pick_chunk(const Dev* d, int64_t n, bool staged, bool direct) {
     if (d->k.pipe_chunk > 0) return d->k.pipe_chunk;
-    const int64_t cap = int64_t(1) << 22;
+    const int64_t cap = int64_t(1) << (direct ? 19 : 22);
     return std::max<int64_t>(1, staged ? std::min(n, cap) : n);
 }
 
-hipError_t alloc_staging(int32_t*& p, int64_t cap) {
-    return hipHostMalloc((void**)&p, (size_t)kSlots * 2 * (size_t)cap * sizeof(int32_t), hipHostMallocDefault);
+hipError_t alloc_staging(int32_t*& p, int32_t*& p_dev, int64_t cap) {
+    hipError_t e = hipHostMalloc((void**)&p, (size_t)kSlots * 2 * (size_t)cap * sizeof(int32_t), hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    return hipHostGetDevicePointer((void**)&p_dev, p, 0);
 }
 
 struct Call {
@@ -654,7 +737,8 @@ struct Call {
     int32_t* out_e = nullptr;
     int64_t out_base = 0;
     bool out_pinned = false;
-    bool direct = false;           // kernels store results straight into the pinned host arrays
+    bool direct = false;           // kernels read host pair lists and store results through host mappings
+                                   // (the caller's pinned arrays, or pinned staging slots for pageable ones)
     bool timing = false;
 };
 
@@ -667,6 +751,8 @@ struct Job {
     const int32_t* dev_b = nullptr;
     int32_t* ka = nullptr;  // device copies of the host list (local indexing)
     int32_t* kb = nullptr;
+    const int32_t* za = nullptr;  // direct: device addresses of the caller's pinned pair arrays (local indexing)
+    const int32_t* zb = nullptr;
     int32_t* d_score = nullptr;  // device results (local indexing)
     int32_t* d_end = nullptr;
 };
@@ -676,18 +762,26 @@ int setup_job(const Call& C, Job& J) {
     const int64_t n = J.hi - J.lo;
     if (n <= 0) return OVL_OK;
     HIPCHK(d, hipSetDevice(d->device));
-    // direct stores from a resident list need no pipeline: one launch per device
-    const bool staged = (C.h_a && !C.in_pinned) || !C.out_pinned;
-    J.chunk = (C.direct && !C.h_a) ? n : pick_chunk(d, n, staged);
+    const bool need_in = C.h_a && !C.in_pinned, need_out = !C.out_pinned;
+    J.chunk = pick_chunk(d, n, need_in || need_out, C.direct);
     J.nchunks = (n + J.chunk - 1) / J.chunk;
     const size_t bytes = sizeof(int32_t) * (size_t)n;
-    if (C.h_a) {
+    if (C.h_a && !C.direct) {
         HIPCHK(d, ensure(d->a, bytes));
         HIPCHK(d, ensure(d->b, bytes));
         J.ka = as<int32_t>(d->a);
         J.kb = as<int32_t>(d->b);
     }
-    if (C.direct) {
+    if (C.h_a && C.direct && C.in_pinned) {
+        // the kernels read this device's slice of the caller's pinned pair arrays in place
+        void* pa = nullptr;
+        void* pb = nullptr;
+        HIPCHK(d, hipHostGetDevicePointer(&pa, const_cast<int32_t*>(C.h_a + J.lo), 0));
+        HIPCHK(d, hipHostGetDevicePointer(&pb, const_cast<int32_t*>(C.h_b + J.lo), 0));
+        J.za = reinterpret_cast<const int32_t*>(pa);
+        J.zb = reinterpret_cast<const int32_t*>(pb);
+    }
+    if (C.direct && C.out_pinned) {
         // the device's address of this slice of the caller's pinned arrays
         void* ps = nullptr;
         void* pe = nullptr;
@@ -695,21 +789,20 @@ int setup_job(const Call& C, Job& J) {
         HIPCHK(d, hipHostGetDevicePointer(&pe, C.out_e + (J.lo - C.out_base), 0));
         J.d_score = reinterpret_cast<int32_t*>(ps);
         J.d_end = reinterpret_cast<int32_t*>(pe);
-    } else {
+    } else if (!C.direct) {
         HIPCHK(d, ensure(d->score, bytes));
         HIPCHK(d, ensure(d->end, bytes));
         J.d_score = as<int32_t>(d->score);
         J.d_end = as<int32_t>(d->end);
     }
     // pinned staging rings for pageable caller arrays, both allocated with capacity d->st_cap
-    const bool need_in = C.h_a && !C.in_pinned, need_out = !C.out_pinned;
     if ((need_in || need_out) && J.chunk > d->st_cap) {
         free_staging(d->st_in);
         free_staging(d->st_out);
         d->st_cap = J.chunk;
     }
-    if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_cap));
-    if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_cap));
+    if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
+    if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
     if (C.timing && (int64_t)d->t_ev.size() < 2 * J.nchunks) {
         while ((int64_t)d->t_ev.size() < 2 * J.nchunks) {
             hipEvent_t ev;
@@ -720,7 +813,48 @@ int setup_job(const Call& C, Job& J) {
     return OVL_OK;
 }
 
+// Direct mode: the kernels read the pair list and store the results through host mappings (no copy-engine
+// transfers); pageable arrays are copied into / out of the pinned staging slots on the host.
+int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
+    Dev* d = J.d;
+    HIPCHK(d, hipSetDevice(d->device));
+    const int64_t off = k * J.chunk;
+    const int64_t g = J.lo + off;
+    const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
+    const size_t nb = sizeof(int32_t) * (size_t)n;
+    const int slot = (int)(k % kSlots);
+    const size_t so = (size_t)slot * 2 * (size_t)d->st_cap;
+    const bool staged_in = C.h_a && !C.in_pinned;
+    // the slot's previous user, chunk k - kSlots, must be done (its staged results were drained already)
+    if (staged_in && k >= kSlots && C.out_pinned) HIPCHK(d, hipEventSynchronize(d->ev_k[slot]));
+    const int32_t* ka;
+    const int32_t* kb;
+    if (C.h_a) {
+        if (staged_in) {
+            host_copy(d->st_in + so, C.h_a + g, nb);
+            host_copy(d->st_in + so + d->st_cap, C.h_b + g, nb);
+            ka = d->st_in_dev + so;
+            kb = d->st_in_dev + so + d->st_cap;
+        } else {
+            ka = J.za + off;
+            kb = J.zb + off;
+        }
+    } else {
+        ka = J.dev_a + g;
+        kb = J.dev_b + g;
+    }
+    int32_t* os = C.out_pinned ? J.d_score + off : d->st_out_dev + so;
+    int32_t* oe = C.out_pinned ? J.d_end + off : d->st_out_dev + so + d->st_cap;
+    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
+    int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
+    if (rc != OVL_OK) return rc;
+    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
+    if (staged_in || !C.out_pinned) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
+    return OVL_OK;
+}
+
 int issue_chunk(const Call& C, Job& J, int64_t k) {
+    if (C.direct) return issue_chunk_direct(C, J, k);
     Dev* d = J.d;
     HIPCHK(d, hipSetDevice(d->device));
     const int64_t off = k * J.chunk;
@@ -737,8 +871,8 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
             // the slot's previous H2D (chunk k - kSlots) must have read it
             if (k >= kSlots) HIPCHK(d, hipEventSynchronize(d->ev_in[slot]));
             int32_t* st = d->st_in + (size_t)slot * 2 * (size_t)d->st_cap;
-            memcpy(st, sa, nb);
-            memcpy(st + d->st_cap, sb, nb);
+            host_copy(st, sa, nb);
+            host_copy(st + d->st_cap, sb, nb);
             sa = st;
             sb = st + d->st_cap;
         }
@@ -758,7 +892,6 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
                           d->stream);
     if (rc != OVL_OK) return rc;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
-    if (C.direct) return OVL_OK;  // the kernel stored the results in the caller's arrays
     HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
     HIPCHK(d, hipStreamWaitEvent(d->s_out, d->ev_k[slot], 0));
     int32_t* ds;
@@ -776,17 +909,18 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     return OVL_OK;
 }
 
-// Pageable outputs: copy chunk k out of its staging slot once its D2H is done.
+// Pageable outputs: copy chunk k out of its staging slot once its results are there (the D2H copy, or in
+// direct mode the kernel that stored them).
 int drain_chunk(const Call& C, Job& J, int64_t k) {
     Dev* d = J.d;
     const int64_t off = k * J.chunk;
     const int64_t g = J.lo + off;
     const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
     const int slot = (int)(k % kSlots);
-    HIPCHK(d, hipEventSynchronize(d->ev_out[slot]));
+    HIPCHK(d, hipEventSynchronize(C.direct ? d->ev_k[slot] : d->ev_out[slot]));
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
-    memcpy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);
-    memcpy(C.out_e + (g - C.out_base), ss + d->st_cap, sizeof(int32_t) * (size_t)n);
+    host_copy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);
+    host_copy(C.out_e + (g - C.out_base), ss + d->st_cap, sizeof(int32_t) * (size_t)n);
     return OVL_OK;
 }
 
@@ -1230,7 +1364,7 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.out_e = out_end;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = c->timing != 0;
-    C.direct = C.out_pinned && c->devs[0]->k.pipe_direct;
+    C.direct = c->devs[0]->k.pipe_direct != 0;
     const int32_t S = (int32_t)c->devs.size();
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);
@@ -1464,7 +1598,7 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.out_base = lo;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = ctx->timing != 0;
-    C.direct = C.out_pinned && ctx->devs[0]->k.pipe_direct;
+    C.direct = ctx->devs[0]->k.pipe_direct != 0;
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);
