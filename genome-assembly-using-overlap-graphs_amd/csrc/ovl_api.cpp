@@ -130,6 +130,7 @@ struct Dev {
     uint32_t* h_flag = nullptr;      // pinned error flag of host-array calls (the kernels store into it)
     uint32_t* h_flag_dev = nullptr;  // its device address
     uint32_t* cur_flag = nullptr;    // the flag the next launches write: err_flag (device calls) or h_flag_dev
+    bool host_out = false;           // the next launches' outputs are host-mapped (direct host-array calls)
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
 };
 
@@ -345,8 +346,11 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         seed.kernel = pl.seed_kernel;
         seed.key64 = pl.seed_key64;
         seed.wide = pl.seed_wide;
+        const bool host_out = c->host_out;
+        c->host_out = false;  // the seeds stay in HBM
         int rc = launch_score_chunk(c, seed, d_a, d_b, n_pairs, match, mismatch, INT32_MIN, as<int32_t>(c->seed_s),
                                     as<int32_t>(c->seed_e), s);
+        c->host_out = host_out;
         if (rc != OVL_OK) return rc;
         seed_end = as<int32_t>(c->seed_e);
     }
@@ -383,6 +387,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.wmax = c->wmax;
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
+        g.host_out = c->host_out ? 1 : 0;
         HIPCHK(c, ovl_launch_ungapped(&g, s));
     } else {
         OvlDpArgs g{};
@@ -935,21 +940,25 @@ void quiesce(std::vector<Job>& jobs) {
 // the host reads after the call's synchronisation (no flag copy behind the results).
 struct HostFlag {
     std::vector<Job>& jobs;
-    explicit HostFlag(std::vector<Job>& j) : jobs(j) {
+    HostFlag(std::vector<Job>& j, bool host_out) : jobs(j) {
         for (Job& J : jobs) {
             *(volatile uint32_t*)J.d->h_flag = 0;
             J.d->cur_flag = J.d->h_flag_dev;
+            J.d->host_out = host_out;
         }
     }
     ~HostFlag() {
-        for (Job& J : jobs) J.d->cur_flag = as<uint32_t>(J.d->err_flag);
+        for (Job& J : jobs) {
+            J.d->cur_flag = as<uint32_t>(J.d->err_flag);
+            J.d->host_out = false;
+        }
     }
 };
 
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
     int rc = OVL_OK;
-    HostFlag host_flag(jobs);
+    HostFlag host_flag(jobs, C.direct);
     for (Job& J : jobs)
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
     int64_t maxch = 0;

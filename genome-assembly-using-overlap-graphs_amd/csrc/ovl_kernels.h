@@ -30,6 +30,7 @@ struct OvlUngappedArgs {
     int32_t lw;          // dominant read length for uniform_kernel (0: general kernel only)
     const uint32_t* full; // bit r set iff len[r] == lw
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
+    int32_t host_out;    // out_score / out_end are host-mapped (uniform_kernel<..., HOUT>: non-temporal stores)
 };
 
 // kernels of the band knob (ovl_launch_dp); OVL_BAND_FORM env picks one for tests

@@ -53,6 +53,14 @@ __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t 
     return __builtin_amdgcn_alignbit(hi, lo, r);
 }
 
+// A result store: results that leave the GPU (host-mapped output arrays) go out as non-temporal stores, so
+// they stream to the link without allocating in L2; device outputs are plain stores.
+template <bool HOUT>
+__device__ __forceinline__ void put_result(int32_t* p, int32_t v) {
+    if constexpr (HOUT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
 // would otherwise sum a block's word counts with an extra v_add3)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t v, uint32_t acc) {
@@ -546,7 +554,7 @@ __device__ __forceinline__ typename Key<KM>::T general_core(bool ok, int32_t n, 
     return group_max(best, 64 >> rs_log2);
 }
 
-template <int P, int W, int KM>
+template <int P, int W, int KM, bool HOUT = false>
 __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, int32_t b,
                                              const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx,
                                              const int32_t* __restrict__ len, int32_t n_reads, int r0,
@@ -567,8 +575,8 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
     if (mine && r0 == 0) {
         int32_t sc, en;
         Key<KM>::decode(full, sc, en);
-        out_score[p] = ok ? sc : -1;
-        out_end[p] = ok ? en : -1;
+        put_result<HOUT>(out_score + p, ok ? sc : -1);
+        put_result<HOUT>(out_end + p, ok ? en : -1);
     }
 }
 
@@ -589,7 +597,7 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
 // most that fits without spilling
 #define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : 4))) \
                                   : ((W) <= 4 ? 7 : ((W) <= 5 ? 6 : ((W) <= 6 ? 5 : 4))))
-template <int W, int KM, bool LAT>
+template <int W, int KM, bool LAT, bool HOUT>
 __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
@@ -627,8 +635,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         const bool mine = slot < count;
         int4 e = make_int4(0, 0, 0, 0);
         if (mine) e = ring[(head + slot) & (RING - 1)];
-        general_unit<P, W, KM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
-                               mismatch, out_score, out_end, err_flag);
+        general_unit<P, W, KM, HOUT>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
+                                     mismatch, out_score, out_end, err_flag);
         head += count;
     };
 #ifdef OVL_TRACE
@@ -659,8 +667,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
             if (mine && !ok) {
                 ovl_flag_error(err_flag);
-                out_score[p] = -1;
-                out_end[p] = -1;
+                put_result<HOUT>(out_score + p, -1);
+                put_result<HOUT>(out_end + p, -1);
             }
             // (n = lw, m <= lw) pairs are the sweeping wave's: uniform and (TT) t-truncated alike
             const bool push = ok && (TT ? n != lw : !(n == lw && m == lw));
@@ -707,8 +715,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
                 if (own && r0 == 0) {
                     int32_t sc, e2;
                     Key<KM>::decode(full, sc, e2);
-                    out_score[en.x] = sc;
-                    out_end[en.x] = e2;
+                    put_result<HOUT>(out_score + en.x, sc);
+                    put_result<HOUT>(out_end + en.x, e2);
                 }
             }
             __builtin_amdgcn_s_setprio(0);
@@ -749,8 +757,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
-            out_score[p] = ok ? sc : -1;
-            out_end[p] = ok ? en : -1;
+            put_result<HOUT>(out_score + p, ok ? sc : -1);
+            put_result<HOUT>(out_end + p, ok ? en : -1);
         }
         OVL_TR_CLOCK(4, (uint32_t)best);
 #ifndef OVL_ABLATE_DRAIN
@@ -1285,16 +1293,23 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
     return hipGetLastError();
 }
 
-template <int W, int KM>
-static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    if (g.rs_log2 > 0)  // latency mode: two wavefronts per tile
-        uniform_kernel<W, KM, true><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
+template <int W, int KM, bool LAT, bool HOUT>
+static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    uniform_kernel<W, KM, LAT, HOUT><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
                                                                 g.n_pairs, g.lw, g.full, g.match, g.mismatch,
                                                                 g.out_score, g.out_end, g.err_flag);
-    else
-        uniform_kernel<W, KM, false><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
-                                                                 g.n_pairs, g.lw, g.full, g.match, g.mismatch,
-                                                                 g.out_score, g.out_end, g.err_flag);
+}
+
+template <int W, int KM>
+static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    // latency mode (two wavefronts per tile) when rs_log2 > 0; host-mapped outputs stream out non-temporally
+    if (g.rs_log2 > 0) {
+        if (g.host_out) launch_uniform_4<W, KM, true, true>(g, blocks, stream);
+        else launch_uniform_4<W, KM, true, false>(g, blocks, stream);
+    } else {
+        if (g.host_out) launch_uniform_4<W, KM, false, true>(g, blocks, stream);
+        else launch_uniform_4<W, KM, false, false>(g, blocks, stream);
+    }
 }
 
 template <int P, int W, int KM>

@@ -1,25 +1,25 @@
 #!/bin/bash
-# round 2 profiles of the default bench command's workload (target point): GPU tests, kernel trace + stats,
-# FETCH_SIZE / WRITE_SIZE passes (separate runs), and the processes left after bench exits.
+# Round-2 profiles of the default bench workload (target point), the headline command without extras:
+#   kernel trace + stats (the step's uniform_kernel<4, 0, false, true> storing to host memory, and the
+#   kernel-only uniform_kernel<4, 0, false, false> that roofline.kernel_ms times), then PMC passes over the
+#   kernel-only variant, each in its own run: FETCH_SIZE, WRITE_SIZE, SQ instruction counts, occupancy, LDS.
+# usage: bash tools/gpu_r02_profile.sh [config] [tag]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-OUT="$GRAFT_REPO_ROOT/gpurun_out/r02prof"
+CFG=${1:-target}
+TAG=${2:-r02prof}
+OUT="$GRAFT_REPO_ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B="$GRAFT_REPO_ROOT/bench.py"
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 \
-  || { echo "gpu tests failed"; tail -40 "$OUT/gpu_tests.log"; exit 1; }
-tail -1 "$OUT/gpu_tests.log"
+ARGS="--config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-extra"
 echo "== kernel trace + stats"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d "$OUT/kt" -o kt --output-format csv -- python3 "$B" --steps 20 --warmup 5 --no-cpu-baseline --no-extra > "$OUT/kt.log" 2>&1 || { echo "kt failed"; tail -20 "$OUT/kt.log"; exit 1; }
-KT=$(find "$OUT/kt" -name "kt_kernel_trace.csv" | head -1)
-python3 tools/kt_phases.py "$KT" uniform_kernel 5 20 "$OUT/phases.json"
-echo "== pmc FETCH_SIZE"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --kernel-include-regex uniform_kernel -d "$OUT/fetch" -o fetch --output-format csv -- python3 "$B" --steps 20 --warmup 5 --no-cpu-baseline --no-extra > "$OUT/fetch.log" 2>&1 || { echo "fetch failed"; tail -20 "$OUT/fetch.log"; exit 1; }
-echo "== pmc WRITE_SIZE"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --kernel-include-regex uniform_kernel -d "$OUT/write" -o write --output-format csv -- python3 "$B" --steps 20 --warmup 5 --no-cpu-baseline --no-extra > "$OUT/write.log" 2>&1 || { echo "write failed"; tail -20 "$OUT/write.log"; exit 1; }
-echo "== processes after bench"
-timeout -k 10 300 python3 "$B" --steps 20 --warmup 5 --no-extra --cpu-budget 2 > "$OUT/bench_ps.json" 2>&1; echo "bench rc=$?"
-sleep 1
-ps -u "$(id -u)" -o pid,ppid,stat,etime,cmd > "$OUT/ps_after.txt"; cat "$OUT/ps_after.txt"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 "$B" $ARGS > "$OUT/kt.log" 2>&1 || { echo "kt failed"; tail -20 "$OUT/kt.log"; exit 1; }
+KRE="uniform_kernel<[0-9], 0, false, false>"
+i=0
+for CTRS in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+  i=$((i+1))
+  echo "== pmc pass $i: $CTRS"
+  timeout -k 10 -s KILL 240 rocprofv3 --pmc $CTRS --kernel-trace --kernel-include-regex "$KRE" -d "$OUT/p$i" -o p$i --output-format csv -- python3 "$B" $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -20 "$OUT/p$i.log"; exit 1; }
+done
 echo done
