@@ -666,10 +666,15 @@ int create_on(const int32_t* ids, int32_t n, ovl_ctx** out) {
     HIPCHK((ovl_ctx*)nullptr, hipGetDeviceCount(&count));
     if (count <= 0) return fail((ovl_ctx*)nullptr, OVL_E_HIP, "no HIP device visible");
     if (n <= 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "no devices requested");
+    // OVL_SHARE_DEVICES=1 (tests on a one-GPU box): a device may be listed more than once; each entry is
+    // an independent shard slot (own streams, buffers, staging and flag) on that GPU, so the N-device
+    // sharding, per-device jobs and slice copies run for real
+    const char* share = getenv("OVL_SHARE_DEVICES");
+    const bool allow_dup = share && atoi(share) == 1;
     for (int32_t i = 0; i < n; ++i) {
         if (ids[i] < 0 || ids[i] >= count)
             return fail((ovl_ctx*)nullptr, OVL_E_ARG, "device %d outside [0, %d)", ids[i], count);
-        for (int32_t j = 0; j < i; ++j)
+        for (int32_t j = 0; j < i && !allow_dup; ++j)
             if (ids[j] == ids[i]) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "device %d listed twice", ids[i]);
     }
     DeviceGuard guard;

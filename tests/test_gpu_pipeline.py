@@ -198,6 +198,52 @@ def test_multi_device_context(oracle_mod, cfg2, cfg2_ref):
     assert L.ovl_create(n_dev + 1, ctypes.byref(ctx)) == -1
 
 
+@pytest.mark.parametrize("slots", [2, 3])
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_multi_device_sharding_on_shared_gpu(oracle_mod, cfg2, cfg2_ref, slots, direct):
+    """N-device contexts with every slot on GPU 0 (OVL_SHARE_DEVICES=1): the Σ n·m shards of host and
+    device lists, per-device kernels and their slices of pinned / pageable results, the gapped and banded
+    kernels, with kernels storing through host mappings (direct) and through copy-engine transfers."""
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = cfg2
+    eng = _engine_env({"OVL_SHARE_DEVICES": "1", "OVL_PIPE_DIRECT": direct, "OVL_PIPE_CHUNK": "20000"},
+                      devices=[0] * slots)
+    try:
+        assert eng.devices == [0] * slots
+        eng.set_reads(reads)
+        n = a.shape[0]
+        sc, en = eng.score(a, b)
+        np.testing.assert_array_equal(sc, cfg2_ref[0])
+        np.testing.assert_array_equal(en, cfg2_ref[1])
+        out = (np.full(n, 7, np.int32), np.full(n, 7, np.int32))
+        pa, pb = pinned_empty(n), pinned_empty(n)
+        pa[:], pb[:] = a, b
+        eng.score(pa, pb, out=out)
+        np.testing.assert_array_equal(out[0], cfg2_ref[0])
+        np.testing.assert_array_equal(out[1], cfg2_ref[1])
+        assert eng.enumerate_candidates(5) == n
+        cs, ce = eng.score_candidates()
+        np.testing.assert_array_equal(cs, cfg2_ref[0])
+        np.testing.assert_array_equal(ce, cfg2_ref[1])
+        cs, ce = eng.score_candidates_range(1000, n - 777, out=(out[0][:n - 1777], out[1][:n - 1777]))
+        np.testing.assert_array_equal(cs, cfg2_ref[0][1000:n - 777])
+        for args, ref in (((10, -1, -2), oracle_mod.batch_dp), ((10, -1, -2, 8), oracle_mod.batch_banded)):
+            idx = np.arange(0, n, 7)
+            sc, en = eng.score(a[idx], b[idx], *args)
+            rs, re_ = ref(reads, a[idx], b[idx], *args)
+            np.testing.assert_array_equal(sc, rs)
+            np.testing.assert_array_equal(en, re_)
+        bad = b.copy()
+        bad[-3] = len(reads)  # in the last shard
+        from ovlgraph import OvlError
+        with pytest.raises(OvlError, match="OVL_E_INDEX"):
+            eng.score(a, bad)
+        sc, en = eng.score(a, b)
+        np.testing.assert_array_equal(sc, cfg2_ref[0])
+    finally:
+        eng.close()
+
+
 def test_device_shard_bounds_and_ranges(engine, cfg2, cfg2_ref):
     from ovlgraph.sharded import pair_costs, shard_bounds
     reads, a, b = cfg2
