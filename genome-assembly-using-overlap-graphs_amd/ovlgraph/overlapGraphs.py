@@ -115,7 +115,7 @@ def candidates_and_scores(distinct: Sequence[str], k: int, engine: Optional[Over
 
 
 def assemble_graph_direct(distinct: Sequence[str], counts: Sequence[int], a, b, score, end,
-                          min_score: Optional[int] = None) -> nx.DiGraph:
+                          min_score: Optional[int] = None, native: Optional[bool] = None) -> nx.DiGraph:
     """``assemble_graph`` without networkx's per-edge ``add_edge`` overhead.
 
     Builds the DiGraph's own node / successor / predecessor dicts in bulk, in the
@@ -127,19 +127,56 @@ def assemble_graph_direct(distinct: Sequence[str], counts: Sequence[int], a, b, 
     * pairs x copies are expanded into edge arrays (u, v node ids) with numpy;
     * successor dicts: edges stably sorted by u keep the global order per u;
     * predecessor dicts: edges stably sorted by v keep the global order per v.
+
+    The dicts are built by the C extension (csrc/ovl_digraph.c) in one pass over the edges when it is
+    built (``native=None``: when available; True: required; False: the Python grouping below).
     """
     # millions of new dicts: the cyclic GC would re-traverse them at every generation-2 pass
     # (they hold no cycles), so it is paused for the bulk build
     gc_was = gc.isenabled()
     gc.disable()
     try:
-        return _assemble_direct(distinct, counts, a, b, score, end, min_score)
+        return _assemble_direct(distinct, counts, a, b, score, end, min_score, native)
     finally:
         if gc_was:
             gc.enable()
 
 
-def _assemble_direct(distinct, counts, a, b, score, end, min_score):
+_digraph_mod = None
+
+
+def _digraph():
+    """The C builder of the adjacency dicts (build/_digraph*.so, csrc/ovl_digraph.c), or None if not built."""
+    global _digraph_mod
+    if _digraph_mod is None:
+        import importlib.machinery
+        import importlib.util
+        import os
+        import sysconfig
+        from ._lib import PKG_ROOT
+        path = os.path.join(PKG_ROOT, "build", "_digraph" + sysconfig.get_config_var("EXT_SUFFIX"))
+        _digraph_mod = False
+        if os.path.exists(path):
+            spec = importlib.util.spec_from_file_location("ovlgraph._digraph", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            _digraph_mod = mod
+    return _digraph_mod or None
+
+
+class _EdgeAttrs:
+    """Its instances' ``__dict__`` is a key-sharing dict (PEP 412) with the two edge attributes; the C builder
+    copies it, so every edge's attribute dict shares one key table (values only per edge)."""
+
+
+def _attr_template() -> dict:
+    t = _EdgeAttrs()
+    t.weight = None
+    t.end_position = None
+    return t.__dict__
+
+
+def _assemble_direct(distinct, counts, a, b, score, end, min_score, native: Optional[bool] = None):
     names = _node_names(distinct, counts)
     order = [n for group in names for n in group]
     cnt = np.fromiter((len(g) for g in names), dtype=np.int64, count=len(names))
@@ -163,6 +200,20 @@ def _assemble_direct(distinct, counts, a, b, score, end, min_score):
     cb = cnt[b_arr][pid]
     u = first[a_arr][pid] + k // cb
     v = first[b_arr][pid] + k % cb
+    mod = _digraph() if native is not False else None
+    if native and mod is None:
+        raise RuntimeError("ovlgraph._digraph is not built (make -C genome-assembly-using-overlap-graphs_amd/csrc)")
+    if mod is not None:
+        # one pass in C over the edges in insertion order: the same dicts as the grouped build below
+        G = nx.DiGraph()
+        node, succ, pred = mod.build(order, np.ascontiguousarray(u, np.int64), np.ascontiguousarray(v, np.int64),
+                                     np.ascontiguousarray(s_arr[pid], np.int32),
+                                     np.ascontiguousarray(e_arr[pid], np.int32), _attr_template())
+        G._node = node
+        G._succ = succ
+        G._pred = pred
+        nx._clear_cache(G)
+        return G
     dicts = [{"weight": sc, "end_position": en}
              for sc, en in zip(s_arr[pid].tolist(), e_arr[pid].tolist())]
     n_nodes = len(order)

@@ -7,6 +7,8 @@ order, copies and attribute types against the reference's golden graphs.
 import contextlib
 import io
 
+import pytest
+
 from conftest import assert_graph_matches_record
 from ovlgraph import overlapGraphs as og
 
@@ -71,17 +73,40 @@ def _scored_case(seed, n_reads=300, alphabet="ACG", k=2):
     return d, c, a, b, sc, en
 
 
-def test_direct_assembly_matches_networkx_construction():
-    """assemble_graph_direct builds the same DiGraph as networkx's add_edges_from (copies, filters, empty)."""
+@pytest.mark.parametrize("native", [True, False])
+def test_direct_assembly_matches_networkx_construction(native):
+    """assemble_graph_direct builds the same DiGraph as networkx's add_edges_from (copies, filters, empty),
+    through the C builder (csrc/ovl_digraph.c) and through the Python grouping."""
     import numpy as np
     for seed in (1, 2, 3):
         d, c, a, b, sc, en = _scored_case(seed)
         assert max(c) > 1  # copies exercised
         for ms in (None, 0, 5):
-            _same_graph(og.assemble_graph(d, c, a, b, sc, en, ms), og.assemble_graph_direct(d, c, a, b, sc, en, ms))
+            _same_graph(og.assemble_graph(d, c, a, b, sc, en, ms),
+                        og.assemble_graph_direct(d, c, a, b, sc, en, ms, native=native))
     z = np.zeros(0, np.int32)
-    _same_graph(og.assemble_graph(["A"], [2], z, z, z, z), og.assemble_graph_direct(["A"], [2], z, z, z, z))
-    _same_graph(og.assemble_graph([], [], z, z, z, z), og.assemble_graph_direct([], [], z, z, z, z))
+    _same_graph(og.assemble_graph(["A"], [2], z, z, z, z), og.assemble_graph_direct(["A"], [2], z, z, z, z, native=native))
+    _same_graph(og.assemble_graph([], [], z, z, z, z), og.assemble_graph_direct([], [], z, z, z, z, native=native))
+
+
+def test_native_builder_attribute_dicts_behave_like_dicts():
+    """The C builder's per-edge dicts share one key table (PEP 412) but are ordinary, independent dicts."""
+    import copy
+    import pickle
+    d, c, a, b, sc, en = _scored_case(4)
+    G = og.assemble_graph_direct(d, c, a, b, sc, en, native=True)
+    (u1, v1, d1), (u2, v2, d2) = list(G.edges(data=True))[:2]
+    assert type(d1) is dict and d1 is G.pred[v1][u1]
+    d1["color"] = "red"
+    d1["weight"] += 1000
+    assert "color" not in d2 and d2["weight"] < 1000
+    del d1["end_position"]
+    assert list(d1) == ["weight", "color"] and list(d2) == ["weight", "end_position"]
+    H = pickle.loads(pickle.dumps(G))
+    assert list(H.edges(data=True)) == list(G.edges(data=True))
+    assert list(copy.deepcopy(G).edges(data=True)) == list(G.edges(data=True))
+    G.add_edge(u2, v2, weight=-1)  # networkx updates the existing dict in place
+    assert G[u2][v2] is d2 and d2 == {"weight": -1, "end_position": int(d2["end_position"])}
 
 
 def test_overlap_edges_columns_match_graph():
