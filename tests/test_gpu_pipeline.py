@@ -244,6 +244,47 @@ def test_multi_device_sharding_on_shared_gpu(oracle_mod, cfg2, cfg2_ref, slots, 
         eng.close()
 
 
+def test_contexts_on_concurrent_host_threads(oracle_mod, cfg2, cfg2_ref):
+    """Separate contexts are independent (include/ovl.h): four Python threads (ctypes releases the GIL)
+    score through their own engines at once, with pageable arrays, so the staging copies of all calls
+    share the process's copy pool."""
+    import threading
+    from ovlgraph import OverlapEngine
+    reads, a, b = cfg2
+    n = a.shape[0]
+    errors, results = [], {}
+
+    def work(t):
+        try:
+            eng = _engine_env({"OVL_PIPE_CHUNK": str(9000 + 1000 * t)})
+            try:
+                eng.set_reads(reads)
+                for rep in range(5):
+                    out = (np.empty(n, np.int32), np.empty(n, np.int32))
+                    if (t + rep) % 2:
+                        eng.score(a, b, out=out)
+                    else:
+                        eng.enumerate_candidates(5)
+                        eng.score_candidates(out=out)
+                    results[(t, rep)] = out
+            finally:
+                eng.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    assert len(results) == 20
+    for out in results.values():
+        np.testing.assert_array_equal(out[0], cfg2_ref[0])
+        np.testing.assert_array_equal(out[1], cfg2_ref[1])
+    assert OverlapEngine  # the engines above were independent contexts on GPU 0
+
+
 def test_device_shard_bounds_and_ranges(engine, cfg2, cfg2_ref):
     from ovlgraph.sharded import pair_costs, shard_bounds
     reads, a, b = cfg2
