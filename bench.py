@@ -421,6 +421,35 @@ def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
     return out
 
 
+def sharded_band_sweep(world: int, rank: int, dev, eng, bands, indel: int, steps: int, backend: str):
+    """BASELINE configs[4] across the ranks: cfg5's one shared list sharded by Σ n·m, every rank's results
+    into rank 0's shared host buffer, at each band (-1 = the full reference DP); max-over-ranks step time."""
+    import torch
+    import torch.distributed as dist
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.reads import CONFIGS, config_reads
+    from ovlgraph.sharded import ShardedStep
+    reads, _ = dedup_reads(config_reads("cfg5", seed=0))
+    out = {"workload": WORKLOAD_DESC["cfg5"], "indel": indel, "match": 10, "mismatch": -1, "points": []}
+    for band in bands:
+        st = ShardedStep(reads, k=CONFIGS["cfg5"]["k"], engine=eng, dest="host", indel=indel, band=band)
+        el = timed_steps(st.step, steps, 1, dev, world)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        ok = None
+        if rank == 0 and band == bands[0]:
+            got = st.results()
+            ref = eng.score_candidates(10, -1, indel, band)
+            ok = bool(np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]))
+        out["pairs"] = st.n_pairs
+        out["points"].append({"band": band, "kernel": eng.plan(10, -1, indel, band), "ms_per_step": el / steps * 1e3,
+                              "pairs_per_s": st.n_pairs * steps / el,
+                              **({"matches_single_gpu": ok} if ok is not None else {})})
+        st.close()
+    return out
+
+
 def multi_gpu(args, world: int, rank: int, dev, backend: str):
     """N > 1: one shared list (cfg4 by default) sharded over the ranks, results to rank 0's host."""
     import torch
@@ -469,6 +498,11 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str):
         el2 = timed_steps(st2.step, max(5, args.steps), 2, dev, world)
         rccl = el2
         st2.close()
+    band_sweep_line = None
+    if not args.no_extra:
+        # BASELINE configs[4] (cfg5 band-width sweep, "4xMI355X"): the same sharded step per band
+        band_sweep_line = sharded_band_sweep(world, rank, dev, eng, [8, 16, 32, 64, -1], args.sweep_indel,
+                                             args.sweep_steps, backend)
     red = torch.tensor([elapsed, kernel_ms, 0.0 if ok else 1.0, rccl or 0.0, t_setup], dtype=torch.float64,
                        device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(red, op=dist.ReduceOp.MAX)
@@ -499,6 +533,8 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str):
         "setup_s": round(t_setup, 2),
         "cpu_baseline": None,
     }
+    if band_sweep_line is not None:
+        line["cfg5_band_sweep_sharded"] = band_sweep_line
     if rccl_el:
         line["rccl_gather_to_rank0_hbm"] = {"ms_per_step": rccl_el / max(5, args.steps) * 1e3,
                                             "pairs_per_s": n * max(5, args.steps) / rccl_el,

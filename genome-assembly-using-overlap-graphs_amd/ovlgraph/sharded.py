@@ -116,6 +116,9 @@ def score_pairs_sharded(reads: Sequence[str], a_idx, b_idx, match: int = 10, mis
     return _gather_rows(packed, bounds, a.shape[0], dst, group)
 
 
+_shm_seq = 0
+
+
 class SharedResults:
     """A (score, end) host buffer of n pairs shared by the ranks of one node (POSIX shm).
 
@@ -127,10 +130,12 @@ class SharedResults:
         import torch.distributed as dist
         from multiprocessing import resource_tracker, shared_memory
 
+        global _shm_seq
         self.n = int(n_pairs)
         self.rank = dist.get_rank(group)
         size = max(8, 8 * self.n)
-        name = [f"ovl_{os.getpid()}_{tag}"[:30] if self.rank == 0 else None]
+        _shm_seq += 1  # several buffers may be alive at once (one per ShardedStep)
+        name = [f"ovl_{os.getpid()}_{_shm_seq}_{tag}"[:30] if self.rank == 0 else None]
         if self.rank == 0:
             self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=size)
         dist.broadcast_object_list(name, src=0, group=group)
@@ -187,7 +192,8 @@ class ShardedStep:
 
     Setup once: the read set on this rank's GPU, the candidate list (``a_idx``/``b_idx`` host
     arrays, or ``k`` to enumerate it on the device, identical on every rank), this rank's
-    Σ n·m-balanced shard, and the destination.  ``step()`` scores the shard and gathers:
+    Σ n·m-balanced shard, the scoring (``match``, ``mismatch``, ``indel``, ``band``) and the
+    destination.  ``step()`` scores the shard and gathers:
 
     * ``dest="host"``: the shard's results DMA into rank 0's shared host arrays; ``step()``
       returns after this rank's copies are done and a barrier (every slice has landed);
@@ -201,7 +207,7 @@ class ShardedStep:
     def __init__(self, reads: Sequence[str], a_idx=None, b_idx=None, k: Optional[int] = None,
                  match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT, group=None,
                  engine: Optional[OverlapEngine] = None, local_scorer: Optional[Callable] = None,
-                 dest: str = "host", balance: bool = True):
+                 dest: str = "host", balance: bool = True, band: int = -1):
         import torch
         import torch.distributed as dist
 
@@ -211,7 +217,7 @@ class ShardedStep:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.dest = dest
-        self.scoring = (match, mismatch, indel)
+        self.scoring = (match, mismatch, indel, band)
         self.local_scorer = local_scorer
         self.reads = reads
         self.device = _device(dist, group)
@@ -253,21 +259,21 @@ class ShardedStep:
                 rows = self.packed.numpy()
                 if self.on_device_list:
                     self._launch = lambda: self.eng.score_candidates_range(
-                        lo, hi, match, mismatch, indel, out=(rows[0], rows[1]))
+                        lo, hi, match, mismatch, indel, band, out=(rows[0], rows[1]))
                 else:
                     self._launch = lambda: self.eng.score(self.a[lo:hi], self.b[lo:hi], match, mismatch, indel,
-                                                          out=(rows[0], rows[1]))
+                                                          band, out=(rows[0], rows[1]))
             elif self.eng is not None and hi > lo:
                 if self.on_device_list:
                     pa, pb, _ = self.eng.candidates_device()
                     self._launch = lambda: self.eng.score_device(
                         pa + 4 * lo, pb + 4 * lo, hi - lo, self.packed[0].data_ptr(), self.packed[1].data_ptr(),
-                        match, mismatch, indel, stream=torch.cuda.current_stream(self.device).cuda_stream)
+                        match, mismatch, indel, band, stream=torch.cuda.current_stream(self.device).cuda_stream)
                 else:
                     self.ta = torch.as_tensor(self.a[lo:hi], device=self.device)
                     self.tb = torch.as_tensor(self.b[lo:hi], device=self.device)
                     self._launch = self.eng.launcher(self.ta, self.tb, self.packed[0], self.packed[1],
-                                                     match, mismatch, indel)
+                                                     match, mismatch, indel, band)
 
     def _local(self):
         lo, hi = self.lo, self.hi

@@ -335,6 +335,20 @@ def test_sharded_paths_on_rccl_world1(nccl_world1, engine, cfg2, cfg2_ref):
             st.close()
             np.testing.assert_array_equal(got[0], cfg2_ref[0])
             np.testing.assert_array_equal(got[1], cfg2_ref[1])
+    # gapped and banded scoring through the same steps (bench.py's sharded cfg5 band sweep), two buffers alive
+    keep = ShardedStep(reads, engine=engine, dest="host", k=5)
+    for band in (8, -1):
+        engine.set_reads(reads)
+        engine.enumerate_candidates(5)
+        ref = engine.score_candidates(10, -1, -2, band)
+        for dest in ("host", "rank0"):
+            st = ShardedStep(reads, engine=engine, dest=dest, k=5, indel=-2, band=band)
+            st.step()
+            got = st.results()
+            st.close()
+            np.testing.assert_array_equal(got[0], ref[0])
+            np.testing.assert_array_equal(got[1], ref[1])
+    keep.close()
 
 
 def test_lane_kernel_on_two_streams(oracle_mod, cfg2):
