@@ -148,7 +148,7 @@ def test_banded_long_reads_vs_oracle(engine, oracle_mod, band):
 
 @pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (5, -4, -1), (10, -1, -30), (3, 2, -1),
                                     (5, -4, 0), (0, 0, -1), (-1, -2, -1), (100, -90, -60), (2, -1, 3)])
-@pytest.mark.parametrize("band", [0, 1, 4, 8, 13, 24, 32])
+@pytest.mark.parametrize("band", [0, 1, 4, 8, 13, 24, 32, 40, 48, 56, 64])
 @pytest.mark.parametrize("planes", ["1", "0"])
 def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes):
     """The lane-per-pair band kernel over mixed lengths (empty reads, reads shorter than the band,
