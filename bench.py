@@ -450,6 +450,40 @@ def sharded_band_sweep(world: int, rank: int, dev, eng, bands, indel: int, steps
     return out
 
 
+def single_process_all_gpus(rank: int, reads, k: int, steps: int, eng):
+    """The reference's own shape on the whole node: ONE process, one context over every visible GPU
+    (ovl_create over the device list), the same list scored with each GPU storing its
+    shard of (score, end) straight into the caller's pinned arrays.  Rank 0 runs it alone while the other
+    ranks wait; checked against rank 0's one-GPU engine."""
+    import torch
+    from ovlgraph import OverlapEngine
+    from ovlgraph.hostmem import pinned_empty
+    if rank != 0:
+        return None
+    ids = list(range(torch.cuda.device_count()))
+    t0 = time.perf_counter()
+    multi = OverlapEngine(devices=ids)
+    multi.set_reads(reads)
+    n = multi.enumerate_candidates(k)
+    setup = time.perf_counter() - t0
+    out = (pinned_empty(n), pinned_empty(n))
+    for _ in range(3):
+        multi.score_candidates(out=out)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        multi.score_candidates(out=out)
+    el = time.perf_counter() - t0
+    eng.set_reads(reads)
+    eng.enumerate_candidates(k)
+    ref = eng.score_candidates()
+    ok = bool(np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]))
+    multi.close()
+    return {"devices": ids, "pairs": n, "ms_per_step": el / steps * 1e3, "pairs_per_s": n * steps / el,
+            "setup_s": round(setup, 2), "matches_single_gpu": ok,
+            "what": "one process, OverlapEngine(devices=all visible): shards by sum n*m, each GPU's kernels "
+                    "store its slice into the caller's pinned arrays (no collective)"}
+
+
 def multi_gpu(args, world: int, rank: int, dev, backend: str):
     """N > 1: one shared list (cfg4 by default) sharded over the ranks, results to rank 0's host."""
     import torch
@@ -509,6 +543,10 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str):
     elapsed, kernel_ms, bad, rccl_el, t_setup = (float(x) for x in red.tolist())
     lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
     st.close()
+    single = None
+    if not args.no_extra:
+        single = single_process_all_gpus(rank, reads, cfg["k"], args.steps, eng)
+        dist.barrier()
     if rank != 0:
         return None
     algo_per_rank = (n // world) * (2 * int((lens.max() + 3) // 4) + 16)
@@ -535,6 +573,8 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str):
     }
     if band_sweep_line is not None:
         line["cfg5_band_sweep_sharded"] = band_sweep_line
+    if single is not None:
+        line["single_process_all_gpus"] = single
     if rccl_el:
         line["rccl_gather_to_rank0_hbm"] = {"ms_per_step": rccl_el / max(5, args.steps) * 1e3,
                                             "pairs_per_s": n * max(5, args.steps) / rccl_el,
