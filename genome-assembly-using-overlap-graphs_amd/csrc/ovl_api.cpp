@@ -13,7 +13,10 @@
 // else a DP kernel.  Never falls back to the CPU.
 #include <hip/hip_runtime.h>
 
+#include <pthread.h>
 #include <unistd.h>
+
+#include <new>
 
 #include <algorithm>
 #include <chrono>
@@ -539,11 +542,11 @@ Knobs read_knobs() {
 class CopyPool {
   public:
     static CopyPool& get() {
-        static CopyPool* pool = nullptr;
-        static std::mutex mu;
-        std::lock_guard<std::mutex> lk(mu);
-        if (!pool || pool->pid_ != getpid()) pool = new CopyPool();  // a forked child starts a fresh pool
-        return *pool;
+        static const int registered = pthread_atfork(nullptr, nullptr, &CopyPool::after_fork);
+        (void)registered;
+        std::lock_guard<std::mutex> lk(get_mutex());
+        if (!pool_ || pool_->pid_ != getpid()) pool_ = new CopyPool();  // a forked child starts a fresh pool
+        return *pool_;
     }
     // dst[i] = src[i] for [0, bytes), on the workers and the calling thread
     void copy(void* dst, const void* src, size_t bytes) {
@@ -571,6 +574,17 @@ class CopyPool {
 
   private:
     static constexpr size_t kMinPart = size_t(1) << 19;
+    static inline CopyPool* pool_ = nullptr;
+    static std::mutex& get_mutex() {
+        static std::mutex* mu = new std::mutex();
+        return *mu;
+    }
+    // fork() copies only the calling thread: the child drops the parent's pool (its workers do not exist
+    // there, and a mutex another thread held at the fork would never be released) and builds its own
+    static void after_fork() {
+        new (&get_mutex()) std::mutex();
+        pool_ = nullptr;
+    }
     CopyPool() : pid_(getpid()) {
         int n = (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = getenv("OVL_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
