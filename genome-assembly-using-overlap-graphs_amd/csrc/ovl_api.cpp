@@ -13,6 +13,7 @@
 // else a DP kernel.  Never falls back to the CPU.
 #include <hip/hip_runtime.h>
 
+#include <emmintrin.h>
 #include <pthread.h>
 #include <unistd.h>
 
@@ -68,6 +69,11 @@ struct Knobs {
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic)
     int32_t pipe_direct = 1;      // OVL_PIPE_DIRECT=0: copy-engine H2D / D2H transfers instead of kernels reading
                                   // and storing host memory through its device mapping (A/B knob)
+    int32_t pack = 1;             // OVL_PACK=0: host-array results cross the link as int32 pairs even when the
+                                  // packed form (2 bytes per pair) holds (A/B knob)
+    int64_t pack_min = 1 << 20;   // OVL_PACK_MIN: packed transport from this many pairs per call
+    int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
+    int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
 };
 
 }  // namespace
@@ -133,7 +139,8 @@ struct Dev {
     uint32_t* h_flag = nullptr;      // pinned error flag of host-array calls (the kernels store into it)
     uint32_t* h_flag_dev = nullptr;  // its device address
     uint32_t* cur_flag = nullptr;    // the flag the next launches write: err_flag (device calls) or h_flag_dev
-    bool host_out = false;           // the next launches' outputs are host-mapped (direct host-array calls)
+    int32_t out_mode = 0;            // result sink of the next ungapped launches (OvlUngappedArgs::host_out):
+                                     // 0 HBM, 1 host-mapped int32 arrays, 2 host-mapped packed uint16
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
 };
 
@@ -349,11 +356,11 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         seed.kernel = pl.seed_kernel;
         seed.key64 = pl.seed_key64;
         seed.wide = pl.seed_wide;
-        const bool host_out = c->host_out;
-        c->host_out = false;  // the seeds stay in HBM
+        const int32_t out_mode = c->out_mode;
+        c->out_mode = 0;  // the seeds stay in HBM
         int rc = launch_score_chunk(c, seed, d_a, d_b, n_pairs, match, mismatch, INT32_MIN, as<int32_t>(c->seed_s),
                                     as<int32_t>(c->seed_e), s);
-        c->host_out = host_out;
+        c->out_mode = out_mode;
         if (rc != OVL_OK) return rc;
         seed_end = as<int32_t>(c->seed_e);
     }
@@ -390,7 +397,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.wmax = c->wmax;
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
-        g.host_out = c->host_out ? 1 : 0;
+        g.host_out = c->out_mode;
         HIPCHK(c, ovl_launch_ungapped(&g, s));
     } else {
         OvlDpArgs g{};
@@ -528,6 +535,10 @@ Knobs read_knobs() {
         if (v >= 1 && v <= 1024) k.blocks_per_cu = v;
     }
     if (const char* e = getenv("OVL_PIPE_DIRECT")) k.pipe_direct = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PACK")) k.pack = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
+    if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -548,28 +559,33 @@ class CopyPool {
         if (!pool_ || pool_->pid_ != getpid()) pool_ = new CopyPool();  // a forked child starts a fresh pool
         return *pool_;
     }
-    // dst[i] = src[i] for [0, bytes), on the workers and the calling thread
-    void copy(void* dst, const void* src, size_t bytes) {
-        const size_t parts = std::min<size_t>(workers_.size() + 1, bytes / kMinPart);
+    // f(lo, hi) over [0, n) cut into parts of >= min_part items (multiples of 64), on the workers and the
+    // calling thread
+    void parallel(size_t n, size_t min_part, const std::function<void(size_t, size_t)>& f) {
+        const size_t parts = std::min<size_t>(workers_.size() + 1, n / std::max<size_t>(min_part, 1));
         if (parts <= 1) {
-            memcpy(dst, src, bytes);
+            f(0, n);
             return;
         }
-        const size_t step = (bytes / parts + 63) & ~size_t(63);
+        const size_t step = (n / parts + 63) & ~size_t(63);
         std::lock_guard<std::mutex> one_call(call_mu_);  // calls from several host threads take turns
         std::unique_lock<std::mutex> lk(mu_);
         pending_ = 0;
         for (size_t i = 1; i < parts; ++i) {
-            const size_t lo = i * step, hi = std::min(bytes, lo + step);
+            const size_t lo = i * step, hi = std::min(n, lo + step);
             if (lo >= hi) break;
-            tasks_.push_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, hi - lo); });
+            tasks_.push_back([&f, lo, hi] { f(lo, hi); });
             ++pending_;
         }
         lk.unlock();
         cv_.notify_all();
-        memcpy(dst, src, std::min(step, bytes));
+        f(0, std::min(step, n));
         lk.lock();
         done_.wait(lk, [&] { return pending_ == 0; });
+    }
+    // dst[i] = src[i] for [0, bytes)
+    void copy(void* dst, const void* src, size_t bytes) {
+        parallel(bytes, kMinPart, [=](size_t lo, size_t hi) { memcpy((char*)dst + lo, (const char*)src + lo, hi - lo); });
     }
 
   private:
@@ -615,6 +631,78 @@ class CopyPool {
 };
 
 void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
+
+// Packed results (ovl_kernels.hip put_pair, sink 2) into the caller's int32 arrays.  Per pair one uint16
+// j << 8 | X: score = match*(j - X) + mismatch*X; X = 0xFF: the score is esc[i] (0xFFFF: a bad pair,
+// (-1, -1)).  Eight pairs per step in 16-bit lanes (every int32-key score fits int16, so the wrapping
+// 16-bit products are exact), non-temporal stores where aligned: the arrays are written once and not
+// re-read here, so no read-for-ownership traffic.
+void expand_range(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
+                  bool nt, size_t lo, size_t hi) {
+    auto one = [&](size_t i) {
+        const uint32_t v = pk[i], j = v >> 8, x = v & 0xFFu;
+        if (v == 0xFFFFu) {
+            s[i] = e[i] = -1;
+            return;
+        }
+        s[i] = x == 0xFFu ? esc[i] : match * (int32_t)(j - x) + mismatch * (int32_t)x;
+        e[i] = (int32_t)j;
+    };
+    size_t i = lo;
+    for (; i < hi && ((uintptr_t)(s + i) & 15); ++i) one(i);
+    const bool s_al = nt, e_al = nt && ((uintptr_t)(e + i) & 15) == 0;
+    const __m128i lo8 = _mm_set1_epi16(0xFF), ones = _mm_set1_epi16(-1), zero = _mm_setzero_si128();
+    const __m128i vm = _mm_set1_epi16((int16_t)match), vd = _mm_set1_epi16((int16_t)(mismatch - match));
+    auto put = [](int32_t* p, __m128i v, bool al) {
+        if (al) _mm_stream_si128(reinterpret_cast<__m128i*>(p), v);
+        else _mm_storeu_si128(reinterpret_cast<__m128i*>(p), v);
+    };
+    for (; i + 8 <= hi; i += 8) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(pk + i));
+        const __m128i x = _mm_and_si128(v, lo8);
+        const __m128i j = _mm_srli_epi16(v, 8);
+        const __m128i bad = _mm_cmpeq_epi16(v, ones);
+        // match*j + (mismatch - match)*X as int16, then sign-extended to int32
+        __m128i sc = _mm_add_epi16(_mm_mullo_epi16(j, vm), _mm_mullo_epi16(x, vd));
+        __m128i s0 = _mm_srai_epi32(_mm_unpacklo_epi16(zero, sc), 16);
+        __m128i s1 = _mm_srai_epi32(_mm_unpackhi_epi16(zero, sc), 16);
+        const __m128i spill = _mm_cmpeq_epi16(x, lo8);  // escaped or bad
+        if (_mm_movemask_epi8(spill)) {
+            alignas(16) int32_t t[8];
+            _mm_store_si128(reinterpret_cast<__m128i*>(t), s0);
+            _mm_store_si128(reinterpret_cast<__m128i*>(t + 4), s1);
+            for (int k = 0; k < 8; ++k)
+                if ((pk[i + k] & 0xFFu) == 0xFFu) t[k] = pk[i + k] == 0xFFFFu ? -1 : esc[i + k];
+            s0 = _mm_load_si128(reinterpret_cast<const __m128i*>(t));
+            s1 = _mm_load_si128(reinterpret_cast<const __m128i*>(t + 4));
+        }
+        put(s + i, s0, s_al);
+        put(s + i + 4, s1, s_al);
+        const __m128i en = _mm_or_si128(j, bad);  // 0xFFFF -> -1 through the high half below
+        put(e + i, _mm_unpacklo_epi16(en, bad), e_al);
+        put(e + i + 4, _mm_unpackhi_epi16(en, bad), e_al);
+    }
+    for (; i < hi; ++i) one(i);
+    _mm_sfence();
+}
+
+void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
+                 bool nt, size_t n) {
+    CopyPool::get().parallel(n, size_t(1) << 16, [=](size_t lo, size_t hi) {
+        expand_range(s, e, pk, esc, match, mismatch, nt, lo, hi);
+    });
+}
+
+// The pipeline's waits for a chunk: polled (a chunk is tens of microseconds away; a blocking wait can
+// add its own wake-up latency per chunk, depending on the device's scheduling flags) or hipEventSynchronize.
+hipError_t wait_event(const Dev* d, hipEvent_t ev) {
+    if (!d->k.spin_wait) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        _mm_pause();
+    }
+}
 
 void free_staging(int32_t*& p) {
     if (p) (void)hipHostFree(p);
@@ -737,10 +825,12 @@ bool host_pinned(const void* p, size_t bytes) {
 // copies of pinned arrays run as one chunk; only pageable arrays, which go through pinned staging slots,
 // are cut into chunks (the slot size): 4 M pairs with copy-engine transfers, 512 K pairs when the kernels
 // read and store the staging slots themselves (the host copy of chunk k+1 overlaps the kernel of chunk k).
-// Direct kernel stores into pinned arrays need no chunks at all.
-int64_t pick_chunk(const Dev* d, int64_t n, bool staged, bool direct) {
+// Direct kernel stores into pinned arrays need no chunks at all.  Packed results (pack_ok) are expanded
+// on the host chunk by chunk while the next chunk is scored: 1 M pairs (tools/host_paths_ab.py at the
+// target point: 128 K 0.53 ms, 256 K 0.38, 512 K 0.30, 1 M 0.25, one chunk 0.29).
+int64_t pick_chunk(const Dev* d, int64_t n, bool staged, bool direct, bool pack) {
     if (d->k.pipe_chunk > 0) return d->k.pipe_chunk;
-    const int64_t cap = int64_t(1) << (direct ? 19 : 22);
+    const int64_t cap = int64_t(1) << (pack ? 20 : (direct ? 19 : 22));
     return std::max<int64_t>(1, staged ? std::min(n, cap) : n);
 }
 
@@ -763,6 +853,9 @@ struct Call {
     bool out_pinned = false;
     bool direct = false;           // kernels read host pair lists and store results through host mappings
                                    // (the caller's pinned arrays, or pinned staging slots for pageable ones)
+    bool pack = false;             // direct: results cross the link packed (2 bytes per pair) into the staging
+                                   // slots and are expanded into the caller's arrays on the host
+    bool staged_out() const { return !out_pinned || pack; }
     bool timing = false;
 };
 
@@ -786,8 +879,8 @@ int setup_job(const Call& C, Job& J) {
     const int64_t n = J.hi - J.lo;
     if (n <= 0) return OVL_OK;
     HIPCHK(d, hipSetDevice(d->device));
-    const bool need_in = C.h_a && !C.in_pinned, need_out = !C.out_pinned;
-    J.chunk = pick_chunk(d, n, need_in || need_out, C.direct);
+    const bool need_in = C.h_a && !C.in_pinned, need_out = C.staged_out();
+    J.chunk = pick_chunk(d, n, need_in || need_out, C.direct, C.pack);
     J.nchunks = (n + J.chunk - 1) / J.chunk;
     const size_t bytes = sizeof(int32_t) * (size_t)n;
     if (C.h_a && !C.direct) {
@@ -805,7 +898,7 @@ int setup_job(const Call& C, Job& J) {
         J.za = reinterpret_cast<const int32_t*>(pa);
         J.zb = reinterpret_cast<const int32_t*>(pb);
     }
-    if (C.direct && C.out_pinned) {
+    if (C.direct && !C.staged_out()) {
         // the device's address of this slice of the caller's pinned arrays
         void* ps = nullptr;
         void* pe = nullptr;
@@ -850,7 +943,7 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     const size_t so = (size_t)slot * 2 * (size_t)d->st_cap;
     const bool staged_in = C.h_a && !C.in_pinned;
     // the slot's previous user, chunk k - kSlots, must be done (its staged results were drained already)
-    if (staged_in && k >= kSlots && C.out_pinned) HIPCHK(d, hipEventSynchronize(d->ev_k[slot]));
+    if (staged_in && k >= kSlots && !C.staged_out()) HIPCHK(d, wait_event(d, d->ev_k[slot]));
     const int32_t* ka;
     const int32_t* kb;
     if (C.h_a) {
@@ -867,13 +960,13 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
         ka = J.dev_a + g;
         kb = J.dev_b + g;
     }
-    int32_t* os = C.out_pinned ? J.d_score + off : d->st_out_dev + so;
-    int32_t* oe = C.out_pinned ? J.d_end + off : d->st_out_dev + so + d->st_cap;
+    int32_t* os = C.staged_out() ? d->st_out_dev + so : J.d_score + off;
+    int32_t* oe = C.staged_out() ? d->st_out_dev + so + d->st_cap : J.d_end + off;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
     int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
     if (rc != OVL_OK) return rc;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
-    if (staged_in || !C.out_pinned) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
+    if (staged_in || C.staged_out()) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
     return OVL_OK;
 }
 
@@ -893,7 +986,7 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
         const int32_t* sb = C.h_b + g;
         if (!C.in_pinned) {
             // the slot's previous H2D (chunk k - kSlots) must have read it
-            if (k >= kSlots) HIPCHK(d, hipEventSynchronize(d->ev_in[slot]));
+            if (k >= kSlots) HIPCHK(d, wait_event(d, d->ev_in[slot]));
             int32_t* st = d->st_in + (size_t)slot * 2 * (size_t)d->st_cap;
             host_copy(st, sa, nb);
             host_copy(st + d->st_cap, sb, nb);
@@ -941,8 +1034,13 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int64_t g = J.lo + off;
     const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
     const int slot = (int)(k % kSlots);
-    HIPCHK(d, hipEventSynchronize(C.direct ? d->ev_k[slot] : d->ev_out[slot]));
+    HIPCHK(d, wait_event(d, C.direct ? d->ev_k[slot] : d->ev_out[slot]));
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
+    if (C.pack) {
+        host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
+                    ss + d->st_cap, C.match, C.mismatch, d->k.pack_nt != 0, (size_t)n);
+        return OVL_OK;
+    }
     host_copy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);
     host_copy(C.out_e + (g - C.out_base), ss + d->st_cap, sizeof(int32_t) * (size_t)n);
     return OVL_OK;
@@ -959,17 +1057,17 @@ void quiesce(std::vector<Job>& jobs) {
 // the host reads after the call's synchronisation (no flag copy behind the results).
 struct HostFlag {
     std::vector<Job>& jobs;
-    HostFlag(std::vector<Job>& j, bool host_out) : jobs(j) {
+    HostFlag(std::vector<Job>& j, int32_t out_mode) : jobs(j) {
         for (Job& J : jobs) {
             *(volatile uint32_t*)J.d->h_flag = 0;
             J.d->cur_flag = J.d->h_flag_dev;
-            J.d->host_out = host_out;
+            J.d->out_mode = out_mode;
         }
     }
     ~HostFlag() {
         for (Job& J : jobs) {
             J.d->cur_flag = as<uint32_t>(J.d->err_flag);
-            J.d->host_out = false;
+            J.d->out_mode = 0;
         }
     }
 };
@@ -977,7 +1075,7 @@ struct HostFlag {
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
     int rc = OVL_OK;
-    HostFlag host_flag(jobs, C.direct);
+    HostFlag host_flag(jobs, C.direct ? (C.pack ? 2 : 1) : 0);
     for (Job& J : jobs)
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
     int64_t maxch = 0;
@@ -986,11 +1084,11 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
             if ((rc = issue_chunk(C, J, k)) != OVL_OK) break;
-            if (!C.out_pinned && k >= kSlots - 1 && (rc = drain_chunk(C, J, k - (kSlots - 1))) != OVL_OK) break;
+            if (C.staged_out() && k >= kSlots - 1 && (rc = drain_chunk(C, J, k - (kSlots - 1))) != OVL_OK) break;
         }
     }
     for (Job& J : jobs) {
-        if (rc != OVL_OK || C.out_pinned) break;
+        if (rc != OVL_OK || !C.staged_out()) break;
         for (int64_t k = std::max<int64_t>(0, J.nchunks - (kSlots - 1)); k < J.nchunks; ++k)
             if ((rc = drain_chunk(C, J, k)) != OVL_OK) break;
     }
@@ -1070,6 +1168,16 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
                              d->stream));
     HIPCHK(d, hipStreamSynchronize(d->stream));
     return OVL_OK;
+}
+
+// Direct host-array calls move results packed (ovl_kernels.hip put_pair, sink 2: end and mismatch count
+// in a uint16) when the uniform kernel scores them with int32 keys and reads are at most 254 bases (ends
+// and mismatch counts below the 0xFF marker).
+bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs) {
+    const Dev* d = c->devs[0];
+    return d->k.pack && d->k.pipe_direct && n_pairs >= d->k.pack_min && p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
+           d->planes == 2 &&
+           d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
 }
 
 int check_scoring_args(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* p) {
@@ -1393,6 +1501,7 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = c->timing != 0;
     C.direct = c->devs[0]->k.pipe_direct != 0;
+    C.pack = pack_ok(c, p, n_pairs);
     const int32_t S = (int32_t)c->devs.size();
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);
@@ -1627,6 +1736,7 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = ctx->timing != 0;
     C.direct = ctx->devs[0]->k.pipe_direct != 0;
+    C.pack = pack_ok(ctx, p, hi - lo);
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);

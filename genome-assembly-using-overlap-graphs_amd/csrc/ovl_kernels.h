@@ -30,7 +30,9 @@ struct OvlUngappedArgs {
     int32_t lw;          // dominant read length for uniform_kernel (0: general kernel only)
     const uint32_t* full; // bit r set iff len[r] == lw
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
-    int32_t host_out;    // out_score / out_end are host-mapped (uniform_kernel<..., HOUT>: non-temporal stores)
+    int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
+                         // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
+                         // out_score as uint16, the score of the few pairs that need it in out_end
 };
 
 // kernels of the band knob (ovl_launch_dp); OVL_BAND_FORM env picks one for tests

@@ -61,6 +61,41 @@ __device__ __forceinline__ void put_result(int32_t* p, int32_t v) {
     else *p = v;
 }
 
+// The (score, end) of pair p into the call's result sink (OvlUngappedArgs::host_out):
+//   OM 0: the int32 arrays in HBM;  OM 1: the int32 arrays, host-mapped (non-temporal stores);
+//   OM 2: packed, host-mapped into a pinned staging slot that the host expands into the int32 arrays
+//         (2 instead of 8 link bytes per pair).  An end j <= n (the read a's length) has L = j compared
+//         bases (aligners.py:27-48 with gaps that cannot win), so score = match*(j - X) + mismatch*X and the
+//         pair is (j, X): one uint16 j << 8 | X.  X = 0xFF marks the rest: j << 8 | 0xFF with the score in
+//         out_end[p] (j > n: a shorter read a inside b's window), or 0xFFFF for a bad pair.  The host asks
+//         for it when lmax <= 254 (so j, X <= 254) and the keys are int32; inv = 1 / (match - mismatch),
+//         or 0 when they are equal (X is then immaterial and 0).
+template <int OM>
+__device__ __forceinline__ void put_pair(int32_t* out_score, int32_t* out_end, int64_t p, int32_t sc, int32_t en,
+                                         int32_t n = 0, int32_t match = 0, float inv = 0.f) {
+    if constexpr (OM == 2) {
+        uint32_t v;
+        if (en < 0) {
+            v = 0xFFFFu;
+        } else if (en > n) {
+            v = ((uint32_t)en << 8) | 0xFFu;
+            __builtin_nontemporal_store(sc, out_end + p);
+        } else {
+            // X = (match*j - score) / (match - mismatch), an exact quotient below 2^8: float is exact
+            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * en - sc) * inv);
+            v = ((uint32_t)en << 8) | x;
+        }
+        __builtin_nontemporal_store((uint16_t)v, reinterpret_cast<uint16_t*>(out_score) + p);
+    } else {
+        put_result<OM == 1>(out_score + p, sc);
+        put_result<OM == 1>(out_end + p, en);
+    }
+}
+
+__device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
+    return match != mismatch ? 1.0f / (float)(match - mismatch) : 0.f;
+}
+
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
 // would otherwise sum a block's word counts with an extra v_add3)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t v, uint32_t acc) {
@@ -554,7 +589,7 @@ __device__ __forceinline__ typename Key<KM>::T general_core(bool ok, int32_t n, 
     return group_max(best, 64 >> rs_log2);
 }
 
-template <int P, int W, int KM, bool HOUT = false>
+template <int P, int W, int KM, int OM = 0>
 __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, int32_t b,
                                              const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx,
                                              const int32_t* __restrict__ len, int32_t n_reads, int r0,
@@ -575,8 +610,7 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
     if (mine && r0 == 0) {
         int32_t sc, en;
         Key<KM>::decode(full, sc, en);
-        put_result<HOUT>(out_score + p, ok ? sc : -1);
-        put_result<HOUT>(out_end + p, ok ? en : -1);
+        put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, n, match, pack_inv(match, mismatch));
     }
 }
 
@@ -597,7 +631,7 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
 // most that fits without spilling
 #define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : 4))) \
                                   : ((W) <= 4 ? 7 : ((W) <= 5 ? 6 : ((W) <= 6 ? 5 : 4))))
-template <int W, int KM, bool LAT, bool HOUT>
+template <int W, int KM, bool LAT, int OM>
 __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
@@ -635,7 +669,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         const bool mine = slot < count;
         int4 e = make_int4(0, 0, 0, 0);
         if (mine) e = ring[(head + slot) & (RING - 1)];
-        general_unit<P, W, KM, HOUT>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
+        general_unit<P, W, KM, OM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
                                      mismatch, out_score, out_end, err_flag);
         head += count;
     };
@@ -667,8 +701,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
             if (mine && !ok) {
                 ovl_flag_error(err_flag);
-                put_result<HOUT>(out_score + p, -1);
-                put_result<HOUT>(out_end + p, -1);
+                put_pair<OM>(out_score, out_end, p, -1, -1);
             }
             // (n = lw, m <= lw) pairs are the sweeping wave's: uniform and (TT) t-truncated alike
             const bool push = ok && (TT ? n != lw : !(n == lw && m == lw));
@@ -715,8 +748,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
                 if (own && r0 == 0) {
                     int32_t sc, e2;
                     Key<KM>::decode(full, sc, e2);
-                    put_result<HOUT>(out_score + en.x, sc);
-                    put_result<HOUT>(out_end + en.x, e2);
+                    put_pair<OM>(out_score, out_end, en.x, sc, e2, en.z, match, pack_inv(match, mismatch));
                 }
             }
             __builtin_amdgcn_s_setprio(0);
@@ -757,8 +789,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
-            put_result<HOUT>(out_score + p, ok ? sc : -1);
-            put_result<HOUT>(out_end + p, ok ? en : -1);
+            put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, lw, match, pack_inv(match, mismatch));
         }
         OVL_TR_CLOCK(4, (uint32_t)best);
 #ifndef OVL_ABLATE_DRAIN
@@ -1293,23 +1324,33 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
     return hipGetLastError();
 }
 
-template <int W, int KM, bool LAT, bool HOUT>
+template <int W, int KM, bool LAT, int OM>
 static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    uniform_kernel<W, KM, LAT, HOUT><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
+    uniform_kernel<W, KM, LAT, OM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
                                                                 g.n_pairs, g.lw, g.full, g.match, g.mismatch,
                                                                 g.out_score, g.out_end, g.err_flag);
 }
 
-template <int W, int KM>
-static void launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    // latency mode (two wavefronts per tile) when rs_log2 > 0; host-mapped outputs stream out non-temporally
-    if (g.rs_log2 > 0) {
-        if (g.host_out) launch_uniform_4<W, KM, true, true>(g, blocks, stream);
-        else launch_uniform_4<W, KM, true, false>(g, blocks, stream);
-    } else {
-        if (g.host_out) launch_uniform_4<W, KM, false, true>(g, blocks, stream);
-        else launch_uniform_4<W, KM, false, false>(g, blocks, stream);
+template <int W, int KM, bool LAT>
+static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    switch (g.host_out) {
+        case 0: launch_uniform_4<W, KM, LAT, 0>(g, blocks, stream); return true;
+        case 1: launch_uniform_4<W, KM, LAT, 1>(g, blocks, stream); return true;
+        case 2:
+            if constexpr (KM == 0) {  // packed results: int32 keys only (the host asks for them only then)
+                launch_uniform_4<W, KM, LAT, 2>(g, blocks, stream);
+                return true;
+            }
+            return false;
     }
+    return false;
+}
+
+template <int W, int KM>
+static bool launch_uniform_t(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    // latency mode (two wavefronts per tile) when rs_log2 > 0; host-mapped outputs stream out non-temporally
+    return g.rs_log2 > 0 ? launch_uniform_m<W, KM, true>(g, blocks, stream)
+                         : launch_uniform_m<W, KM, false>(g, blocks, stream);
 }
 
 template <int P, int W, int KM>
@@ -1322,14 +1363,14 @@ static void launch_general_t(const OvlUngappedArgs& g, unsigned blocks, hipStrea
 template <int KM>
 static bool dispatch_uniform(const OvlUngappedArgs& g, unsigned blocks, hipStream_t s) {
     switch (g.wmax) {
-        case 1: launch_uniform_t<1, KM>(g, blocks, s); return true;
-        case 2: launch_uniform_t<2, KM>(g, blocks, s); return true;
-        case 3: launch_uniform_t<3, KM>(g, blocks, s); return true;
-        case 4: launch_uniform_t<4, KM>(g, blocks, s); return true;
-        case 5: launch_uniform_t<5, KM>(g, blocks, s); return true;
-        case 6: launch_uniform_t<6, KM>(g, blocks, s); return true;
-        case 7: launch_uniform_t<7, KM>(g, blocks, s); return true;
-        case 8: launch_uniform_t<8, KM>(g, blocks, s); return true;
+        case 1: return launch_uniform_t<1, KM>(g, blocks, s);
+        case 2: return launch_uniform_t<2, KM>(g, blocks, s);
+        case 3: return launch_uniform_t<3, KM>(g, blocks, s);
+        case 4: return launch_uniform_t<4, KM>(g, blocks, s);
+        case 5: return launch_uniform_t<5, KM>(g, blocks, s);
+        case 6: return launch_uniform_t<6, KM>(g, blocks, s);
+        case 7: return launch_uniform_t<7, KM>(g, blocks, s);
+        case 8: return launch_uniform_t<8, KM>(g, blocks, s);
     }
     return false;
 }
@@ -1372,6 +1413,7 @@ static unsigned grid_for(int64_t pairs, int rs_log2, int64_t max_blocks) {
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
+    if (g->host_out == 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
     if (g->lw > 0) {
         // rs_log2 > 0 here selects the latency mode
         const unsigned nb = grid_for(g->n_pairs << (g->rs_log2 > 0 ? 1 : 0), 0, g->max_blocks);

@@ -101,6 +101,82 @@ def test_pipeline_host_list_pinned_and_pageable(oracle_mod, cfg2, cfg2_ref, chun
         eng.close()
 
 
+@pytest.mark.parametrize("pack,nt", [("1", "1"), ("1", "0"), ("0", "1")])
+@pytest.mark.parametrize("chunk", ["0", "1000"])
+def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, chunk):
+    """Results cross the link packed (uint16 score | end << 8) and are expanded on the host: pinned,
+    pageable and misaligned caller arrays, list lengths that are not a multiple of the 8-pair step, staging
+    slot reuse (many chunks), bad pairs expanded to (-1, -1); non-temporal or ordinary host stores;
+    OVL_PACK=0 is the int32 transport.  (OVL_PACK_MIN=0: packed below the default 1 M-pair threshold.)"""
+    from ovlgraph import OvlError
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = cfg2
+    eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_NT": nt, "OVL_PIPE_CHUNK": chunk})
+    try:
+        eng.set_reads(reads)
+        n = a.shape[0] - 3
+        outs = {"pinned": (pinned_empty(n), pinned_empty(n)),
+                "pageable": (np.empty(n, np.int32), np.empty(n, np.int32)),
+                # 4-byte offsets: the expansion's 16-byte alignment differs between the two arrays
+                "misaligned": (np.empty(n + 1, np.int32)[1:], np.empty(n + 2, np.int32)[2:])}
+        for name, out in outs.items():
+            out[0][:] = 7
+            out[1][:] = 7
+            eng.score(a[:n], b[:n], out=out)
+            np.testing.assert_array_equal(out[0], cfg2_ref[0][:n], err_msg=name)
+            np.testing.assert_array_equal(out[1], cfg2_ref[1][:n], err_msg=name)
+        # the resident candidate list into a misaligned pageable pair of arrays
+        eng.candidates(5)
+        out = (np.empty(a.shape[0] + 1, np.int32)[1:], np.empty(a.shape[0], np.int32))
+        eng.score_candidates(out=out)
+        np.testing.assert_array_equal(out[0], cfg2_ref[0])
+        np.testing.assert_array_equal(out[1], cfg2_ref[1])
+        # bad pairs: (-1, -1) at their positions, every other pair scored
+        bad = b.copy()
+        pos = [0, 7, 8, len(bad) // 2, len(bad) - 1]
+        bad[pos] = len(reads) + 5
+        out = (np.empty(len(a), np.int32), np.empty(len(a), np.int32))
+        with pytest.raises(OvlError, match="OVL_E_INDEX"):
+            eng.score(a, bad, out=out)
+        want_s, want_e = cfg2_ref[0].copy(), cfg2_ref[1].copy()
+        want_s[pos] = -1
+        want_e[pos] = -1
+        np.testing.assert_array_equal(out[0], want_s)
+        np.testing.assert_array_equal(out[1], want_e)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("l", [254, 255])
+@pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
+def test_packed_results_at_the_length_limit(oracle_mod, l, scoring):
+    """The packed transport carries (end, mismatch count) for reads up to 254 bases (255 falls back to
+    int32 results), under any scores with int32 keys: match == mismatch (mismatch count immaterial),
+    mismatch > match, and pairs whose best end lies past a shorter read a (the score travels separately).
+    Identical full-length reads end at l."""
+    match, mismatch = scoring
+    rng = np.random.default_rng(l * 10 + match)
+    pack_env = {"OVL_PACK_MIN": "0"}
+    base = ["".join(rng.choice(list("ACGT"), l)) for _ in range(40)]
+    reads = base + [r[i + 1:] for i, r in enumerate(base[:20])]  # suffixes: a inside b's window (end > n)
+    reads += [r[: l - 1 - i] for i, r in enumerate(base[20:])]  # prefixes
+    m = len(reads)
+    a = np.concatenate([np.arange(40), np.arange(40, 60), rng.integers(0, m, 3000)]).astype(np.int32)
+    b = np.concatenate([np.arange(40), np.arange(20), rng.integers(0, m, 3000)]).astype(np.int32)
+    eng = _engine_env(pack_env)
+    try:
+        eng.set_reads(reads)
+        out = (np.empty(len(a), np.int32), np.empty(len(a), np.int32))
+        eng.score(a, b, match, mismatch, out=out)
+        rs, re_ = oracle_mod.batch_ungapped(reads, a, b, match, mismatch)
+        np.testing.assert_array_equal(out[0], rs)
+        np.testing.assert_array_equal(out[1], re_)
+        if match > max(mismatch, 0):
+            assert out[1][:40].tolist() == [l] * 40 and out[0][:40].tolist() == [match * l] * 40
+    finally:
+        eng.close()
+
+
 def test_pipeline_gapped_and_banded(oracle_mod, cfg2):
     """The pipeline around the DP kernels (lane kernel above 65,536 pairs) and the band knob."""
     reads, a, b = cfg2

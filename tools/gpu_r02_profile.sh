@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 profiles of the default bench workload (target point), the headline command without extras:
-#   kernel trace + stats (the step's uniform_kernel<4, 0, false, true> storing to host memory, and the
-#   kernel-only uniform_kernel<4, 0, false, false> that roofline.kernel_ms times), then PMC passes over the
+#   kernel trace + stats (the step's uniform_kernel<4, 0, false, 1 or 2> storing to host memory, and the
+#   kernel-only uniform_kernel<4, 0, false, 0> that roofline.kernel_ms times), then PMC passes over the
 #   kernel-only variant, each in its own run: FETCH_SIZE, WRITE_SIZE, SQ instruction counts, occupancy, LDS.
 # usage: bash tools/gpu_r02_profile.sh [config] [tag]
 set -o pipefail
@@ -15,7 +15,7 @@ B="$GRAFT_REPO_ROOT/bench.py"
 ARGS="--config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-extra"
 echo "== kernel trace + stats"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 "$B" $ARGS > "$OUT/kt.log" 2>&1 || { echo "kt failed"; tail -20 "$OUT/kt.log"; exit 1; }
-KRE="uniform_kernel<[0-9], 0, false, false>"
+KRE="uniform_kernel<[0-9], 0, false, 0>"
 i=0
 for CTRS in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   i=$((i+1))

@@ -1,7 +1,8 @@
 """Host-array entry points at one config (default: target): every combination of where the pair list
 lives (device-enumerated / pinned host / pageable host) and where results go (pinned / pageable), in direct
-mode (kernels read and store host memory through its mapping; OVL_PIPE_DIRECT=1, the default) and
-copy-engine mode (OVL_PIPE_DIRECT=0), with the host staging copies on 1 thread or the pool's default.
+mode (kernels read and store host memory through its mapping; OVL_PIPE_DIRECT=1, the default) with packed
+results (the default) or int32 results (OVL_PACK=0) and a few chunk sizes, and copy-engine mode
+(OVL_PIPE_DIRECT=0), with the host staging copies on 1 thread or the pool's default.
 
     python tools/host_paths_ab.py [config] [reps]
 """
@@ -18,7 +19,8 @@ import numpy as np  # noqa: E402
 def run_setting(reads, k, env, reps):
     from ovlgraph import OverlapEngine
     from ovlgraph.hostmem import PinnedPool
-    keep = {x: os.environ.get(x) for x in ("OVL_PIPE_DIRECT",)}
+    keep = {x: os.environ.get(x) for x in ("OVL_PIPE_DIRECT", "OVL_PACK", "OVL_PIPE_CHUNK", "OVL_PACK_MIN",
+                                           "OVL_PACK_NT")}
     os.environ.update(env)
     try:
         eng = OverlapEngine(0)
@@ -67,10 +69,17 @@ def main():
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
     out = {"config": cfg, "host_threads_env": os.environ.get("OVL_HOST_THREADS")}
     refs = []
-    for name, env in (("direct", {"OVL_PIPE_DIRECT": "1"}), ("copy_engine", {"OVL_PIPE_DIRECT": "0"})):
+    modes = (("direct", {"OVL_PIPE_DIRECT": "1"}),
+             ("direct_unpacked", {"OVL_PIPE_DIRECT": "1", "OVL_PACK": "0"}),
+             ("packed_any_size", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0"}),
+             ("packed_plain_stores", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0", "OVL_PACK_NT": "0"}),
+             ("packed_chunk512k", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0", "OVL_PIPE_CHUNK": "524288"}),
+             ("packed_chunk2m", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0", "OVL_PIPE_CHUNK": "2097152"}),
+             ("copy_engine", {"OVL_PIPE_DIRECT": "0"}))
+    for name, env in modes:
         out[name], r = run_setting(reads, CONFIGS[cfg]["k"], env, reps)
         refs.append(r)
-    out["modes_agree"] = bool(np.array_equal(refs[0][0], refs[1][0]) and np.array_equal(refs[0][1], refs[1][1]))
+    out["modes_agree"] = all(bool(np.array_equal(refs[0][0], r[0]) and np.array_equal(refs[0][1], r[1])) for r in refs)
     print(json.dumps(out, indent=1))
 
 
