@@ -74,6 +74,9 @@ struct Knobs {
     int64_t pack_min = 1 << 20;   // OVL_PACK_MIN: packed transport from this many pairs per call
     int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
     int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
+    int32_t pack_direct_pct = 25; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
+                                  // pairs (the last chunk) as int32 straight into them, over the link while the
+                                  // host expands the packed chunks
 };
 
 }  // namespace
@@ -539,6 +542,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -854,15 +858,18 @@ struct Call {
     bool direct = false;           // kernels read host pair lists and store results through host mappings
                                    // (the caller's pinned arrays, or pinned staging slots for pageable ones)
     bool pack = false;             // direct: results cross the link packed (2 bytes per pair) into the staging
-                                   // slots and are expanded into the caller's arrays on the host
-    bool staged_out() const { return !out_pinned || pack; }
+                                   // slots and are expanded into the caller's arrays on the host (all chunks for
+                                   // pageable arrays; for pinned ones all but a last direct chunk, Job::n_packed)
     bool timing = false;
 };
 
 struct Job {
     Dev* d = nullptr;
     int64_t lo = 0, hi = 0;  // global pair range of this device
-    int64_t chunk = 1, nchunks = 0;
+    int64_t chunk = 1;       // largest chunk (the staging slot capacity)
+    std::vector<int64_t> cb; // chunk k: pairs [cb[k], cb[k + 1]) of the range (local indexing)
+    int64_t nchunks = 0;
+    int64_t n_packed = 0;    // C.pack: the first n_packed chunks are packed and staged
     int64_t st_in_cap = 0, st_out_cap = 0;
     const int32_t* dev_a = nullptr;  // device pair list (global indexing) when the call has no host list
     const int32_t* dev_b = nullptr;
@@ -874,14 +881,35 @@ struct Job {
     int32_t* d_end = nullptr;
 };
 
+// Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
+bool chunk_staged(const Call& C, const Job& J, int64_t k) { return !C.out_pinned || (C.pack && k < J.n_packed); }
+
 int setup_job(const Call& C, Job& J) {
     Dev* d = J.d;
     const int64_t n = J.hi - J.lo;
+    J.cb.assign(1, 0);
+    J.nchunks = J.n_packed = 0;
     if (n <= 0) return OVL_OK;
     HIPCHK(d, hipSetDevice(d->device));
-    const bool need_in = C.h_a && !C.in_pinned, need_out = C.staged_out();
+    const bool need_in = C.h_a && !C.in_pinned, need_out = !C.out_pinned || C.pack;
     J.chunk = pick_chunk(d, n, need_in || need_out, C.direct, C.pack);
-    J.nchunks = (n + J.chunk - 1) / J.chunk;
+    // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
+    int64_t packed = 0;
+    if (C.pack) {
+        packed = C.out_pinned ? (n - n * d->k.pack_direct_pct / 100) & ~int64_t(63) : n;
+        if (packed >= n - 64) packed = n;
+        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
+        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
+        if (packed > 0) J.cb.push_back(packed);
+        J.n_packed = (int64_t)J.cb.size() - 1;
+    }
+    for (int64_t o = packed; o < n;) {
+        o = std::min(n, o + J.chunk);
+        J.cb.push_back(o);
+    }
+    J.nchunks = (int64_t)J.cb.size() - 1;
+    for (int64_t k = 0; k < J.nchunks; ++k) J.chunk = std::max(J.chunk, J.cb[(size_t)k + 1] - J.cb[(size_t)k]);
     const size_t bytes = sizeof(int32_t) * (size_t)n;
     if (C.h_a && !C.direct) {
         HIPCHK(d, ensure(d->a, bytes));
@@ -898,7 +926,7 @@ int setup_job(const Call& C, Job& J) {
         J.za = reinterpret_cast<const int32_t*>(pa);
         J.zb = reinterpret_cast<const int32_t*>(pb);
     }
-    if (C.direct && !C.staged_out()) {
+    if (C.direct && C.out_pinned) {
         // the device's address of this slice of the caller's pinned arrays
         void* ps = nullptr;
         void* pe = nullptr;
@@ -935,15 +963,16 @@ int setup_job(const Call& C, Job& J) {
 int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     Dev* d = J.d;
     HIPCHK(d, hipSetDevice(d->device));
-    const int64_t off = k * J.chunk;
+    const int64_t off = J.cb[(size_t)k];
     const int64_t g = J.lo + off;
-    const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
+    const int64_t n = J.cb[(size_t)k + 1] - off;
+    const bool staged_out = chunk_staged(C, J, k);
     const size_t nb = sizeof(int32_t) * (size_t)n;
     const int slot = (int)(k % kSlots);
     const size_t so = (size_t)slot * 2 * (size_t)d->st_cap;
     const bool staged_in = C.h_a && !C.in_pinned;
     // the slot's previous user, chunk k - kSlots, must be done (its staged results were drained already)
-    if (staged_in && k >= kSlots && !C.staged_out()) HIPCHK(d, wait_event(d, d->ev_k[slot]));
+    if (staged_in && k >= kSlots && !chunk_staged(C, J, k - kSlots)) HIPCHK(d, wait_event(d, d->ev_k[slot]));
     const int32_t* ka;
     const int32_t* kb;
     if (C.h_a) {
@@ -960,13 +989,14 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
         ka = J.dev_a + g;
         kb = J.dev_b + g;
     }
-    int32_t* os = C.staged_out() ? d->st_out_dev + so : J.d_score + off;
-    int32_t* oe = C.staged_out() ? d->st_out_dev + so + d->st_cap : J.d_end + off;
+    int32_t* os = staged_out ? d->st_out_dev + so : J.d_score + off;
+    int32_t* oe = staged_out ? d->st_out_dev + so + d->st_cap : J.d_end + off;
+    d->out_mode = C.pack && k < J.n_packed ? 2 : 1;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
     int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
     if (rc != OVL_OK) return rc;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
-    if (staged_in || C.staged_out()) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
+    if (staged_in || staged_out) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
     return OVL_OK;
 }
 
@@ -974,9 +1004,9 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     if (C.direct) return issue_chunk_direct(C, J, k);
     Dev* d = J.d;
     HIPCHK(d, hipSetDevice(d->device));
-    const int64_t off = k * J.chunk;
+    const int64_t off = J.cb[(size_t)k];
     const int64_t g = J.lo + off;
-    const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
+    const int64_t n = J.cb[(size_t)k + 1] - off;
     const size_t nb = sizeof(int32_t) * (size_t)n;
     const int slot = (int)(k % kSlots);
     const int32_t* ka;
@@ -1030,9 +1060,9 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
 // direct mode the kernel that stored them).
 int drain_chunk(const Call& C, Job& J, int64_t k) {
     Dev* d = J.d;
-    const int64_t off = k * J.chunk;
+    const int64_t off = J.cb[(size_t)k];
     const int64_t g = J.lo + off;
-    const int64_t n = std::min(J.chunk, (J.hi - J.lo) - off);
+    const int64_t n = J.cb[(size_t)k + 1] - off;
     const int slot = (int)(k % kSlots);
     HIPCHK(d, wait_event(d, C.direct ? d->ev_k[slot] : d->ev_out[slot]));
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
@@ -1075,7 +1105,7 @@ struct HostFlag {
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
     int rc = OVL_OK;
-    HostFlag host_flag(jobs, C.direct ? (C.pack ? 2 : 1) : 0);
+    HostFlag host_flag(jobs, C.direct ? 1 : 0);  // (direct chunks set their own sink: issue_chunk_direct)
     for (Job& J : jobs)
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
     int64_t maxch = 0;
@@ -1084,13 +1114,14 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
             if ((rc = issue_chunk(C, J, k)) != OVL_OK) break;
-            if (C.staged_out() && k >= kSlots - 1 && (rc = drain_chunk(C, J, k - (kSlots - 1))) != OVL_OK) break;
+            const int64_t j = k - (kSlots - 1);
+            if (j >= 0 && chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
         }
     }
     for (Job& J : jobs) {
-        if (rc != OVL_OK || !C.staged_out()) break;
+        if (rc != OVL_OK) break;
         for (int64_t k = std::max<int64_t>(0, J.nchunks - (kSlots - 1)); k < J.nchunks; ++k)
-            if ((rc = drain_chunk(C, J, k)) != OVL_OK) break;
+            if (chunk_staged(C, J, k) && (rc = drain_chunk(C, J, k)) != OVL_OK) break;
     }
     if (rc != OVL_OK) {
         quiesce(jobs);

@@ -101,17 +101,21 @@ def test_pipeline_host_list_pinned_and_pageable(oracle_mod, cfg2, cfg2_ref, chun
         eng.close()
 
 
-@pytest.mark.parametrize("pack,nt", [("1", "1"), ("1", "0"), ("0", "1")])
+@pytest.mark.parametrize("pack,nt,pct", [("1", "1", "25"), ("1", "0", "25"), ("1", "1", "0"), ("1", "1", "60"),
+                                         ("1", "1", "100"), ("0", "1", "25")])
 @pytest.mark.parametrize("chunk", ["0", "1000"])
-def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, chunk):
+def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, pct, chunk):
     """Results cross the link packed (uint16 score | end << 8) and are expanded on the host: pinned,
     pageable and misaligned caller arrays, list lengths that are not a multiple of the 8-pair step, staging
-    slot reuse (many chunks), bad pairs expanded to (-1, -1); non-temporal or ordinary host stores;
-    OVL_PACK=0 is the int32 transport.  (OVL_PACK_MIN=0: packed below the default 1 M-pair threshold.)"""
+    slot reuse (many chunks, 1000-pair chunks that are not a multiple of the 64-pair rounding), bad pairs
+    expanded to (-1, -1); non-temporal or ordinary host stores; pinned arrays with 0-100 % of the pairs in
+    direct int32 chunks after the packed ones; OVL_PACK=0 is the int32 transport.  (OVL_PACK_MIN=0: packed
+    below the default 1 M-pair threshold.)"""
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
-    eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_NT": nt, "OVL_PIPE_CHUNK": chunk})
+    eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_NT": nt, "OVL_PACK_DIRECT_PCT": pct,
+                       "OVL_PIPE_CHUNK": chunk})
     try:
         eng.set_reads(reads)
         n = a.shape[0] - 3

@@ -34,9 +34,12 @@ def main():
             w.eng.score_candidates(10, -1, w.indel, w.band, out=o)
         return (time.perf_counter() - t0) / reps * 1e3
 
-    res["same_out_ms"] = t(w.out)
-    res["fresh_pinned_ms"] = t((pinned_empty(n), pinned_empty(n)))
-    res["pageable_ms"] = t((np.empty(n, np.int32), np.empty(n, np.int32)))
+    fresh = (pinned_empty(n), pinned_empty(n))
+    pg = (np.empty(n, np.int32), np.empty(n, np.int32))
+    for k in range(3):  # alternations: run-to-run noise within one process
+        res[f"same_out_ms_{k}"] = t(w.out)
+        res[f"fresh_pinned_ms_{k}"] = t(fresh)
+        res[f"pageable_ms_{k}"] = t(pg)
     res["out_ptrs"] = [hex(w.out[0].ctypes.data), hex(w.out[1].ctypes.data)]
     res["bench_timed_steps_again_ms"] = bench.timed_steps(w.step, reps, 5, dev, 1) / reps * 1e3
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in res.items()}))

@@ -1,6 +1,5 @@
-# packed result transport: pipeline + parity GPU tests, host-array entry points A/B (packed / int32 / chunk
-# sizes / store kinds / copy engine; the host pool at its default 8 and at 16 threads) at the target point
-# and cfg2, then the bench line
+# packed result transport: pipeline + parity GPU tests, host-array entry points A/B (packed / int32 / direct
+# share / chunk sizes / store kinds / copy engine) at the target point and cfg2, then the bench line
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/pk
@@ -12,7 +11,6 @@ for k, v in d.items():
 timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py tests/test_gpu_c_abi.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pk/pytest.log 2>&1 || { tail -40 gpurun_out/pk/pytest.log; exit 1; }
 tail -2 gpurun_out/pk/pytest.log
 timeout -k 10 300 python tools/host_paths_ab.py target 30 > gpurun_out/pk/target.json && show gpurun_out/pk/target.json && \
-OVL_HOST_THREADS=16 timeout -k 10 300 python tools/host_paths_ab.py target 30 > gpurun_out/pk/target_t16.json && show gpurun_out/pk/target_t16.json && \
-timeout -k 10 300 python tools/host_paths_ab.py cfg2 200 > gpurun_out/pk/cfg2.json && show gpurun_out/pk/cfg2.json && \
+timeout -k 10 300 python tools/host_paths_ab.py cfg3 20 > gpurun_out/pk/cfg3.json && show gpurun_out/pk/cfg3.json && \
 timeout -k 10 300 python bench.py > gpurun_out/pk/bench.log 2>&1 && grep '^{"metric"' gpurun_out/pk/bench.log | python -c "
-import json, sys; d = json.loads(sys.stdin.read()); print({k: d[k] for k in ('value', 'ms_per_step')}, d.get('roofline', {}).get('kernel_ms'), d.get('extra_configs', {}).get('cfg2', {}).get('ms_per_step'))"
+import json, sys; d = json.loads(sys.stdin.read()); print({k: d[k] for k in ('value', 'ms_per_step')}, d.get('roofline', {}).get('kernel_ms'), {k: v.get('ms_per_step') for k, v in d.get('extra_configs', {}).items() if isinstance(v, dict)})"

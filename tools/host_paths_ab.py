@@ -20,7 +20,7 @@ def run_setting(reads, k, env, reps):
     from ovlgraph import OverlapEngine
     from ovlgraph.hostmem import PinnedPool
     keep = {x: os.environ.get(x) for x in ("OVL_PIPE_DIRECT", "OVL_PACK", "OVL_PIPE_CHUNK", "OVL_PACK_MIN",
-                                           "OVL_PACK_NT")}
+                                           "OVL_PACK_NT", "OVL_PACK_DIRECT_PCT")}
     os.environ.update(env)
     try:
         eng = OverlapEngine(0)
@@ -72,9 +72,13 @@ def main():
     modes = (("direct", {"OVL_PIPE_DIRECT": "1"}),
              ("direct_unpacked", {"OVL_PIPE_DIRECT": "1", "OVL_PACK": "0"}),
              ("packed_any_size", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0"}),
-             ("packed_plain_stores", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0", "OVL_PACK_NT": "0"}),
-             ("packed_chunk512k", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0", "OVL_PIPE_CHUNK": "524288"}),
-             ("packed_chunk2m", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_MIN": "0", "OVL_PIPE_CHUNK": "2097152"}),
+             ("packed_direct_0pct", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_DIRECT_PCT": "0"}),
+             ("packed_direct_15pct", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_DIRECT_PCT": "15"}),
+             ("packed_direct_35pct", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_DIRECT_PCT": "35"}),
+             ("packed_direct_50pct", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_DIRECT_PCT": "50"}),
+             ("packed_plain_stores", {"OVL_PIPE_DIRECT": "1", "OVL_PACK_NT": "0"}),
+             ("packed_chunk512k", {"OVL_PIPE_DIRECT": "1", "OVL_PIPE_CHUNK": "524288"}),
+             ("packed_chunk2m", {"OVL_PIPE_DIRECT": "1", "OVL_PIPE_CHUNK": "2097152"}),
              ("copy_engine", {"OVL_PIPE_DIRECT": "0"}))
     for name, env in modes:
         out[name], r = run_setting(reads, CONFIGS[cfg]["k"], env, reps)
