@@ -5,8 +5,10 @@ set: the distinct reads and the reference-ordered candidate list (aligners.py:27
 every pair of overlapGraphs.py:43-53) are resident in HBM when the timed region starts
 (the list is enumerated on the device, ovl_candidates), and the step ends with every
 pair's (score, end) in host memory: the ABI call ``ovl_score_candidates`` runs the
-kernels in chunks and DMA-copies each chunk's results into pinned host arrays while
-the next chunk scores.
+kernels, which store their results over the link into host memory -- packed (end and
+mismatch count, 2 B per pair) for the first chunks, which host threads expand into the
+caller's pinned int32 arrays while the next chunks score, and as int32 straight into
+those arrays for the last quarter of the pairs.
 
     python bench.py [--gpus 1 --steps K --warmup W --config target]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -282,14 +284,16 @@ def step_breakdown(w: Workload, ms_per_step: float, reps: int = 5):
         w.step()
         k.append(w.eng.last_timing()["kernel_ms"])
     w.eng.set_timing(False)
-    d2h = 8 * w.n_pairs
+    x = w.eng.last_transfer()
+    d2h = x["link_bytes"]
     gbs = d2h / (ms_per_step * 1e-3) / 1e9
     return {"kernels_ms_in_step": float(np.median(k)), "d2h_bytes_per_step": d2h,
-            "d2h_gbs_over_step": gbs,
+            "packed_pairs_per_step": x["packed_pairs"], "d2h_gbs_over_step": gbs,
             "pcie_roofline": {"bound": "pcie", "achieved": gbs, "peak": PCIE_PEAK_GBS, "unit": "GB/s",
                               "frac": gbs / PCIE_PEAK_GBS,
-                              "what": "results (8 B/pair) over the whole step time; the step is bound by the D2H "
-                                      "when the kernels are faster than the copies"}}
+                              "what": "result bytes over the link (ovl_last_transfer: 2 B per pair in packed "
+                                      "chunks, expanded on the host; 8 B per pair stored straight into the "
+                                      "pinned arrays) over the whole step time"}}
 
 
 def host_paths(w: Workload, reps: int = 10):
@@ -391,13 +395,14 @@ def local_alignment_timing(eng, reps: int = 5):
 def config_line(w: Workload, steps: int, dev):
     """One config's step (results to pinned host) and kernel-only numbers."""
     el = timed_steps(w.step, steps, 2, dev, 1)
+    link = w.eng.last_transfer()["link_bytes"]
     km = kernel_timing(w, steps, dev)
     algo = w.algo_bytes()
     return {"workload": WORKLOAD_DESC[w.name], "pairs": w.n_pairs, "kernel": w.kernel,
             "value": w.n_pairs * steps / el, "ms_per_step": el / steps * 1e3,
             "kernel_ms": km, "kernel_pairs_per_s": w.n_pairs / (km * 1e-3),
             "roofline_frac": algo / (km * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "d2h_gbs_over_step": 8 * w.n_pairs / (el / steps) / 1e9}
+            "d2h_bytes_per_step": link, "d2h_gbs_over_step": link / (el / steps) / 1e9}
 
 
 def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
@@ -651,8 +656,9 @@ def main() -> None:
             "reads": len(w.reads),
             "pairs": w.n_pairs,
             "read_length": w.cfg["l"],
-            "step": "ovl_score_candidates: resident reads + device-enumerated list -> chunked kernels -> "
-                    "(score, end) DMA'd into pinned host arrays (SURVEY.md §8d, results in host memory)",
+            "step": "ovl_score_candidates: resident reads + device-enumerated list -> kernels storing over the "
+                    "link -> (score, end) in pinned host int32 arrays (SURVEY.md §8d, results in host memory; "
+                    "packed 2 B/pair chunks expanded by host threads, the last quarter stored directly)",
             "parallelism": "1 GPU",
             "kernel": w.kernel,
             "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},

@@ -153,6 +153,7 @@ struct ovl_ctx {
     std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
     int32_t timing = 0;          // ovl_set_timing
     double t_kernel_ms = 0.0, t_call_ms = 0.0;
+    int64_t x_link_bytes = 0, x_packed_pairs = 0;  // ovl_last_transfer
 };
 
 namespace {
@@ -1151,6 +1152,16 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     }
     c->t_kernel_ms = kms;
     c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    int64_t link = 0, packed = 0;
+    for (const Job& J : jobs) {
+        const int64_t n = J.hi - J.lo;
+        if (n <= 0) continue;
+        const int64_t np = J.n_packed ? J.cb[(size_t)J.n_packed] : 0;
+        packed += np;
+        link += (C.h_a ? 8 * n : 0) + 2 * np + 8 * (n - np);
+    }
+    c->x_link_bytes = link;
+    c->x_packed_pairs = packed;
     return rc;
 }
 
@@ -1309,6 +1320,13 @@ OVL_API int ovl_host_unregister(void* ptr) {
 OVL_API int ovl_set_timing(ovl_ctx* c, int32_t on) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     c->timing = on ? 1 : 0;
+    return OVL_OK;
+}
+
+OVL_API int ovl_last_transfer(const ovl_ctx* c, int64_t* link_bytes, int64_t* packed_pairs) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (link_bytes) *link_bytes = c->x_link_bytes;
+    if (packed_pairs) *packed_pairs = c->x_packed_pairs;
     return OVL_OK;
 }
 

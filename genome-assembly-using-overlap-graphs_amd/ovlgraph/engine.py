@@ -117,6 +117,12 @@ class OverlapEngine:
         check(self._L.ovl_last_timing(self._ctx, ctypes.byref(k), ctypes.byref(w)), self._ctx)
         return {"kernel_ms": k.value, "call_ms": w.value}
 
+    def last_transfer(self) -> Dict[str, int]:
+        """{link_bytes, packed_pairs} of the last host-array scoring call (ovl_last_transfer)."""
+        b, p = ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.ovl_last_transfer(self._ctx, ctypes.byref(b), ctypes.byref(p)), self._ctx)
+        return {"link_bytes": b.value, "packed_pairs": p.value}
+
     # ---------------------------------------------------------------- lifecycle
     def close(self) -> None:
         if getattr(self, "_ctx", None):

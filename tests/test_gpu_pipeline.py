@@ -129,6 +129,17 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, pct, c
             eng.score(a[:n], b[:n], out=out)
             np.testing.assert_array_equal(out[0], cfg2_ref[0][:n], err_msg=name)
             np.testing.assert_array_equal(out[1], cfg2_ref[1][:n], err_msg=name)
+            # ovl_last_transfer: the pair list (8 B/pair) plus 2 B per packed and 8 B per other pair
+            x = eng.last_transfer()
+            if pack == "0":
+                want = 0
+            elif name == "pinned":
+                want = (n - n * int(pct) // 100) & ~63
+                want = n if want >= n - 64 else want
+            else:
+                want = n
+            assert x["packed_pairs"] == want, (name, x)
+            assert x["link_bytes"] == 8 * n + 2 * want + 8 * (n - want), (name, x)
         # the resident candidate list into a misaligned pageable pair of arrays
         eng.candidates(5)
         out = (np.empty(a.shape[0] + 1, np.int32)[1:], np.empty(a.shape[0], np.int32))
