@@ -1214,10 +1214,13 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
 
 // Direct host-array calls move results packed (ovl_kernels.hip put_pair, sink 2: end and mismatch count
 // in a uint16) when the uniform kernel scores them with int32 keys and reads are at most 254 bases (ends
-// and mismatch counts below the 0xFF marker).
+// and mismatch counts below the 0xFF marker).  One-device contexts only: the calling thread's host pool
+// expands every packed chunk, so N devices would funnel N links' results through one pool, where int32
+// results take N links in parallel (one process per GPU packs per process).
 bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs) {
     const Dev* d = c->devs[0];
-    return d->k.pack && d->k.pipe_direct && n_pairs >= d->k.pack_min && p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
+    return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= d->k.pack_min &&
+           p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
 }
