@@ -1,7 +1,7 @@
 """Summarise tools/gpu_r02_profile.sh into profiles/<round>_<config>_{kernel_stats.csv,pmc.json}.
 
-The step launches uniform_kernel<W, 0, false, 1 or 2> (results stored straight into pinned host memory, PCIe-bound)
-and roofline.kernel_ms times uniform_kernel<W, 0, false, 0> (device outputs); their names differ, so the
+The step launches uniform_kernel<W, 0, false, 2> (packed chunks into pinned staging slots) and
+uniform_kernel<W, 0, false, 1> (its last chunk, int32 straight into the pinned arrays), and roofline.kernel_ms times uniform_kernel<W, 0, false, 0> (device outputs); their names differ, so the
 rocprofv3 --stats rows are already one per phase.  PMC passes cover the kernel-only variant:
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1 KiB (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md);
 mean resident wavefronts per SIMD = 4 * SQ_WAVE_CYCLES / (duration * shader clock * 1024 SIMDs).
@@ -54,14 +54,15 @@ def main():
     clock = m["GRBM_GUI_ACTIVE"] / 8 / (sum(gdurs) / len(gdurs) * 1e-9)
     waves = 4 * m["SQ_WAVE_CYCLES"] / (dur_ns * 1e-9 * clock * SIMDS)
     lds_block = int(meta.get("LDS_Block_Size") or meta.get("Lds_Size") or 0)
-    step_name = next((k for k in st if "uniform_kernel" in k and k.split("(")[0].endswith((", 1>", ", 2>"))), None)
+    step_names = [k for k in st if "uniform_kernel" in k and k.split("(")[0].endswith((", 1>", ", 2>"))]
     ko_name = next((k for k in st if "uniform_kernel" in k and k.split("(")[0].endswith(", 0>")), None)
     out = {
         "workload": cfg, "kernel": name.split("(")[0] if name else None,
         "command": "bench.py --config %s --steps 20 --warmup 5 --no-cpu-baseline --no-extra" % cfg,
         "rocprof_stats": {
-            "step_kernel": step_name.split("(")[0] if step_name else None,
-            "step_average_ns": float(st[step_name]["AverageNs"]) if step_name else None,
+            # the step's chunks: sink 2 (packed into the staging slots) and sink 1 (int32 into the pinned arrays)
+            "step_kernels": {k.split("(")[0]: {"calls": int(st[k]["Calls"]), "average_ns": float(st[k]["AverageNs"])}
+                             for k in step_names},
             "kernel_only": ko_name.split("(")[0] if ko_name else None,
             "kernel_only_average_ns": float(st[ko_name]["AverageNs"]) if ko_name else None,
             "bench_roofline_kernel_ms_same_run": bench["roofline"]["kernel_ms"],
