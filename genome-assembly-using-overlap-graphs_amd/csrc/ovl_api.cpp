@@ -15,11 +15,15 @@
 
 #include <emmintrin.h>
 #include <pthread.h>
+#include <sched.h>
 #include <unistd.h>
+
+#include <cctype>
 
 #include <new>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
@@ -74,9 +78,12 @@ struct Knobs {
     int64_t pack_min = 1 << 20;   // OVL_PACK_MIN: packed transport from this many pairs per call
     int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
     int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
-    int32_t pack_direct_pct = 25; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
+    int64_t pack_first = 0;       // OVL_PACK_FIRST: first packed chunk of this many pairs, doubling up to the chunk
+                                  // size (0: equal chunks), so the host expansion starts sooner
+    int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
-                                  // host expands the packed chunks
+                                  // host expands the packed chunks (tools/pack_ab.py, target point, six
+                                  // processes: 0 % 0.16-0.26 ms, 10 % 0.16-0.25, 18 % 0.157-0.226, 25 % 0.175-0.209)
 };
 
 }  // namespace
@@ -544,6 +551,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
+    if (const char* e = getenv("OVL_PACK_FIRST")) k.pack_first = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -574,19 +582,26 @@ class CopyPool {
         }
         const size_t step = (n / parts + 63) & ~size_t(63);
         std::lock_guard<std::mutex> one_call(call_mu_);  // calls from several host threads take turns
-        std::unique_lock<std::mutex> lk(mu_);
-        pending_ = 0;
-        for (size_t i = 1; i < parts; ++i) {
-            const size_t lo = i * step, hi = std::min(n, lo + step);
-            if (lo >= hi) break;
-            tasks_.push_back([&f, lo, hi] { f(lo, hi); });
-            ++pending_;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            size_t k = 0;
+            for (size_t i = 1; i < parts; ++i) {
+                const size_t lo = i * step, hi = std::min(n, lo + step);
+                if (lo >= hi) break;
+                tasks_.push_back([&f, lo, hi] { f(lo, hi); });
+                ++k;
+            }
+            pending_.store(k, std::memory_order_release);
+            queued_.store(tasks_.size(), std::memory_order_release);
         }
-        lk.unlock();
         cv_.notify_all();
         f(0, std::min(step, n));
-        lk.lock();
-        done_.wait(lk, [&] { return pending_ == 0; });
+        // the batch's end: polled for a while (the workers finish within microseconds of the caller), then
+        // a blocking wait
+        if (!spin_until([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
+        }
     }
     // dst[i] = src[i] for [0, bytes)
     void copy(void* dst, const void* src, size_t bytes) {
@@ -609,28 +624,104 @@ class CopyPool {
     CopyPool() : pid_(getpid()) {
         int n = (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = getenv("OVL_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
+        if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_us_ = std::max(0, std::min(100000, atoi(e)));
+        CPU_ZERO(&cpus_);
+        const char* numa = getenv("OVL_POOL_NUMA");
+        if (numa && atoi(numa) == 1) near_gpu_cpus(&cpus_);
         for (int i = 0; i + 1 < n; ++i) {
-            std::thread t([this] { run(); });
+            std::thread t([this] {
+                if (CPU_COUNT(&cpus_) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus_), &cpus_);
+                run();
+            });
             t.detach();  // lives with the process; never joined at exit
             workers_.push_back(0);
         }
     }
+    // The allowed CPUs of the current GPU's NUMA node (sysfs: the device's PCI numa_node and the node's
+    // cpulist, intersected with this process's affinity); empty when unknown.  OVL_POOL_NUMA=1 pins the
+    // workers there, next to the pinned host memory the runtime allocates on that node.  Off by default:
+    // on the 2-socket box (4 GPUs per socket) three processes each way gave the same 0.16-0.26 ms spread.
+    static void near_gpu_cpus(cpu_set_t* out) {
+        CPU_ZERO(out);
+        int dev = 0;
+        char bus[64] = {0};
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+        char path[256];
+        snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+        FILE* f = fopen(path, "r");
+        int node = -1;
+        if (f) {
+            if (fscanf(f, "%d", &node) != 1) node = -1;
+            fclose(f);
+        }
+        if (node < 0) return;
+        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+        f = fopen(path, "r");
+        if (!f) return;
+        cpu_set_t allowed;
+        CPU_ZERO(&allowed);
+        if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) {
+            fclose(f);
+            return;
+        }
+        int lo = 0, hi = 0;
+        char sep = 0;
+        while (fscanf(f, "%d", &lo) == 1) {
+            hi = lo;
+            if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+                if (fscanf(f, "%d", &hi) != 1) break;
+                if (fscanf(f, "%c", &sep) != 1) sep = 0;
+            }
+            for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c)
+                if (CPU_ISSET(c, &allowed)) CPU_SET(c, out);
+            if (sep != ',') break;
+        }
+        fclose(f);
+    }
+    // poll `ready` for up to spin_us_ microseconds
+    template <typename F>
+    bool spin_until(F ready) const {
+        if (ready()) return true;
+        if (spin_us_ <= 0) return false;
+        const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+        for (int i = 1;; ++i) {
+            _mm_pause();
+            if (ready()) return true;
+            if ((i & 31) == 0 && std::chrono::steady_clock::now() > end) return false;
+        }
+    }
+    // a worker polls for work for spin_us_ after its last task (the chunks of one call, and back-to-back
+    // calls, arrive tens of microseconds apart: a condition-variable wake-up per chunk costs about as much),
+    // then sleeps on the condition variable
     void run() {
-        std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            cv_.wait(lk, [&] { return !tasks_.empty(); });
-            auto f = std::move(tasks_.back());
-            tasks_.pop_back();
-            lk.unlock();
+            spin_until([&] { return queued_.load(std::memory_order_acquire) != 0; });
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !tasks_.empty(); });
+                f = std::move(tasks_.back());
+                tasks_.pop_back();
+                queued_.store(tasks_.size(), std::memory_order_release);
+            }
             f();
-            lk.lock();
-            if (--pending_ == 0) done_.notify_all();
+            if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);  // the waiter tests pending_ under mu_: no lost wake-up
+                done_.notify_all();
+            }
         }
     }
     pid_t pid_;
     std::vector<int> workers_;
     std::vector<std::function<void()>> tasks_;
-    size_t pending_ = 0;
+    std::atomic<size_t> queued_{0};   // tasks_.size(), readable without mu_ by polling workers
+    std::atomic<size_t> pending_{0};  // tasks of the current batch not finished yet
+    int spin_us_ = 100;               // OVL_POOL_SPIN_US
+    cpu_set_t cpus_;                  // workers' CPUs (OVL_POOL_NUMA=1: the GPU's NUMA node; else unpinned)
     std::mutex mu_, call_mu_;
     std::condition_variable cv_, done_;
 };
@@ -899,10 +990,22 @@ int setup_job(const Call& C, Job& J) {
     if (C.pack) {
         packed = C.out_pinned ? (n - n * d->k.pack_direct_pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
-        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
-        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
-        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
-        if (packed > 0) J.cb.push_back(packed);
+        if (d->k.pack_first > 0) {
+            // growing chunks: first, 2 first, ... up to J.chunk; a remainder below half a chunk joins the last
+            int64_t c = std::max<int64_t>(64, d->k.pack_first & ~int64_t(63)), o = 0;
+            while (o < packed) {
+                int64_t t = std::min(c, packed - o);
+                if (packed - o - t < c / 2) t = packed - o;
+                o += t;
+                J.cb.push_back(o);
+                c = std::min(2 * c, std::max<int64_t>(64, J.chunk));
+            }
+        } else {
+            const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
+            const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+            for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
+            if (packed > 0) J.cb.push_back(packed);
+        }
         J.n_packed = (int64_t)J.cb.size() - 1;
     }
     for (int64_t o = packed; o < n;) {

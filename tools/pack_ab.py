@@ -1,5 +1,6 @@
 """Packed result transport A/B with the modes interleaved: one engine per setting (env knobs read at context
-creation), the same output arrays (pinned from the pool, pinned coherent / non-coherent, pageable), R rounds of `reps` steps per setting, medians per setting.  Resident
+creation), the same output arrays (pinned from the pool, pageable; PACK_AB_KINDS=1 adds pinned coherent /
+non-coherent), R rounds of `reps` steps per setting, medians per setting.  Resident
 candidate list -> pinned (the bench's step) and pageable arrays.
 
     python tools/pack_ab.py [config] [rounds] [reps]
@@ -13,11 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
 import numpy as np  # noqa: E402
 
-KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
+KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN", "OVL_PACK_FIRST")
 SETTINGS = (("int32", {"OVL_PACK": "0"}),
             ("packed_pct0", {"OVL_PACK_DIRECT_PCT": "0"}),
-            ("packed_pct25", {"OVL_PACK_DIRECT_PCT": "25"}),
-            ("packed_pct35", {"OVL_PACK_DIRECT_PCT": "35"}))
+            ("packed_pct10", {"OVL_PACK_DIRECT_PCT": "10"}),
+            ("packed_pct18", {"OVL_PACK_DIRECT_PCT": "18"}),
+            ("packed_pct25", {"OVL_PACK_DIRECT_PCT": "25"}))
 
 
 def main():
@@ -41,12 +43,13 @@ def main():
         n = eng.enumerate_candidates(CONFIGS[cfg]["k"])
         engines[name] = eng
     outs = {"pinned": (pinned_empty(n), pinned_empty(n))}
-    # pinned arrays of each host-memory kind (ovl_host_alloc reads OVL_HOST_COHERENT per allocation)
-    for kind, v in (("pinned_coherent", "1"), ("pinned_noncoherent", "0")):
-        os.environ["OVL_HOST_COHERENT"] = v
-        pool = PinnedPool()
-        outs[kind] = (pool.empty(n), pool.empty(n))
-        os.environ.pop("OVL_HOST_COHERENT", None)
+    if os.environ.get("PACK_AB_KINDS"):
+        # pinned arrays of each host-memory kind (ovl_host_alloc reads OVL_HOST_COHERENT per allocation)
+        for kind, v in (("pinned_coherent", "1"), ("pinned_noncoherent", "0")):
+            os.environ["OVL_HOST_COHERENT"] = v
+            pool = PinnedPool()
+            outs[kind] = (pool.empty(n), pool.empty(n))
+            os.environ.pop("OVL_HOST_COHERENT", None)
     outs["pageable"] = (np.empty(n, np.int32), np.empty(n, np.int32))
     times = {(s, o): [] for s, _ in SETTINGS for o in outs}
     ref = None
