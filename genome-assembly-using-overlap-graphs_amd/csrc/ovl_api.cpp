@@ -78,8 +78,6 @@ struct Knobs {
     int64_t pack_min = 1 << 20;   // OVL_PACK_MIN: packed transport from this many pairs per call
     int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
     int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
-    int64_t pack_first = 0;       // OVL_PACK_FIRST: first packed chunk of this many pairs, doubling up to the chunk
-                                  // size (0: equal chunks), so the host expansion starts sooner
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -551,7 +549,6 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
-    if (const char* e = getenv("OVL_PACK_FIRST")) k.pack_first = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -990,22 +987,10 @@ int setup_job(const Call& C, Job& J) {
     if (C.pack) {
         packed = C.out_pinned ? (n - n * d->k.pack_direct_pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
-        if (d->k.pack_first > 0) {
-            // growing chunks: first, 2 first, ... up to J.chunk; a remainder below half a chunk joins the last
-            int64_t c = std::max<int64_t>(64, d->k.pack_first & ~int64_t(63)), o = 0;
-            while (o < packed) {
-                int64_t t = std::min(c, packed - o);
-                if (packed - o - t < c / 2) t = packed - o;
-                o += t;
-                J.cb.push_back(o);
-                c = std::min(2 * c, std::max<int64_t>(64, J.chunk));
-            }
-        } else {
-            const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
-            const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
-            for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
-            if (packed > 0) J.cb.push_back(packed);
-        }
+        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
+        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
+        if (packed > 0) J.cb.push_back(packed);
         J.n_packed = (int64_t)J.cb.size() - 1;
     }
     for (int64_t o = packed; o < n;) {

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
 import numpy as np  # noqa: E402
 
-KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN", "OVL_PACK_FIRST")
+KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
 SETTINGS = (("int32", {"OVL_PACK": "0"}),
             ("packed_pct0", {"OVL_PACK_DIRECT_PCT": "0"}),
             ("packed_pct10", {"OVL_PACK_DIRECT_PCT": "10"}),
