@@ -48,6 +48,11 @@ constexpr int32_t kFastMaxLen = 256;   // bit-plane layouts up to W = 8 words of
 constexpr int32_t kDpMaxLen = 8192;    // DP kernel: LDS row of the t read
 constexpr int32_t kLaneMaxLen = 1024;  // lane-per-pair DP: hand-off column buffer per wavefront slot
 constexpr int kSlots = 3;              // pipeline depth: staging slots / events per device
+// Host memory that kernels store into and host code reads within one call (staging slots, the error
+// flag): fine-grained, whose device stores snoop the CPU caches, so a line the host read in an earlier call
+// is never returned stale.  (HIP's default for hipHostMalloc, with HIP_HOST_COHERENT unset, is the
+// coarse-grained kind.)
+constexpr unsigned kHostShared = hipHostMallocPortable | hipHostMallocCoherent;
 
 struct DevBuf {
     void* p = nullptr;
@@ -845,7 +850,7 @@ hipError_t init_dev(Dev* d) {
         }
     e = hipEventCreateWithFlags(&d->scratch_evt, hipEventDisableTiming);
     if (e != hipSuccess) return e;
-    e = hipHostMalloc((void**)&d->h_flag, 64, hipHostMallocDefault);
+    e = hipHostMalloc((void**)&d->h_flag, 64, kHostShared);
     if (e != hipSuccess) return e;
     *d->h_flag = 0;
     e = hipHostGetDevicePointer((void**)&d->h_flag_dev, d->h_flag, 0);
@@ -928,7 +933,7 @@ int64_t pick_chunk(const Dev* d, int64_t n, bool staged, bool direct, bool pack)
 }
 
 hipError_t alloc_staging(int32_t*& p, int32_t*& p_dev, int64_t cap) {
-    hipError_t e = hipHostMalloc((void**)&p, (size_t)kSlots * 2 * (size_t)cap * sizeof(int32_t), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc((void**)&p, (size_t)kSlots * 2 * (size_t)cap * sizeof(int32_t), kHostShared);
     if (e != hipSuccess) return e;
     return hipHostGetDevicePointer((void**)&p_dev, p, 0);
 }
@@ -1145,6 +1150,34 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     return OVL_OK;
 }
 
+// OVL_TRACE_PIPE=1 (diagnostics): one stderr line per host-array call with the microsecond offsets of its
+// pipeline events (s setup, i<k> chunk k issued, w<k> its results ready on the host side, d<k> drained,
+// y final synchronisation).
+struct PipeTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    std::string line;
+    PipeTrace() : on(enabled()), t0(std::chrono::steady_clock::now()) {}
+    static bool enabled() {
+        static const bool e = [] {
+            const char* v = getenv("OVL_TRACE_PIPE");
+            return v && atoi(v) != 0;
+        }();
+        return e;
+    }
+    void mark(char what, int64_t k) {
+        if (!on) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        char buf[48];
+        snprintf(buf, sizeof(buf), " %c%lld=%.1f", what, (long long)k, us);
+        line += buf;
+    }
+    ~PipeTrace() {
+        if (on) fprintf(stderr, "ovl_pipe:%s\n", line.c_str());
+    }
+};
+thread_local PipeTrace* g_trace = nullptr;
+
 // Pageable outputs: copy chunk k out of its staging slot once its results are there (the D2H copy, or in
 // direct mode the kernel that stored them).
 int drain_chunk(const Call& C, Job& J, int64_t k) {
@@ -1154,6 +1187,13 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int64_t n = J.cb[(size_t)k + 1] - off;
     const int slot = (int)(k % kSlots);
     HIPCHK(d, wait_event(d, C.direct ? d->ev_k[slot] : d->ev_out[slot]));
+    if (g_trace) g_trace->mark('w', k);
+    struct Drained {
+        int64_t k;
+        ~Drained() {
+            if (g_trace) g_trace->mark('d', k);
+        }
+    } drained{k};
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
     if (C.pack) {
         host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
@@ -1193,16 +1233,23 @@ struct HostFlag {
 
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
+    PipeTrace trace;
+    g_trace = &trace;
+    struct Unset {
+        ~Unset() { g_trace = nullptr; }
+    } unset;
     int rc = OVL_OK;
     HostFlag host_flag(jobs, C.direct ? 1 : 0);  // (direct chunks set their own sink: issue_chunk_direct)
     for (Job& J : jobs)
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
+    trace.mark('s', 0);
     int64_t maxch = 0;
     for (const Job& J : jobs) maxch = std::max(maxch, J.nchunks);
     for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
             if ((rc = issue_chunk(C, J, k)) != OVL_OK) break;
+            trace.mark('i', k);
             const int64_t j = k - (kSlots - 1);
             if (j >= 0 && chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
         }
@@ -1221,6 +1268,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         HIPCHK(c, hipSetDevice(J.d->device));
         HIPCHK(c, hipStreamSynchronize(C.direct ? J.d->stream : J.d->s_out));
     }
+    trace.mark('y', 0);
     double kms = 0.0;
     for (Job& J : jobs) {
         Dev* d = J.d;
@@ -1382,11 +1430,12 @@ OVL_API int ovl_host_alloc(int64_t bytes, void** out_ptr) {
     if (!out_ptr) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "out_ptr is NULL");
     *out_ptr = nullptr;
     if (bytes < 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "bytes < 0");
-    // OVL_HOST_COHERENT=1 / 0 forces fine-grained (coherent) / coarse-grained host memory (A/B knob);
-    // unset: the HIP runtime's default
-    unsigned flags = hipHostMallocPortable;
+    // fine-grained (coherent) by default: kernels store results into it while host code may hold cached
+    // copies of the same lines (a caller reusing its arrays); OVL_HOST_COHERENT=0 gives the coarse-grained
+    // kind (A/B knob: no difference in step time, profiles/r02_pack_ab_target.json)
+    unsigned flags = hipHostMallocPortable | hipHostMallocCoherent;
     if (const char* e = getenv("OVL_HOST_COHERENT"))
-        flags |= atoi(e) ? hipHostMallocCoherent : hipHostMallocNonCoherent;
+        if (!atoi(e)) flags = hipHostMallocPortable | hipHostMallocNonCoherent;
     HIPCHK((ovl_ctx*)nullptr, hipHostMalloc(out_ptr, (size_t)std::max<int64_t>(bytes, 64), flags));
     return OVL_OK;
 }
