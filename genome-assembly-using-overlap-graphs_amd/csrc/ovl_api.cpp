@@ -15,10 +15,7 @@
 
 #include <emmintrin.h>
 #include <pthread.h>
-#include <sched.h>
 #include <unistd.h>
-
-#include <cctype>
 
 #include <new>
 
@@ -38,6 +35,7 @@
 #include <vector>
 
 #include "ovl.h"
+#include "ovl_expand.h"
 #include "ovl_kernels.h"
 
 #define OVL_API extern "C" __attribute__((visibility("default")))
@@ -627,62 +625,11 @@ class CopyPool {
         int n = (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = getenv("OVL_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_us_ = std::max(0, std::min(100000, atoi(e)));
-        CPU_ZERO(&cpus_);
-        const char* numa = getenv("OVL_POOL_NUMA");
-        if (numa && atoi(numa) == 1) near_gpu_cpus(&cpus_);
         for (int i = 0; i + 1 < n; ++i) {
-            std::thread t([this] {
-                if (CPU_COUNT(&cpus_) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus_), &cpus_);
-                run();
-            });
+            std::thread t([this] { run(); });
             t.detach();  // lives with the process; never joined at exit
             workers_.push_back(0);
         }
-    }
-    // The allowed CPUs of the current GPU's NUMA node (sysfs: the device's PCI numa_node and the node's
-    // cpulist, intersected with this process's affinity); empty when unknown.  OVL_POOL_NUMA=1 pins the
-    // workers there, next to the pinned host memory the runtime allocates on that node.  Off by default:
-    // on the 2-socket box (4 GPUs per socket) three processes each way gave the same 0.16-0.26 ms spread.
-    static void near_gpu_cpus(cpu_set_t* out) {
-        CPU_ZERO(out);
-        int dev = 0;
-        char bus[64] = {0};
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
-            (void)hipGetLastError();
-            return;
-        }
-        for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
-        char path[256];
-        snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
-        FILE* f = fopen(path, "r");
-        int node = -1;
-        if (f) {
-            if (fscanf(f, "%d", &node) != 1) node = -1;
-            fclose(f);
-        }
-        if (node < 0) return;
-        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
-        f = fopen(path, "r");
-        if (!f) return;
-        cpu_set_t allowed;
-        CPU_ZERO(&allowed);
-        if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) {
-            fclose(f);
-            return;
-        }
-        int lo = 0, hi = 0;
-        char sep = 0;
-        while (fscanf(f, "%d", &lo) == 1) {
-            hi = lo;
-            if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
-                if (fscanf(f, "%d", &hi) != 1) break;
-                if (fscanf(f, "%c", &sep) != 1) sep = 0;
-            }
-            for (int c = lo; c <= hi && c < CPU_SETSIZE; ++c)
-                if (CPU_ISSET(c, &allowed)) CPU_SET(c, out);
-            if (sep != ',') break;
-        }
-        fclose(f);
     }
     // poll `ready` for up to spin_us_ microseconds
     template <typename F>
@@ -723,72 +670,23 @@ class CopyPool {
     std::atomic<size_t> queued_{0};   // tasks_.size(), readable without mu_ by polling workers
     std::atomic<size_t> pending_{0};  // tasks of the current batch not finished yet
     int spin_us_ = 100;               // OVL_POOL_SPIN_US
-    cpu_set_t cpus_;                  // workers' CPUs (OVL_POOL_NUMA=1: the GPU's NUMA node; else unpinned)
     std::mutex mu_, call_mu_;
     std::condition_variable cv_, done_;
 };
 
 void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
 
-// Packed results (ovl_kernels.hip put_pair, sink 2) into the caller's int32 arrays.  Per pair one uint16
-// j << 8 | X: score = match*(j - X) + mismatch*X; X = 0xFF: the score is esc[i] (0xFFFF: a bad pair,
-// (-1, -1)).  Eight pairs per step in 16-bit lanes (every int32-key score fits int16, so the wrapping
-// 16-bit products are exact), non-temporal stores where aligned: the arrays are written once and not
-// re-read here, so no read-for-ownership traffic.
-void expand_range(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
-                  bool nt, size_t lo, size_t hi) {
-    auto one = [&](size_t i) {
-        const uint32_t v = pk[i], j = v >> 8, x = v & 0xFFu;
-        if (v == 0xFFFFu) {
-            s[i] = e[i] = -1;
-            return;
-        }
-        s[i] = x == 0xFFu ? esc[i] : match * (int32_t)(j - x) + mismatch * (int32_t)x;
-        e[i] = (int32_t)j;
-    };
-    size_t i = lo;
-    for (; i < hi && ((uintptr_t)(s + i) & 15); ++i) one(i);
-    const bool s_al = nt, e_al = nt && ((uintptr_t)(e + i) & 15) == 0;
-    const __m128i lo8 = _mm_set1_epi16(0xFF), ones = _mm_set1_epi16(-1), zero = _mm_setzero_si128();
-    const __m128i vm = _mm_set1_epi16((int16_t)match), vd = _mm_set1_epi16((int16_t)(mismatch - match));
-    auto put = [](int32_t* p, __m128i v, bool al) {
-        if (al) _mm_stream_si128(reinterpret_cast<__m128i*>(p), v);
-        else _mm_storeu_si128(reinterpret_cast<__m128i*>(p), v);
-    };
-    for (; i + 8 <= hi; i += 8) {
-        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(pk + i));
-        const __m128i x = _mm_and_si128(v, lo8);
-        const __m128i j = _mm_srli_epi16(v, 8);
-        const __m128i bad = _mm_cmpeq_epi16(v, ones);
-        // match*j + (mismatch - match)*X as int16, then sign-extended to int32
-        __m128i sc = _mm_add_epi16(_mm_mullo_epi16(j, vm), _mm_mullo_epi16(x, vd));
-        __m128i s0 = _mm_srai_epi32(_mm_unpacklo_epi16(zero, sc), 16);
-        __m128i s1 = _mm_srai_epi32(_mm_unpackhi_epi16(zero, sc), 16);
-        const __m128i spill = _mm_cmpeq_epi16(x, lo8);  // escaped or bad
-        if (_mm_movemask_epi8(spill)) {
-            alignas(16) int32_t t[8];
-            _mm_store_si128(reinterpret_cast<__m128i*>(t), s0);
-            _mm_store_si128(reinterpret_cast<__m128i*>(t + 4), s1);
-            for (int k = 0; k < 8; ++k)
-                if ((pk[i + k] & 0xFFu) == 0xFFu) t[k] = pk[i + k] == 0xFFFFu ? -1 : esc[i + k];
-            s0 = _mm_load_si128(reinterpret_cast<const __m128i*>(t));
-            s1 = _mm_load_si128(reinterpret_cast<const __m128i*>(t + 4));
-        }
-        put(s + i, s0, s_al);
-        put(s + i + 4, s1, s_al);
-        const __m128i en = _mm_or_si128(j, bad);  // 0xFFFF -> -1 through the high half below
-        put(e + i, _mm_unpacklo_epi16(en, bad), e_al);
-        put(e + i + 4, _mm_unpackhi_epi16(en, bad), e_al);
-    }
-    for (; i < hi; ++i) one(i);
-    _mm_sfence();
-}
-
+// Packed results (ovl_kernels.hip put_pair, sink 2) into the caller's int32 arrays (ovl_expand.h), split
+// over the host pool.  The vector width is the widest this CPU runs unless OVL_EXPAND_ISA names one
+// (scalar, sse2, avx2, avx512; A/B knob).
 void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
                  bool nt, size_t n) {
-    CopyPool::get().parallel(n, size_t(1) << 16, [=](size_t lo, size_t hi) {
-        expand_range(s, e, pk, esc, match, mismatch, nt, lo, hi);
-    });
+    static const ovl_expand::Fn f = [] {
+        const ovl_expand::Fn g = ovl_expand::pick(getenv("OVL_EXPAND_ISA"));
+        return g ? g : ovl_expand::pick(nullptr);
+    }();
+    CopyPool::get().parallel(n, size_t(1) << 16,
+                             [=](size_t lo, size_t hi) { f(s, e, pk, esc, match, mismatch, nt, lo, hi); });
 }
 
 // The pipeline's waits for a chunk: polled (a chunk is tens of microseconds away; a blocking wait can
