@@ -1251,9 +1251,13 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
 // and mismatch counts below the 0xFF marker).  One-device contexts only: the calling thread's host pool
 // expands every packed chunk, so N devices would funnel N links' results through one pool, where int32
 // results take N links in parallel (one process per GPU packs per process).
-bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs) {
+//   From OVL_PACK_MIN pairs into pinned arrays (1 M: below it the int32 stores beat the host hand-off, cfg2
+// 0.039 against 0.056-0.072 ms), from a sixteenth of that into pageable arrays, which need a host pass
+// anyway (cfg2 0.052-0.065 against 0.065-0.079 ms; profiles/r02_pack_ab_cfg2_*.json).
+bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) {
     const Dev* d = c->devs[0];
-    return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= d->k.pack_min &&
+    const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 16;
+    return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= min_pairs &&
            p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
@@ -1588,7 +1592,7 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = c->timing != 0;
     C.direct = c->devs[0]->k.pipe_direct != 0;
-    C.pack = pack_ok(c, p, n_pairs);
+    C.pack = pack_ok(c, p, n_pairs, C.out_pinned);
     const int32_t S = (int32_t)c->devs.size();
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);
@@ -1823,7 +1827,7 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = ctx->timing != 0;
     C.direct = ctx->devs[0]->k.pipe_direct != 0;
-    C.pack = pack_ok(ctx, p, hi - lo);
+    C.pack = pack_ok(ctx, p, hi - lo, C.out_pinned);
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);

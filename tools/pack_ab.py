@@ -32,7 +32,11 @@ def main():
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
     engines = {}
-    for name, env in SETTINGS:
+    settings = SETTINGS
+    if os.environ.get("PACK_AB_MIN0"):  # small lists: packed settings below the default 1 M-pair threshold
+        settings = tuple((nm, dict(env, **({} if env.get("OVL_PACK") == "0" else {"OVL_PACK_MIN": "0"})))
+                         for nm, env in SETTINGS)
+    for name, env in settings:
         for k in KNOBS:
             os.environ.pop(k, None)
         os.environ.update(env)
@@ -51,10 +55,10 @@ def main():
             outs[kind] = (pool.empty(n), pool.empty(n))
             os.environ.pop("OVL_HOST_COHERENT", None)
     outs["pageable"] = (np.empty(n, np.int32), np.empty(n, np.int32))
-    times = {(s, o): [] for s, _ in SETTINGS for o in outs}
+    times = {(s, o): [] for s, _ in settings for o in outs}
     ref = None
     for _ in range(rounds):
-        for name, _ in SETTINGS:
+        for name, _ in settings:
             eng = engines[name]
             for oname, out in outs.items():
                 for _ in range(3):
