@@ -440,6 +440,19 @@ def test_sharded_paths_on_rccl_world1(nccl_world1, engine, cfg2, cfg2_ref):
             np.testing.assert_array_equal(got[0], ref[0])
             np.testing.assert_array_equal(got[1], ref[1])
     keep.close()
+    # packed results (OVL_PACK_MIN=0: below the default threshold) expanded into the registered shared buffer
+    packed = _engine_env({"OVL_PACK_MIN": "0"})
+    try:
+        st = ShardedStep(reads, engine=packed, dest="host", k=5)
+        st.step()
+        st.step()
+        assert packed.last_transfer()["packed_pairs"] > 0
+        got = st.results()
+        st.close()
+        np.testing.assert_array_equal(got[0], cfg2_ref[0])
+        np.testing.assert_array_equal(got[1], cfg2_ref[1])
+    finally:
+        packed.close()
 
 
 def test_lane_kernel_on_two_streams(oracle_mod, cfg2):
