@@ -562,7 +562,7 @@ Knobs read_knobs() {
 // Host copies between pageable caller arrays and the pinned staging rings, split over a few worker threads
 // (one thread copies ~10 GB/s; a 16 MB result column is ~1.5 ms alone).  The pool is created on first
 // use in each process (a forked joblib worker builds its own) and sized by OVL_HOST_THREADS (default:
-// min(8, hardware threads)).
+// min(12, hardware threads)).
 class CopyPool {
   public:
     static CopyPool& get() {
@@ -622,7 +622,9 @@ class CopyPool {
         pool_ = nullptr;
     }
     CopyPool() : pid_(getpid()) {
-        int n = (int)std::min<unsigned>(8u, std::max(1u, std::thread::hardware_concurrency()));
+        // 12 by default: three processes each of 6 / 8 / 12 threads on the box (a 16-CPU share), packed step
+        // 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms (profiles/r02_pool_threads_*.json)
+        int n = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
         if (const char* e = getenv("OVL_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
         if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_us_ = std::max(0, std::min(100000, atoi(e)));
         for (int i = 0; i + 1 < n; ++i) {
