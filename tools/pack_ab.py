@@ -17,9 +17,8 @@ import numpy as np  # noqa: E402
 KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
 SETTINGS = (("int32", {"OVL_PACK": "0"}),
             ("packed_pct10", {"OVL_PACK_DIRECT_PCT": "10"}),
-            ("packed_pct14", {"OVL_PACK_DIRECT_PCT": "14"}),
             ("packed_pct18", {"OVL_PACK_DIRECT_PCT": "18"}),
-            ("packed_pct22", {"OVL_PACK_DIRECT_PCT": "22"}))
+            ("packed_pct25", {"OVL_PACK_DIRECT_PCT": "25"}))
 
 
 def main():
