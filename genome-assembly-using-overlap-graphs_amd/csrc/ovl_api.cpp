@@ -565,6 +565,7 @@ Knobs read_knobs() {
 // min(12, hardware threads)).
 class CopyPool {
   public:
+    static int threads() { return planned_threads(); }
     static CopyPool& get() {
         static const int registered = pthread_atfork(nullptr, nullptr, &CopyPool::after_fork);
         (void)registered;
@@ -621,11 +622,29 @@ class CopyPool {
         new (&get_mutex()) std::mutex();
         pool_ = nullptr;
     }
+    // Threads of the pool (the calling thread included): OVL_HOST_THREADS, else 12 (three processes each of
+    // 6 / 8 / 12 threads on the box, a 16-CPU share: packed step 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms,
+    // profiles/r02_pool_threads_*.json), capped by the hardware threads and by this process's part of the
+    // job's CPU quota (cgroup cpu.max divided over LOCAL_WORLD_SIZE ranks, one CPU left for the rank's own
+    // thread), at least 1.
+    static int planned_threads() {
+        static const int n = [] {
+            if (const char* e = getenv("OVL_HOST_THREADS")) return std::max(1, std::min(64, atoi(e)));
+            int t = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
+            long long quota = 0, period = 0;
+            if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+                if (fscanf(f, "%lld %lld", &quota, &period) != 2) quota = period = 0;  // "max ..." stays 0
+                fclose(f);
+            }
+            int ranks = 1;
+            if (const char* e = getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, atoi(e));
+            if (quota > 0 && period > 0) t = std::min<int>(t, (int)(quota / period / ranks) - 1);
+            return std::max(1, t);
+        }();
+        return n;
+    }
     CopyPool() : pid_(getpid()) {
-        // 12 by default: three processes each of 6 / 8 / 12 threads on the box (a 16-CPU share), packed step
-        // 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms (profiles/r02_pool_threads_*.json)
-        int n = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
-        if (const char* e = getenv("OVL_HOST_THREADS")) n = std::max(1, std::min(64, atoi(e)));
+        const int n = planned_threads();
         if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_us_ = std::max(0, std::min(100000, atoi(e)));
         for (int i = 0; i + 1 < n; ++i) {
             std::thread t([this] { run(); });
@@ -1259,7 +1278,9 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
 bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) {
     const Dev* d = c->devs[0];
     const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 16;
-    return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= min_pairs &&
+    // (the expansion needs the host pool: with fewer than 6 threads, e.g. many ranks on one CPU quota, the
+    // int32 stores over the link are faster)
+    return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
            p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
