@@ -8,7 +8,7 @@ pair's (score, end) in host memory: the ABI call ``ovl_score_candidates`` runs t
 kernels, which store their results over the link into host memory -- packed (end and
 mismatch count, 2 B per pair) for the first chunks, which host threads expand into the
 caller's pinned int32 arrays while the next chunks score, and as int32 straight into
-those arrays for the last 18 % of the pairs.
+those arrays for the last ~20 % of the pairs (the share adapts per call).
 
     python bench.py [--gpus 1 --steps K --warmup W --config target]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -658,7 +658,7 @@ def main() -> None:
             "read_length": w.cfg["l"],
             "step": "ovl_score_candidates: resident reads + device-enumerated list -> kernels storing over the "
                     "link -> (score, end) in pinned host int32 arrays (SURVEY.md §8d, results in host memory; "
-                    "packed 2 B/pair chunks expanded by host threads, the last 18 % stored directly)",
+                    "packed 2 B/pair chunks expanded by host threads, the last ~20 % stored directly)",
             "parallelism": "1 GPU",
             "kernel": w.kernel,
             "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},

@@ -81,6 +81,8 @@ struct Knobs {
     int64_t pack_min = 1 << 20;   // OVL_PACK_MIN: packed transport from this many pairs per call
     int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
     int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
+    int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
+                                  // OVL_PACK_DIRECT_PCT fixes it
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -126,6 +128,8 @@ struct Dev {
     DevBuf lane_col;      // lane-per-pair DP: per-wavefront strip hand-off columns
     DevBuf seed_s, seed_e;  // band knob: the ungapped seed (score, j*) of each pair
     hipEvent_t scratch_evt = nullptr;     // last launch that used lane_col / seed_* ...
+    hipEvent_t ev_last = nullptr;         // packed calls into pinned arrays: after the last (direct) chunk
+    double pack_pct = -1.0;               // live direct share of packed calls into pinned arrays (pack_share)
     hipStream_t scratch_stream = nullptr; // ... and its stream (launches on other streams wait for it)
     bool scratch_used = false;
     int64_t codes_bytes = 0;
@@ -551,7 +555,10 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
+    if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
+        k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
+        k.pack_adapt = 0;  // a fixed share
+    }
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -747,6 +754,7 @@ void destroy_dev(Dev* d) {
     for (hipEvent_t e : d->t_ev)
         if (e) (void)hipEventDestroy(e);
     if (d->scratch_evt) (void)hipEventDestroy(d->scratch_evt);
+    if (d->ev_last) (void)hipEventDestroy(d->ev_last);
     for (hipStream_t s : {d->stream, d->s_in, d->s_out})
         if (s) (void)hipStreamDestroy(s);
     delete d;
@@ -768,6 +776,8 @@ hipError_t init_dev(Dev* d) {
             if (e != hipSuccess) return e;
         }
     e = hipEventCreateWithFlags(&d->scratch_evt, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    e = hipEventCreateWithFlags(&d->ev_last, hipEventDisableTiming);
     if (e != hipSuccess) return e;
     e = hipHostMalloc((void**)&d->h_flag, 64, kHostShared);
     if (e != hipSuccess) return e;
@@ -909,7 +919,9 @@ int setup_job(const Call& C, Job& J) {
     // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
     if (C.pack) {
-        packed = C.out_pinned ? (n - n * d->k.pack_direct_pct / 100) & ~int64_t(63) : n;
+        if (d->pack_pct < 0.0) d->pack_pct = d->k.pack_direct_pct;
+        const int64_t pct = d->k.pack_adapt ? (int64_t)(d->pack_pct + 0.5) : d->k.pack_direct_pct;
+        packed = C.out_pinned ? (n - n * pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
         const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
         const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
@@ -1010,6 +1022,8 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     if (rc != OVL_OK) return rc;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
     if (staged_in || staged_out) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
+    if (C.pack && C.out_pinned && J.n_packed < J.nchunks && k == J.nchunks - 1)
+        HIPCHK(d, hipEventRecord(d->ev_last, d->stream));
     return OVL_OK;
 }
 
@@ -1181,6 +1195,22 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     if (rc != OVL_OK) {
         quiesce(jobs);
         return rc;
+    }
+    // pack_share: the direct share of packed calls into pinned arrays follows which side finished last.  The
+    // host pool has expanded every packed chunk now; if the direct chunk is already done, the link idled
+    // while the host worked (more direct), if the host still waits for it, the host idles (more packed).
+    for (Job& J : jobs) {
+        Dev* d = J.d;
+        if (!C.pack || !C.out_pinned || J.n_packed >= J.nchunks || !d->k.pack_adapt) continue;
+        const auto tw = std::chrono::steady_clock::now();
+        const hipError_t q = hipEventQuery(d->ev_last);
+        if (q == hipSuccess) {
+            d->pack_pct = std::min(50.0, d->pack_pct + 1.0);
+        } else if (q == hipErrorNotReady) {
+            HIPCHK(c, wait_event(d, d->ev_last));
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
+            if (us > 8.0) d->pack_pct = std::max(2.0, d->pack_pct - 1.0);
+        }
     }
     for (Job& J : jobs) {
         if (J.nchunks == 0) continue;

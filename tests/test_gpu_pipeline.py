@@ -162,6 +162,29 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, pct, c
         eng.close()
 
 
+def test_packed_adaptive_share(oracle_mod, cfg2, cfg2_ref):
+    """The direct share of packed calls into pinned arrays adapts call by call (no OVL_PACK_DIRECT_PCT):
+    every call's results stay exact and the packed part stays within its bounds (50-98 % of the pairs)."""
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = cfg2
+    eng = _engine_env({"OVL_PACK_MIN": "0"})
+    try:
+        eng.set_reads(reads)
+        eng.candidates(5)
+        n = a.shape[0]
+        out = (pinned_empty(n), pinned_empty(n))
+        shares = []
+        for _ in range(30):
+            out[0][:] = -9
+            eng.score_candidates(out=out)
+            np.testing.assert_array_equal(out[0], cfg2_ref[0])
+            np.testing.assert_array_equal(out[1], cfg2_ref[1])
+            shares.append(eng.last_transfer()["packed_pairs"] / n)
+        assert all(0.49 <= x <= 0.99 for x in shares), shares
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("l", [254, 255])
 @pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
 def test_packed_results_at_the_length_limit(oracle_mod, l, scoring):

@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 
 KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
 SETTINGS = (("int32", {"OVL_PACK": "0"}),
-            ("packed_pct10", {"OVL_PACK_DIRECT_PCT": "10"}),
+            ("packed_adaptive", {}),
             ("packed_pct18", {"OVL_PACK_DIRECT_PCT": "18"}),
             ("packed_pct25", {"OVL_PACK_DIRECT_PCT": "25"}))
 
@@ -55,6 +55,7 @@ def main():
             os.environ.pop("OVL_HOST_COHERENT", None)
     outs["pageable"] = (np.empty(n, np.int32), np.empty(n, np.int32))
     times = {(s, o): [] for s, _ in settings for o in outs}
+    shares = {}
     ref = None
     for _ in range(rounds):
         for name, _ in settings:
@@ -66,6 +67,8 @@ def main():
                 for _ in range(reps):
                     eng.score_candidates(out=out)
                 times[(name, oname)].append((time.perf_counter() - t0) / reps * 1e3)
+                if oname == "pinned":
+                    shares[name] = eng.last_transfer()["packed_pairs"] / n
                 if ref is None:
                     ref = (out[0].copy(), out[1].copy())
                 assert np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]), (name, oname)
@@ -74,6 +77,8 @@ def main():
         res.setdefault(name, {})[oname] = {"median_ms": round(float(np.median(v)), 4),
                                            "min_ms": round(float(np.min(v)), 4),
                                            "max_ms": round(float(np.max(v)), 4)}
+    for name, v in shares.items():
+        res[name]["packed_share_pinned"] = round(v, 3)
     for eng in engines.values():
         eng.close()
     print(json.dumps(res))
