@@ -78,7 +78,7 @@ struct Knobs {
                                   // and storing host memory through its device mapping (A/B knob)
     int32_t pack = 1;             // OVL_PACK=0: host-array results cross the link as int32 pairs even when the
                                   // packed form (2 bytes per pair) holds (A/B knob)
-    int64_t pack_min = 1 << 20;   // OVL_PACK_MIN: packed transport from this many pairs per call
+    int64_t pack_min = 1 << 18;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
     int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
     int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
@@ -1302,12 +1302,13 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
 // and mismatch counts below the 0xFF marker).  One-device contexts only: the calling thread's host pool
 // expands every packed chunk, so N devices would funnel N links' results through one pool, where int32
 // results take N links in parallel (one process per GPU packs per process).
-//   From OVL_PACK_MIN pairs into pinned arrays (1 M: below it the int32 stores beat the host hand-off, cfg2
-// 0.039 against 0.056-0.072 ms), from a sixteenth of that into pageable arrays, which need a host pass
-// anyway (cfg2 0.052-0.065 against 0.065-0.079 ms; profiles/r02_pack_ab_cfg2_*.json).
+//   From OVL_PACK_MIN pairs into pinned arrays (256 K: tools/pack_size_ab.py, first n pairs of the target
+// list, int32 / packed ms: 131 K 0.040 / 0.041, 262 K 0.065 / 0.057, 524 K 0.099 / 0.082, 1 M 0.182 / 0.100),
+// from a quarter of that into pageable arrays, which need a host pass anyway (cfg2, 122 K pairs: 0.052-0.065
+// against 0.065-0.079 ms; profiles/r02_pack_ab_cfg2_*.json, profiles/r02_pack_size_*.json).
 bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) {
     const Dev* d = c->devs[0];
-    const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 16;
+    const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 4;
     // (the expansion needs the host pool: with fewer than 6 threads, e.g. many ranks on one CPU quota, the
     // int32 stores over the link are faster)
     return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
