@@ -5,12 +5,16 @@
 // of the resident read store (codes + bit-plane layouts in HBM), scratch for
 // host-array calls, pinned staging rings and the device error flag.  Host-array
 // scoring calls shard the pair list over the devices (contiguous ranges balanced
-// by sum n*m) and run a chunked pipeline per device: H2D of chunk
-// k+1, the kernel on chunk k and the D2H of chunk k-1 overlap, and results land
-// directly in the caller's arrays when they are pinned (else through pinned
-// staging).  Kernel choice per call (ovl_plan): the ungapped popcount kernel
-// whenever gaps provably cannot win and the read store has a bit-plane layout,
-// else a DP kernel.  Never falls back to the CPU.
+// by sum n*m) and run a chunked pipeline per device (run_pipeline).
+// In direct mode (the default) the kernels read host pair lists and store results
+// through host mappings: packed (2 bytes per pair, Call::pack) into staging slots
+// that the host pool expands into the caller's int32 arrays while the next chunk
+// scores, with a last share of the pairs stored as int32 straight into pinned
+// arrays; otherwise as int32 into the caller's pinned arrays or staging slots.
+// Copy-engine mode (OVL_PIPE_DIRECT=0) overlaps H2D, kernel and D2H instead.
+// Kernel choice per call (ovl_plan): the ungapped popcount kernel whenever gaps
+// provably cannot win and the read store has a bit-plane layout, else a DP kernel.
+// Never falls back to the CPU.
 #include <hip/hip_runtime.h>
 
 #include <emmintrin.h>
