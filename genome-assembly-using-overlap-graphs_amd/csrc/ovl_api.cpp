@@ -85,6 +85,7 @@ struct Knobs {
     int64_t pack_min = 1 << 18;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
     int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
     int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
+    int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
@@ -140,6 +141,11 @@ struct Dev {
     // device candidate enumeration (ovl_candidates): per-read keys / groups and the pair list
     DevBuf k_pre, k_suf, k_sorted, k_iota, k_order, k_lo, k_hi, k_cnt, k_offs, k_temp, cand_a, cand_b;
     int64_t cand_n = -1;  // -1: no candidate list for the resident reads
+    // heavy tiles of the candidate list (tiles holding side pairs, scheduled first: uniform_kernel), built on
+    // the first throughput-mode launch over the list (ensure_heavy)
+    DevBuf tile_flags, heavy_ids;
+    std::vector<int32_t> h_heavy;
+    int64_t heavy_for = -1;  // cand_n the heavy tiles were built for (-1: none)
     int64_t cand_tail[2] = {0, 0};
     DevBuf sh_cum, sh_temp, sh_cuts;  // shard bounds (ovl_candidates_shards)
     // local alignment (ovl_local_align): query / reference bytes, carried rows, progress, traceback
@@ -363,6 +369,28 @@ int launch_score(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b,
     return OVL_OK;
 }
 
+// The candidate list's heavy tiles (flags per list tile on the device, ascending ids on host and device),
+// once per list; waits for the list's stream.
+int ensure_heavy(Dev* c) {
+    if (c->heavy_for == c->cand_n) return OVL_OK;
+    const int64_t n_tiles = (c->cand_n + 63) / 64;
+    HIPCHK(c, ensure(c->tile_flags, (size_t)std::max<int64_t>(n_tiles, 1)));
+    HIPCHK(c, ovl_launch_tile_flags(as<int32_t>(c->cand_a), c->cand_n, as<uint32_t>(c->full), c->n_reads,
+                                    as<uint8_t>(c->tile_flags), c->stream));
+    std::vector<uint8_t> f((size_t)n_tiles);
+    HIPCHK(c, hipMemcpyAsync(f.data(), c->tile_flags.p, (size_t)n_tiles, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->h_heavy.clear();
+    for (int64_t t = 0; t < n_tiles; ++t)
+        if (f[(size_t)t]) c->h_heavy.push_back((int32_t)t);
+    HIPCHK(c, ensure(c->heavy_ids, sizeof(int32_t) * std::max<size_t>(c->h_heavy.size(), 1)));
+    if (!c->h_heavy.empty())
+        HIPCHK(c, hipMemcpy(c->heavy_ids.p, c->h_heavy.data(), sizeof(int32_t) * c->h_heavy.size(),
+                            hipMemcpyHostToDevice));
+    c->heavy_for = c->cand_n;
+    return OVL_OK;
+}
+
 int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s) {
@@ -418,6 +446,22 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
         g.host_out = c->out_mode;
+        // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
+        const int32_t* ca = as<int32_t>(c->cand_a);
+        if (c->k.heavy_first && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
+            d_a < ca + c->cand_n && d_b == as<int32_t>(c->cand_b) + (d_a - ca) && (d_a - ca) % 64 == 0) {
+            int rc = ensure_heavy(c);
+            if (rc != OVL_OK) return rc;
+            const int64_t t0 = (d_a - ca) / 64, t1 = t0 + (n_pairs + 63) / 64;
+            const auto k0 = std::lower_bound(c->h_heavy.begin(), c->h_heavy.end(), t0);
+            const auto k1 = std::lower_bound(c->h_heavy.begin(), c->h_heavy.end(), t1);
+            if (k1 > k0) {
+                g.heavy_ids = as<int32_t>(c->heavy_ids) + (k0 - c->h_heavy.begin());
+                g.heavy_n = (int32_t)(k1 - k0);
+                g.tile_flags = as<uint8_t>(c->tile_flags);
+                g.tile_base = t0;
+            }
+        }
         HIPCHK(c, ovl_launch_ungapped(&g, s));
     } else {
         OvlDpArgs g{};
@@ -559,6 +603,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_HEAVY_FIRST")) k.heavy_first = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
         k.pack_adapt = 0;  // a fixed share
@@ -746,7 +791,7 @@ void destroy_dev(Dev* d) {
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
                       &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
                       &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
-                      &d->lane_col, &d->seed_s, &d->seed_e})
+                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids})
         release(*b);
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
@@ -1493,6 +1538,7 @@ hipError_t upload_reads(Dev* d, const HostReads& h) {
     if (e != hipSuccess) return e;
     d->n_reads = -1;  // invalid until fully built
     d->cand_n = -1;
+    d->heavy_for = -1;
     const int32_t n_reads = h.n_reads;
     if ((e = ensure(d->off, sizeof(int64_t) * h.off.size())) != hipSuccess) return e;
     if ((e = ensure(d->len, sizeof(int32_t) * h.len.size())) != hipSuccess) return e;
@@ -1541,6 +1587,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     for (Dev* d : c->devs) {
         d->n_reads = -1;
         d->cand_n = -1;
+        d->heavy_for = -1;
     }
     // upload to every device, then wait for all (the uploads and packs overlap across devices)
     for (Dev* d : c->devs)
@@ -1734,6 +1781,7 @@ namespace {
 int cand_count(Dev* c, int32_t k) {
     HIPCHK(c, hipSetDevice(c->device));
     c->cand_n = -1;
+    c->heavy_for = -1;
     const int32_t n = c->n_reads;
     const size_t nr = (size_t)std::max(n, 1);
     const int all = k == 0 ? 1 : 0;
@@ -1815,7 +1863,10 @@ OVL_API int ovl_candidates(ovl_ctx* ctx, int32_t k, int64_t* out_n_pairs) {
     }
     if (rc != OVL_OK) return rc;
     const int64_t total = d0->cand_tail[0] + d0->cand_tail[1];
-    for (Dev* d : ctx->devs) d->cand_n = total;
+    for (Dev* d : ctx->devs) {
+        d->cand_n = total;
+        d->heavy_for = -1;  // a new list: heavy tiles rebuilt on its first launch
+    }
     *out_n_pairs = total;
     return OVL_OK;
 }

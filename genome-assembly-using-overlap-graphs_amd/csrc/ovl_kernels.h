@@ -30,6 +30,10 @@ struct OvlUngappedArgs {
     int32_t lw;          // dominant read length for uniform_kernel (0: general kernel only)
     const uint32_t* full; // bit r set iff len[r] == lw
     int64_t max_blocks;  // grid cap (grid-stride beyond it)
+    const int32_t* heavy_ids;   // throughput mode over a resident candidate list: heavy tiles first (list tile
+    const uint8_t* tile_flags;  // ids, ascending; per-list-tile flags); null: natural order
+    int32_t heavy_n;            // heavy tiles of this launch: heavy_ids[0 .. heavy_n)
+    int64_t tile_base;          // the launch's first pair / 64 within the list
     int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
                          // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
                          // out_score as uint16, the score of the few pairs that need it in out_end
@@ -73,6 +77,9 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
                                       int32_t n_reads, int32_t w, int32_t srow, int32_t trow, uint32_t* sfx,
                                       uint32_t* pfx, hipStream_t stream);
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* args, hipStream_t stream);
+// flags[t] = 1 iff tile t of the pair list holds a pair whose read a is shorter than the dominant length
+extern "C" hipError_t ovl_launch_tile_flags(const int32_t* a_idx, int64_t n_pairs, const uint32_t* full,
+                                            int32_t n_reads, uint8_t* flags, hipStream_t stream);
 
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);
 extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out);

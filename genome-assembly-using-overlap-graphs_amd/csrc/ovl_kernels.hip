@@ -636,7 +636,9 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
     int32_t lw, const uint32_t* __restrict__ full, int32_t match, int32_t mismatch,
-    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag) {
+    int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag,
+    const int32_t* __restrict__ heavy_ids, const uint8_t* __restrict__ tile_flags, int32_t heavy_n,
+    int64_t tile_base) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
@@ -683,10 +685,25 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     }
     OVL_TR_CLOCK(0, lane);
 #endif
-    for (int64_t base = (int64_t)blockIdx.x * G; base < n_tiles; base += (int64_t)gridDim.x * G) {
-        const int64_t tile = base + grp;
+    // Heavy tiles first (throughput mode, a resident candidate list): the tiles holding side pairs cost up to
+    // ~2.6x a uniform tile (their ring drains), and one landing in the last round of wavefronts is the
+    // launch's tail.  Work item i < heavy_n is heavy tile heavy_ids[i] (ids in list tiles, this launch's
+    // tiles start at tile_base); item heavy_n + t is tile t, skipped when it is heavy (done already).
+    const bool hf = !LAT && heavy_ids != nullptr;
+    const int64_t n_items = hf ? n_tiles + heavy_n : n_tiles;
+    for (int64_t base = (int64_t)blockIdx.x * G; base < n_items; base += (int64_t)gridDim.x * G) {
+        const int64_t item = base + grp;  // wave-uniform
+        int64_t tile = item;
+        if (hf) {
+            if (item < heavy_n) {
+                tile = (int64_t)heavy_ids[item] - tile_base;
+            } else {
+                tile = item - heavy_n;
+                if (tile < n_tiles && tile_flags[tile_base + tile]) continue;  // wave-uniform skip
+            }
+        }
         const int64_t p = tile * 64 + lane;
-        const bool mine = tile < n_tiles && p < n_pairs;
+        const bool mine = item < n_items && tile < n_tiles && p < n_pairs;
         int32_t a = mine ? a_idx[p] : 0;
         int32_t b = mine ? b_idx[p] : 0;
         const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
@@ -1328,7 +1345,8 @@ template <int W, int KM, bool LAT, int OM>
 static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
     uniform_kernel<W, KM, LAT, OM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
                                                                 g.n_pairs, g.lw, g.full, g.match, g.mismatch,
-                                                                g.out_score, g.out_end, g.err_flag);
+                                                                g.out_score, g.out_end, g.err_flag, g.heavy_ids,
+                                                                g.tile_flags, g.heavy_n, g.tile_base);
 }
 
 template <int W, int KM, bool LAT>
@@ -1410,13 +1428,43 @@ static unsigned grid_for(int64_t pairs, int rs_log2, int64_t max_blocks) {
 
 // Uniform path (P = 2 and a dominant read length lw): uniform_kernel, which also
 // scores the other pairs through its LDS side ring.  Otherwise general_kernel.
+// flags[t] = 1 iff tile t (pairs 64t .. 64t + 63) holds a pair whose read a is not of the dominant length
+// (a side pair of uniform_kernel's ring); one wavefront per tile
+__global__ __launch_bounds__(256) void tile_flags_kernel(const int32_t* __restrict__ a_idx, int64_t n_pairs,
+                                                         const uint32_t* __restrict__ full, int32_t n_reads,
+                                                         uint8_t* __restrict__ flags) {
+    const int64_t n_tiles = (n_pairs + 63) >> 6;
+    const int lane = threadIdx.x & 63;
+    for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < n_tiles; t += (int64_t)gridDim.x * 4) {
+        const int64_t p = t * 64 + lane;
+        bool side = false;
+        if (p < n_pairs) {
+            const int32_t a = a_idx[p];
+            side = a >= 0 && a < n_reads && !((full[a >> 5] >> (a & 31)) & 1u);
+        }
+        const uint64_t m = __ballot(side);
+        if (lane == 0) flags[t] = m ? 1 : 0;
+    }
+}
+
+extern "C" hipError_t ovl_launch_tile_flags(const int32_t* a_idx, int64_t n_pairs, const uint32_t* full,
+                                            int32_t n_reads, uint8_t* flags, hipStream_t stream) {
+    const int64_t n_tiles = (n_pairs + 63) >> 6;
+    if (n_tiles <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n_tiles + 3) / 4, 8192);
+    tile_flags_kernel<<<(unsigned)blocks, 256, 0, stream>>>(a_idx, n_pairs, full, n_reads, flags);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->host_out == 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
     if (g->lw > 0) {
         // rs_log2 > 0 here selects the latency mode
-        const unsigned nb = grid_for(g->n_pairs << (g->rs_log2 > 0 ? 1 : 0), 0, g->max_blocks);
+        const unsigned nb = grid_for((g->n_pairs << (g->rs_log2 > 0 ? 1 : 0)) +
+                                         (g->heavy_ids && g->rs_log2 == 0 ? 64 * (int64_t)g->heavy_n : 0),
+                                     0, g->max_blocks);
         ok = g->key64 ? dispatch_uniform<1>(*g, nb, stream) : dispatch_uniform<0>(*g, nb, stream);
     } else {
         const unsigned nb = grid_for(g->n_pairs, g->rs_log2, g->max_blocks);
