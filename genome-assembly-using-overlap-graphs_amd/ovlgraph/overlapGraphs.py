@@ -358,20 +358,9 @@ def construct_string_graph(reads, engine: Optional[OverlapEngine] = None, scorer
     return G
 
 
-def remove_cycles_from_graph(overlap_graph):
-    """Remove the weakest edge of the first cycle networkx's ``find_cycle`` reports until the
-    graph is a DAG (overlapGraphs.py:106-130), in place; returns the graph.
-
-    Removes exactly the reference's edges (same cycles, same ``weight`` minimum, first in cycle
-    order on ties), in the same order, by replaying its DFS in ``ovl_remove_cycles`` (C++,
-    csrc/ovl_graph.cpp).  ``weight`` must be an integer on every edge.
-    """
-    from . import _lib
-    import ctypes
-    G = overlap_graph
-    nodes = list(G)
+def _csr_python(nodes, adj):
+    """The successor lists as CSR (node order, adjacency order within a node) -- Python passes."""
     index = {v: i for i, v in enumerate(nodes)}
-    adj = G._adj
     deg = np.fromiter((len(adj[u]) for u in nodes), dtype=np.int64, count=len(nodes))
     off = np.zeros(len(nodes) + 1, dtype=np.int64)
     np.cumsum(deg, out=off[1:])
@@ -381,18 +370,68 @@ def remove_cycles_from_graph(overlap_graph):
     if not all(isinstance(w, (int, np.integer)) and not isinstance(w, bool) for w in wlist):
         raise TypeError("remove_cycles_from_graph needs an integer 'weight' on every edge")
     weights = np.array(wlist, dtype=np.int64) if wlist else np.zeros(0, dtype=np.int64)
+    return off, heads, weights
+
+
+def remove_cycles_from_graph(overlap_graph, native_edges: Optional[bool] = None, timing: Optional[dict] = None):
+    """Remove the weakest edge of the first cycle networkx's ``find_cycle`` reports until the
+    graph is a DAG (overlapGraphs.py:106-130), in place; returns the graph.
+
+    Removes exactly the reference's edges (same cycles, same ``weight`` minimum, first in cycle
+    order on ties), in the same order, by replaying its DFS in ``ovl_remove_cycles`` (C++,
+    csrc/ovl_graph.cpp).  ``weight`` must be an integer on every edge.
+
+    The per-edge passes around the replay -- the successor lists as CSR, and the removals
+    (``del succ[u][v]; del pred[v][u]`` per edge, as ``DiGraph.remove_edge``, one cache clear at the
+    end) -- run in the C extension (csrc/ovl_digraph.c) when it is built (``native_edges=None``;
+    True: required; False: Python passes).  ``timing``: a dict that receives the stage times (s).
+    """
+    import ctypes
+    import time
+    from . import _lib
+    G = overlap_graph
+    t0 = time.perf_counter()
+    nodes = list(G)
+    adj = G._adj
+    mod = _digraph() if native_edges is not False else None
+    if native_edges and mod is None:
+        raise RuntimeError("ovlgraph._digraph is not built (make -C genome-assembly-using-overlap-graphs_amd/csrc)")
+    # the C passes need networkx's own DiGraph (plain dicts; remove_edge not overridden)
+    got = mod.csr(nodes, adj, np.integer) if mod is not None and type(G) is nx.DiGraph and type(adj) is dict else None
+    if got is not None:
+        boff, bheads, bw = got
+        off = np.frombuffer(boff, dtype=np.int64)
+        n_edges = int(off[-1])
+        heads = np.frombuffer(bheads, dtype=np.int32, count=n_edges)
+        weights = np.frombuffer(bw, dtype=np.int64, count=n_edges)
+    else:
+        mod = None
+        off, heads, weights = _csr_python(nodes, adj)
+        n_edges = int(off[-1])
+    t1 = time.perf_counter()
     removed = np.zeros(max(n_edges, 1), dtype=np.int64)
     n_removed = ctypes.c_int64(0)
     L = _lib.load()
     _lib.check(L.ovl_remove_cycles(off.ctypes.data_as(ctypes.c_void_p), heads.ctypes.data_as(ctypes.c_void_p),
                                    weights.ctypes.data_as(ctypes.c_void_p), len(nodes),
                                    removed.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n_removed)))
+    t2 = time.perf_counter()
     if n_removed.value:
         # CSR index -> (u, v): the tail is the node whose adjacency range holds the index
         idx = removed[: n_removed.value]
         tails = np.searchsorted(off, idx, side="right") - 1
-        for t, e in zip(tails.tolist(), idx.tolist()):
-            G.remove_edge(nodes[t], nodes[heads[e]])
+        if mod is not None:
+            try:
+                mod.remove_edges(G._succ, G._pred, nodes, np.ascontiguousarray(tails, np.int64),
+                                 heads[idx].astype(np.int64))
+            finally:
+                nx._clear_cache(G)
+        else:
+            for t, e in zip(tails.tolist(), idx.tolist()):
+                G.remove_edge(nodes[t], nodes[heads[e]])
+    t3 = time.perf_counter()
+    if timing is not None:
+        timing.update(csr=t1 - t0, replay=t2 - t1, remove=t3 - t2, removed=int(n_removed.value))
     return G
 
 

@@ -170,3 +170,60 @@ def test_abi_rejects_bad_csr():
     assert L.ovl_remove_cycles(p(off), p(head), p(w), 2, p(rem), ctypes.byref(n)) < 0
     head = np.array([1, 0], dtype=np.int32)
     assert L.ovl_remove_cycles(p(off), p(head), p(w), 2, p(rem), ctypes.byref(n)) == 0 and n.value == 1
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_native_edge_passes_match_python_passes(seed):
+    """The C passes around the replay (csr + bulk remove_edges, csrc/ovl_digraph.c) leave the same graph
+    as the Python passes (generators + remove_edge per edge): nodes, successor/predecessor order, data."""
+    from ovlgraph import overlapGraphs as og
+    if og._digraph() is None:
+        pytest.skip("ovlgraph._digraph not built")
+    rng = random.Random(100 + seed)
+    for _ in range(25):
+        G = (_layered_graph(rng, rng.randint(1, 8)) if rng.random() < 0.5 else
+             _random_graph(rng, rng.randint(1, 50), rng.choice([0.05, 0.2, 0.5]), whi=rng.choice([1, 5, 1000])))
+        if G.number_of_edges() and rng.random() < 0.3:  # numpy integer weights are accepted by both
+            u, v = next(iter(G.edges()))
+            G[u][v]["weight"] = np.int64(G[u][v]["weight"])
+        t_native, t_py = {}, {}
+        H1 = og.remove_cycles_from_graph(G.copy(), native_edges=True, timing=t_native)
+        H2 = og.remove_cycles_from_graph(G.copy(), native_edges=False, timing=t_py)
+        assert _same(H1, H2) and t_native["removed"] == t_py["removed"]
+        assert all(list(H1.pred[n]) == list(H2.pred[n]) for n in H1)
+        assert nx.is_directed_acyclic_graph(H1)
+
+
+def test_native_edge_passes_errors_and_fallback():
+    from ovlgraph import overlapGraphs as og
+    if og._digraph() is None:
+        pytest.skip("ovlgraph._digraph not built")
+    for bad in (1.5, True, np.bool_(True), "3", None):
+        G = nx.DiGraph()
+        G.add_edge("a", "b", weight=2)
+        G.add_edge("b", "a", weight=bad)
+        with pytest.raises(TypeError):
+            og.remove_cycles_from_graph(G, native_edges=True)
+    G = nx.DiGraph()
+    G.add_edge("a", "b", weight=2)
+    G.add_edge("b", "a", end_position=1)
+    with pytest.raises(KeyError):
+        og.remove_cycles_from_graph(G, native_edges=True)
+
+    class Sub(nx.DiGraph):  # a DiGraph subclass keeps networkx's own remove_edge (Python passes)
+        pass
+    rng = random.Random(7)
+    G = _random_graph(rng, 30, 0.2)
+    S = Sub(G)
+    H = og.remove_cycles_from_graph(S)
+    assert type(H) is Sub and _same(H, og.remove_cycles_from_graph(G.copy(), native_edges=False))
+    mod = og._digraph()
+    assert mod.csr(list(G), {n: dict(G._adj[n]) for n in G}) is not None
+    from collections import OrderedDict
+    assert mod.csr(list(G), {n: OrderedDict(G._adj[n]) for n in G}) is None
+    E = nx.DiGraph()
+    E.add_edge("a", "b", weight=1)
+    with pytest.raises(KeyError):  # b -> a is not an edge
+        mod.remove_edges(E._succ, E._pred, ["a", "b"], np.array([1], np.int64), np.array([0], np.int64))
+    mod.remove_edges(E._succ, E._pred, ["a", "b"], np.array([0], np.int64), np.array([1], np.int64))
+    assert E.number_of_edges() == 0 and list(E.pred["b"]) == []
