@@ -48,12 +48,13 @@ struct Event {
     int64_t old;
 };
 
-// settled[v] = 1 iff v cannot reach a cycle over the live edges.  tail/rev: reverse CSR (edge
-// indices grouped by head).  Iterative Tarjan, then reverse reachability from the cyclic nodes.
+// settled[v] = 1 iff v cannot reach a cycle over the live edges.  roff/rtail/ralive: reverse CSR (edges
+// grouped by head: their tails, and whether they are live, kept contiguous so the reverse pass streams
+// instead of gathering edge ids).  Iterative Tarjan, then reverse reachability from the cyclic nodes.
 // Nodes already settled or explored cannot reach a cycle (explored nodes were all reached by a start
 // whose DFS found none), so they and the edges into them are left out.
 void settle(const int64_t* off, const int32_t* head, const uint8_t* alive, int32_t n,
-            const std::vector<int32_t>& tail, const std::vector<int64_t>& roff, const std::vector<int64_t>& rev,
+            const std::vector<int32_t>& rtail, const std::vector<int64_t>& roff, const std::vector<uint8_t>& ralive,
             const std::vector<uint8_t>& explored, std::vector<uint8_t>& settled) {
     if ((int32_t)settled.size() != n) settled.assign(n, 0);
     std::vector<uint8_t> done(n);
@@ -117,9 +118,8 @@ void settle(const int64_t* off, const int32_t* head, const uint8_t* alive, int32
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const int32_t v = queue[qi];
         for (int64_t k = roff[v]; k < roff[v + 1]; ++k) {
-            const int64_t e = rev[k];
-            if (!alive[e]) continue;
-            const int32_t u = tail[e];
+            if (!ralive[k]) continue;
+            const int32_t u = rtail[k];
             if (!bad[u] && !done[u]) { bad[u] = 1; queue.push_back(u); }
         }
     }
@@ -155,20 +155,23 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<int32_t> tail_of;          // path edge -> its tail (the node whose iterator yielded it)
     int64_t nrem = 0;
 
-    std::vector<int32_t> tail(n_edges);
-    std::vector<int64_t> roff(n_nodes + 1, 0), rev(n_edges);
-    for (int32_t v = 0; v < n_nodes; ++v)
-        for (int64_t e = off[v]; e < off[v + 1]; ++e) {
-            tail[e] = v;
-            ++roff[head[e] + 1];
-        }
+    // reverse CSR: rtail[k] / ralive[k] for the k-th edge into its head; rpos[e] = k (a removal clears both)
+    std::vector<int64_t> roff(n_nodes + 1, 0), rpos(n_edges);
+    std::vector<int32_t> rtail(n_edges);
+    std::vector<uint8_t> ralive(n_edges, 1);
+    for (int64_t e = 0; e < n_edges; ++e) ++roff[head[e] + 1];
     for (int32_t v = 0; v < n_nodes; ++v) roff[v + 1] += roff[v];
     {
         std::vector<int64_t> fill(roff.begin(), roff.end() - 1);
-        for (int64_t e = 0; e < n_edges; ++e) rev[fill[head[e]]++] = e;
+        for (int32_t v = 0; v < n_nodes; ++v)
+            for (int64_t e = off[v]; e < off[v + 1]; ++e) {
+                const int64_t k = fill[head[e]]++;
+                rtail[k] = v;
+                rpos[e] = k;
+            }
     }
     std::vector<uint8_t> settled;
-    settle(off, head, alive.data(), n_nodes, tail, roff, rev, explored, settled);
+    settle(off, head, alive.data(), n_nodes, rtail, roff, ralive, explored, settled);
     // yields between recomputations (OVL_CYCLES_SETTLE_EVERY: a test knob, e.g. 1 = after every yield)
     int64_t every = n_edges / 2;
     if (const char* env = getenv("OVL_CYCLES_SETTLE_EVERY")) every = atoll(env);
@@ -236,7 +239,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
             pos[cur] = q + 1;
             const int32_t h = head[q];
             if (--budget < 0) {
-                settle(off, head, alive.data(), n_nodes, tail, roff, rev, explored, settled);
+                settle(off, head, alive.data(), n_nodes, rtail, roff, ralive, explored, settled);
                 budget = every;
                 if (settled[h]) continue;
             }
@@ -272,6 +275,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 const int32_t tail_of_dead = tail_of[kmin];
                 removed[nrem++] = dead;
                 alive[dead] = 0;
+                ralive[rpos[dead]] = 0;
                 skip[dead] = dead + 1;
                 // rewind the DFS to the moment `dead` was about to be yielded
                 const int64_t target = ckpt[kmin];
