@@ -5,10 +5,12 @@ set: the distinct reads and the reference-ordered candidate list (aligners.py:27
 every pair of overlapGraphs.py:43-53) are resident in HBM when the timed region starts
 (the list is enumerated on the device, ovl_candidates), and the step ends with every
 pair's (score, end) in host memory: the ABI call ``ovl_score_candidates`` runs the
-kernels, which store their results over the link into host memory -- packed (end and
-mismatch count, 2 B per pair) for the first chunks, which host threads expand into the
-caller's pinned int32 arrays while the next chunks score, and as int32 straight into
-those arrays for the last ~20 % of the pairs (the share adapts per call).
+kernels, which store their results over the link into host memory packed (end and
+mismatch count, 2 B per pair) and host threads expand them into the caller's pinned
+int32 arrays.  Reads of <= 128 bases (the target point): ONE launch whose tiles publish
+their packed lines and a checksummed flag as they finish, expanded while the kernel
+still runs (progressive transport); longer reads: packed chunks expanded while the next
+chunk scores, and the last ~20 % of the pairs stored as int32 straight into the arrays.
 
     python bench.py [--gpus 1 --steps K --warmup W --config target]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -660,7 +662,8 @@ def main() -> None:
             "read_length": w.cfg["l"],
             "step": "ovl_score_candidates: resident reads + device-enumerated list -> kernels storing over the "
                     "link -> (score, end) in pinned host int32 arrays (SURVEY.md §8d, results in host memory; "
-                    "packed 2 B/pair chunks expanded by host threads, the last ~20 % stored directly)",
+                    "packed 2 B/pair, expanded by host threads while the kernel runs: progressive tiles for "
+                    "l <= 128, else chunks plus a direct int32 share)",
             "parallelism": "1 GPU",
             "kernel": w.kernel,
             "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},

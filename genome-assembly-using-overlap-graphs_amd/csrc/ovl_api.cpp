@@ -88,6 +88,12 @@ struct Knobs {
     int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
+    int32_t progressive = -1;     // OVL_PROGRESSIVE: whole-list calls into pinned arrays through the progressive
+                                  // transport (1), the chunked packed pipeline (0), or by read length (-1: W <= 4,
+                                  // where it measured faster; progressive_ok)
+    int32_t pg_store = 1;         // OVL_PG_STORE: progressive line/flag stores, 0 system write-through, 1 device
+                                  // write-through, 2 non-temporal; +4 skips the wait before the flag (A/B knob;
+                                  // tools/prog_probe.py, target kernel in the call: 0.35 / 0.12 / 0.13 ms, +4 no change)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -167,6 +173,17 @@ struct Dev {
     int32_t out_mode = 0;            // result sink of the next ungapped launches (OvlUngappedArgs::host_out):
                                      // 0 HBM, 1 host-mapped int32 arrays, 2 host-mapped packed uint16
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
+    // progressive transport (sink 3): fine-grained pinned packed lines, escapes and tile flags, by list tile
+    uint16_t* pg_pk = nullptr;
+    int32_t* pg_esc = nullptr;
+    unsigned long long* pg_flag = nullptr;
+    uint16_t* pg_pk_dev = nullptr;
+    int32_t* pg_esc_dev = nullptr;
+    unsigned long long* pg_flag_dev = nullptr;
+    int64_t pg_tiles = 0;                // capacity in tiles
+    uint32_t pg_epoch = 0;               // last call's flag tag
+    std::vector<uint8_t> pg_heavy;       // per list tile: 1 = heavy (no flag; stored as int32 by the kernel)
+    int64_t pg_heavy_for = -1;           // cand_n pg_heavy was built for
 };
 
 struct ovl_ctx {
@@ -446,6 +463,13 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
         g.host_out = c->out_mode;
+        if (g.host_out == 3) {
+            g.pg_pk = c->pg_pk_dev;
+            g.pg_esc = c->pg_esc_dev;
+            g.pg_flag = c->pg_flag_dev;
+            g.pg_epoch = c->pg_epoch;
+            g.pg_mode = (uint32_t)c->k.pg_store;
+        }
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
         if (c->k.heavy_first && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
@@ -604,6 +628,8 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_HEAVY_FIRST")) k.heavy_first = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PROGRESSIVE")) k.progressive = atoi(e) ? 1 : 0;  // (unset: automatic)
+    if (const char* e = getenv("OVL_PG_STORE")) k.pg_store = std::max(0, std::min(7, atoi(e)));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
         k.pack_adapt = 0;  // a fixed share
@@ -796,6 +822,8 @@ void destroy_dev(Dev* d) {
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
     free_staging(d->st_out);
+    for (void* q : {(void*)d->pg_pk, (void*)d->pg_esc, (void*)d->pg_flag})
+        if (q) (void)hipHostFree(q);
     if (d->h_flag) (void)hipHostFree(d->h_flag);
     for (int i = 0; i < kSlots; ++i)
         for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i]})
@@ -1364,6 +1392,161 @@ bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) 
            p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
+}
+
+// Progressive transport (sink 3) for a whole-list call into pinned arrays on one device: ONE launch of the
+// uniform kernel; each tile without side pairs publishes its packed results (one 128-B line of uint16, put_pair's
+// sink-2 encoding) and then a 64-bit flag (epoch << 32 | checksum) into fine-grained host memory with
+// write-through stores as it finishes, and the host pool expands tiles into the caller's int32 arrays as their
+// flags arrive, while the kernel still runs (the chunked pipeline waits for a whole chunk's launch).  Heavy tiles
+// (side pairs) store int32 straight into the arrays.  A flag is taken only with the line's checksum, so a line
+// that lands after its flag is waited for; one that never matches fails the call (never silently).
+bool progressive_ok(const ovl_ctx* c, const Plan& p, int64_t lo, int64_t hi, bool out_pinned, bool pack) {
+    const Dev* d = c->devs[0];
+    // automatic: reads of <= 128 bases (interleaved A/B, tools/pack_ab.py, seven rounds: target 0.167 against
+    // 0.174 ms for the chunked pipeline; cfg3, l = 150: 0.344 against 0.319, so longer reads keep the chunks)
+    const bool want = d->k.progressive > 0 || (d->k.progressive < 0 && d->wmax <= 4);
+    return pack && out_pinned && want && d->k.heavy_first && c->devs.size() == 1 && lo == 0 &&
+           hi == d->cand_n && hi - lo >= d->k.pack_min && d->split_override < 0 && d->planes == 2 && !p.key64 &&
+           (hi + 63) / 64 > (int64_t)d->cu_count * 8;  // throughput mode (launch_score_chunk's rs_log2 == 0)
+}
+
+int run_progressive(ovl_ctx* c, const Call& C, int64_t n) {
+    Dev* d = c->devs[0];
+    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(c, hipSetDevice(d->device));
+    int rc = ensure_heavy(d);
+    if (rc != OVL_OK) return rc;
+    const int64_t n_tiles = (n + 63) / 64;
+    if (d->pg_tiles < n_tiles) {
+        for (void* q : {(void*)d->pg_pk, (void*)d->pg_esc, (void*)d->pg_flag})
+            if (q) (void)hipHostFree(q);
+        d->pg_pk = nullptr;
+        d->pg_esc = nullptr;
+        d->pg_flag = nullptr;
+        d->pg_tiles = 0;
+        HIPCHK(c, hipHostMalloc((void**)&d->pg_pk, (size_t)n_tiles * 64 * sizeof(uint16_t), kHostShared));
+        HIPCHK(c, hipHostMalloc((void**)&d->pg_esc, (size_t)n_tiles * 64 * sizeof(int32_t), kHostShared));
+        HIPCHK(c, hipHostMalloc((void**)&d->pg_flag, (size_t)n_tiles * sizeof(unsigned long long), kHostShared));
+        memset(d->pg_flag, 0, (size_t)n_tiles * sizeof(unsigned long long));
+        HIPCHK(c, hipHostGetDevicePointer((void**)&d->pg_pk_dev, d->pg_pk, 0));
+        HIPCHK(c, hipHostGetDevicePointer((void**)&d->pg_esc_dev, d->pg_esc, 0));
+        HIPCHK(c, hipHostGetDevicePointer((void**)&d->pg_flag_dev, d->pg_flag, 0));
+        d->pg_tiles = n_tiles;
+    }
+    if (d->pg_heavy_for != d->cand_n) {
+        d->pg_heavy.assign((size_t)n_tiles, 0);
+        for (int32_t t : d->h_heavy) d->pg_heavy[(size_t)t] = 1;
+        d->pg_heavy_for = d->cand_n;
+    }
+    if (++d->pg_epoch == 0) d->pg_epoch = 1;
+    const uint32_t epoch = d->pg_epoch;
+    void* ps = nullptr;
+    void* pe = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer(&ps, C.out_s, 0));
+    HIPCHK(c, hipHostGetDevicePointer(&pe, C.out_e, 0));
+    *(volatile uint32_t*)d->h_flag = 0;
+    d->cur_flag = d->h_flag_dev;
+    d->out_mode = 3;
+    if (C.timing) {
+        while (d->t_ev.size() < 2) {
+            hipEvent_t ev;
+            HIPCHK(c, hipEventCreate(&ev));
+            d->t_ev.push_back(ev);
+        }
+        HIPCHK(c, hipEventRecord(d->t_ev[0], d->stream));
+    }
+    rc = launch_score(d, *C.plan, as<int32_t>(d->cand_a), as<int32_t>(d->cand_b), n, C.match, C.mismatch, C.indel,
+                      reinterpret_cast<int32_t*>(ps), reinterpret_cast<int32_t*>(pe), d->stream);
+    d->cur_flag = as<uint32_t>(d->err_flag);
+    d->out_mode = 0;
+    if (rc != OVL_OK) {
+        (void)hipStreamSynchronize(d->stream);
+        return rc;
+    }
+    if (C.timing) HIPCHK(c, hipEventRecord(d->t_ev[1], d->stream));
+    HIPCHK(c, hipEventRecord(d->ev_last, d->stream));
+    // the pool's threads take blocks of kB tiles round-robin in list order (the kernel finishes tiles roughly
+    // in that order); a block is expanded once all its light tiles' flags and checksums match
+    static const ovl_expand::Fn fx = [] {
+        const ovl_expand::Fn g = ovl_expand::pick(getenv("OVL_EXPAND_ISA"));
+        return g ? g : ovl_expand::pick(nullptr);
+    }();
+    constexpr int64_t kB = 8;
+    const int64_t n_blocks = (n_tiles + kB - 1) / kB;
+    const int P = std::max(1, CopyPool::threads());
+    std::atomic<int64_t> lost{0};
+    std::atomic<int> done{0};  // the kernel is known to have finished (set by whichever thread saw it first)
+    const uint16_t* pk = d->pg_pk;
+    const volatile unsigned long long* fl = d->pg_flag;
+    const uint8_t* heavy = d->pg_heavy.data();
+    std::vector<uint8_t> bad((size_t)n_tiles, 0);
+    auto ready = [&](int64_t t) {
+        std::atomic_signal_fence(std::memory_order_seq_cst);  // reload the line on every poll
+        const unsigned long long f = fl[t];
+        if ((uint32_t)(f >> 32) != epoch) return false;
+        const uint16_t* q = pk + t * 64;
+        uint32_t cs = 0;
+        for (uint32_t l = 0; l < 64; ++l) cs += (uint32_t)q[l] * (2 * l + 1);
+        return cs == (uint32_t)f;
+    };
+    CopyPool::get().parallel((size_t)P * 64, 64, [&](size_t lo_, size_t) {
+        const int64_t me = (int64_t)(lo_ / 64);
+        for (int64_t blk = me; blk < n_blocks; blk += P) {
+            const int64_t t0b = blk * kB, t1b = std::min(n_tiles, t0b + kB);
+            for (int64_t t = t0b; t < t1b; ++t) {
+                if (heavy[t]) continue;
+                for (int64_t spin = 1; !ready(t); ++spin) {
+                    _mm_pause();
+                    if ((spin & 1023) == 0) {
+                        if (!done.load(std::memory_order_acquire)) {
+                            if (hipEventQuery(d->ev_last) != hipErrorNotReady) done.store(1, std::memory_order_release);
+                        } else if (spin > 4096) {  // finished for a while and still no match: left to the check below
+                            bad[(size_t)t] = 1;
+                            lost.fetch_add(1, std::memory_order_relaxed);
+                            break;
+                        }
+                    }
+                }
+            }
+            // the block's pairs, light tiles only (heavy tiles' int32 results are the kernel's)
+            for (int64_t t = t0b; t < t1b; ++t) {
+                if (heavy[t] || bad[(size_t)t]) continue;
+                int64_t t1 = t + 1;
+                while (t1 < t1b && !heavy[t1] && !bad[(size_t)t1]) ++t1;
+                fx(C.out_s, C.out_e, pk, d->pg_esc, C.match, C.mismatch, d->k.pack_nt != 0, (size_t)(t * 64),
+                   (size_t)std::min(n, t1 * 64));
+                t = t1 - 1;
+            }
+        }
+    });
+    HIPCHK(c, hipStreamSynchronize(d->stream));
+    if (lost.load()) {  // the kernel is done: every light tile's line and flag must match now
+        for (int64_t t = 0; t < n_tiles; ++t) {
+            if (!bad[(size_t)t]) continue;
+            if (!ready(t))
+                return fail(c, OVL_E_HIP, "progressive transport: tile %lld never published its results", (long long)t);
+            fx(C.out_s, C.out_e, pk, d->pg_esc, C.match, C.mismatch, d->k.pack_nt != 0, (size_t)(t * 64),
+               (size_t)std::min(n, t * 64 + 64));
+        }
+    }
+    if (d->k.pack_nt) _mm_sfence();
+    if (*(volatile uint32_t*)d->h_flag) {
+        *d->h_flag = 0;
+        rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
+    }
+    double kms = 0.0;
+    if (C.timing) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, d->t_ev[0], d->t_ev[1]) == hipSuccess) kms = ms;
+    }
+    c->t_kernel_ms = kms;
+    c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    int64_t heavy_pairs = 0;
+    for (int32_t t : d->h_heavy) heavy_pairs += std::min<int64_t>(64, n - (int64_t)t * 64);
+    c->x_link_bytes = 2 * (n - heavy_pairs) + 8 * heavy_pairs + 8 * (n_tiles - (int64_t)d->h_heavy.size());
+    c->x_packed_pairs = n - heavy_pairs;
+    return rc;
 }
 
 int check_scoring_args(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* p) {
@@ -1937,6 +2120,7 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.timing = ctx->timing != 0;
     C.direct = ctx->devs[0]->k.pipe_direct != 0;
     C.pack = pack_ok(ctx, p, hi - lo, C.out_pinned);
+    if (C.direct && progressive_ok(ctx, p, lo, hi, C.out_pinned, C.pack)) return run_progressive(ctx, C, hi - lo);
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);

@@ -554,3 +554,74 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
     rs, re_ = oracle_mod.batch_dp(reads, a[idx], b[idx], 10, -1, -2)
     np.testing.assert_array_equal(ls[idx], rs)
     np.testing.assert_array_equal(le[idx], re_)
+
+
+# ----------------------------------------------------------------------------- progressive transport
+@pytest.mark.parametrize("cfg", ["target", "cfg3"])
+def test_progressive_transport_vs_oracle(oracle_mod, cfg):
+    """Whole resident list into pinned arrays (the bench step): the progressive transport (one launch; light tiles
+    publish a packed line + flag that the host expands while the kernel runs, heavy tiles store int32) equals
+    the oracle and the chunked packed pipeline (OVL_PROGRESSIVE=0), call after call (flag epochs), into fresh
+    and reused arrays; ovl_last_transfer counts 2 B per light pair and 8 B per heavy pair plus the flags."""
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.hostmem import pinned_empty
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads(cfg, seed=0))
+    prog = _engine_env({"OVL_PROGRESSIVE": "1"})
+    chunked = _engine_env({"OVL_PROGRESSIVE": "0"})
+    try:
+        for e in (prog, chunked):
+            e.set_reads(reads)
+        a, b = prog.candidates(5)
+        chunked.candidates(5)
+        ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+        n = a.shape[0]
+        out = (pinned_empty(n), pinned_empty(n))
+        for it in range(6):
+            out[0][:] = -7
+            out[1][:] = -7
+            prog.score_candidates(out=out)
+            np.testing.assert_array_equal(out[0], ref_s, err_msg=f"call {it}")
+            np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
+        x = prog.last_transfer()
+        lens = np.array([len(r) for r in reads])
+        side = lens[a] != lens.max()
+        tiles = (n + 63) // 64
+        heavy = np.zeros(tiles, bool)
+        np.logical_or.at(heavy, np.arange(n) // 64, side)
+        heavy_pairs = int(sum(min(64, n - 64 * t) for t in np.flatnonzero(heavy)))
+        assert x["packed_pairs"] == n - heavy_pairs, x
+        assert x["link_bytes"] == 2 * (n - heavy_pairs) + 8 * heavy_pairs + 8 * int((~heavy).sum()), x
+        cs, ce = chunked.score_candidates()
+        np.testing.assert_array_equal(cs, ref_s)
+        np.testing.assert_array_equal(ce, ref_e)
+        fresh = prog.score_candidates()
+        np.testing.assert_array_equal(fresh[0], ref_s)
+        np.testing.assert_array_equal(fresh[1], ref_e)
+    finally:
+        prog.close()
+        chunked.close()
+
+
+def test_progressive_transport_without_heavy_tiles(oracle_mod):
+    """A list with no side pairs (every read of one length: no heavy tiles, no heavy-first ids) and one whose
+    list changes between calls (the tile flags and heavy map follow the new list)."""
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.hostmem import pinned_empty
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("target", seed=3))
+    lw = max(len(r) for r in reads)
+    uniform = [r for r in reads if len(r) == lw]
+    eng = _engine_env({"OVL_PROGRESSIVE": "1"})
+    try:
+        for rs in (uniform, reads, uniform):
+            eng.set_reads(rs)
+            a, b = eng.candidates(5)
+            ref_s, ref_e = oracle_mod.batch_closed_form(rs, a, b)
+            out = (pinned_empty(a.shape[0]), pinned_empty(a.shape[0]))
+            for _ in range(2):
+                eng.score_candidates(out=out)
+                np.testing.assert_array_equal(out[0], ref_s)
+                np.testing.assert_array_equal(out[1], ref_e)
+    finally:
+        eng.close()
