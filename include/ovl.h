@@ -90,8 +90,9 @@ int ovl_set_timing(ovl_ctx* ctx, int32_t on);
 int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 /* Link traffic of the last host-array scoring call (always recorded): link_bytes = pair-list bytes the
  * devices read from host memory + result bytes they stored there (2 per pair in packed chunks, 8 per pair
- * otherwise; the few packed pairs whose score travels separately add 4 each and are not counted);
- * packed_pairs = pairs whose results crossed packed and were expanded on the host. */
+ * otherwise; the few packed pairs whose score travels separately add 4 each and are not counted; a
+ * progressive call adds 8 per published tile flag); packed_pairs = pairs whose results crossed packed and
+ * were expanded on the host. */
 int ovl_last_transfer(const ovl_ctx* ctx, int64_t* link_bytes, int64_t* packed_pairs);
 
 /* Last error message of `ctx`, or of the calling thread when ctx is NULL. */
