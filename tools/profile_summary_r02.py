@@ -1,7 +1,8 @@
 """Summarise tools/gpu_r02_profile.sh into profiles/<round>_<config>_{kernel_stats.csv,pmc.json}.
 
-The step launches uniform_kernel<W, 0, false, 2> (packed chunks into pinned staging slots) and
-uniform_kernel<W, 0, false, 1> (its last chunk, int32 straight into the pinned arrays), and roofline.kernel_ms times uniform_kernel<W, 0, false, 0> (device outputs); their names differ, so the
+The step launches uniform_kernel<W, 0, false, 3> (the progressive transport, reads <= 128 bases) or
+uniform_kernel<W, 0, false, 2> (packed chunks into pinned staging slots) and uniform_kernel<W, 0, false, 1>
+(the last chunk, int32 straight into the pinned arrays), and roofline.kernel_ms times uniform_kernel<W, 0, false, 0> (device outputs); their names differ, so the
 rocprofv3 --stats rows are already one per phase.  PMC passes cover the kernel-only variant:
 HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1 KiB (gfx950 FETCH_SIZE halving, MI355X_MICROARCH.md);
 mean resident wavefronts per SIMD = 4 * SQ_WAVE_CYCLES / (duration * shader clock * 1024 SIMDs).
@@ -54,7 +55,7 @@ def main():
     clock = m["GRBM_GUI_ACTIVE"] / 8 / (sum(gdurs) / len(gdurs) * 1e-9)
     waves = 4 * m["SQ_WAVE_CYCLES"] / (dur_ns * 1e-9 * clock * SIMDS)
     lds_block = int(meta.get("LDS_Block_Size") or meta.get("Lds_Size") or 0)
-    step_names = [k for k in st if "uniform_kernel" in k and k.split("(")[0].endswith((", 1>", ", 2>"))]
+    step_names = [k for k in st if "uniform_kernel" in k and k.split("(")[0].endswith((", 1>", ", 2>", ", 3>"))]
     ko_name = next((k for k in st if "uniform_kernel" in k and k.split("(")[0].endswith(", 0>")), None)
     out = {
         "workload": cfg, "kernel": name.split("(")[0] if name else None,
