@@ -1414,6 +1414,7 @@ bool progressive_ok(const ovl_ctx* c, const Plan& p, int64_t lo, int64_t hi, boo
 int run_progressive(ovl_ctx* c, const Call& C, int64_t n) {
     Dev* d = c->devs[0];
     const auto t0 = std::chrono::steady_clock::now();
+    PipeTrace trace;  // OVL_TRACE_PIPE: s setup, i launched, f first flag seen, x expanded, y synchronised
     HIPCHK(c, hipSetDevice(d->device));
     int rc = ensure_heavy(d);
     if (rc != OVL_OK) return rc;
@@ -1448,6 +1449,7 @@ int run_progressive(ovl_ctx* c, const Call& C, int64_t n) {
     *(volatile uint32_t*)d->h_flag = 0;
     d->cur_flag = d->h_flag_dev;
     d->out_mode = 3;
+    trace.mark('s', 0);
     if (C.timing) {
         while (d->t_ev.size() < 2) {
             hipEvent_t ev;
@@ -1466,6 +1468,7 @@ int run_progressive(ovl_ctx* c, const Call& C, int64_t n) {
     }
     if (C.timing) HIPCHK(c, hipEventRecord(d->t_ev[1], d->stream));
     HIPCHK(c, hipEventRecord(d->ev_last, d->stream));
+    trace.mark('i', 0);
     // the pool's threads take blocks of kB tiles round-robin in list order (the kernel finishes tiles roughly
     // in that order); a block is expanded once all its light tiles' flags and checksums match
     static const ovl_expand::Fn fx = [] {
@@ -1520,7 +1523,9 @@ int run_progressive(ovl_ctx* c, const Call& C, int64_t n) {
             }
         }
     });
+    trace.mark('x', 0);
     HIPCHK(c, hipStreamSynchronize(d->stream));
+    trace.mark('y', 0);
     if (lost.load()) {  // the kernel is done: every light tile's line and flag must match now
         for (int64_t t = 0; t < n_tiles; ++t) {
             if (!bad[(size_t)t]) continue;
