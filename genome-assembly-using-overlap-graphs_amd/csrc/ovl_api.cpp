@@ -644,7 +644,7 @@ Knobs read_knobs() {
 // Host copies between pageable caller arrays and the pinned staging rings, split over a few worker threads
 // (one thread copies ~10 GB/s; a 16 MB result column is ~1.5 ms alone).  The pool is created on first
 // use in each process (a forked joblib worker builds its own) and sized by OVL_HOST_THREADS (default:
-// min(12, hardware threads)).
+// min(15, hardware threads, the CPU quota share)).
 class CopyPool {
   public:
     static int threads() { return planned_threads(); }
@@ -704,15 +704,17 @@ class CopyPool {
         new (&get_mutex()) std::mutex();
         pool_ = nullptr;
     }
-    // Threads of the pool (the calling thread included): OVL_HOST_THREADS, else 12 (three processes each of
+    // Threads of the pool (the calling thread included): OVL_HOST_THREADS, else 15 (three processes each of
     // 6 / 8 / 12 threads on the box, a 16-CPU share: packed step 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms,
-    // profiles/r02_pool_threads_*.json), capped by the hardware threads and by this process's part of the
+    // profiles/r02_pool_threads_*.json; with the progressive transport, which the host expansion bounds,
+    // 12 / 15 threads alternating over three process pairs: 0.175 / 0.158, 0.208 / 0.163, 0.159 / 0.146 ms,
+    // profiles/r02_prog_threads_*.json), capped by the hardware threads and by this process's part of the
     // job's CPU quota (cgroup cpu.max divided over LOCAL_WORLD_SIZE ranks, one CPU left for the rank's own
     // thread), at least 1.
     static int planned_threads() {
         static const int n = [] {
             if (const char* e = getenv("OVL_HOST_THREADS")) return std::max(1, std::min(64, atoi(e)));
-            int t = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
+            int t = (int)std::min<unsigned>(15u, std::max(1u, std::thread::hardware_concurrency()));
             long long quota = 0, period = 0;
             if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
                 if (fscanf(f, "%lld %lld", &quota, &period) != 2) quota = period = 0;  // "max ..." stays 0
