@@ -7,10 +7,9 @@ every pair of overlapGraphs.py:43-53) are resident in HBM when the timed region 
 pair's (score, end) in host memory: the ABI call ``ovl_score_candidates`` runs the
 kernels, which store their results over the link into host memory packed (end and
 mismatch count, 2 B per pair) and host threads expand them into the caller's pinned
-int32 arrays.  Reads of <= 128 bases (the target point): ONE launch whose tiles publish
-their packed lines and a checksummed flag as they finish, expanded while the kernel
-still runs (progressive transport); longer reads: packed chunks expanded while the next
-chunk scores, and the last ~20 % of the pairs stored as int32 straight into the arrays.
+int32 arrays: packed chunks expanded while the next chunk scores, and the last ~20 % of
+the pairs stored as int32 straight into the arrays (OVL_PROGRESSIVE=1 selects the measured
+alternative: one launch whose tiles publish packed lines as they finish).
 
     python bench.py [--gpus 1 --steps K --warmup W --config target]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -662,8 +661,8 @@ def main() -> None:
             "read_length": w.cfg["l"],
             "step": "ovl_score_candidates: resident reads + device-enumerated list -> kernels storing over the "
                     "link -> (score, end) in pinned host int32 arrays (SURVEY.md §8d, results in host memory; "
-                    "packed 2 B/pair, expanded by host threads while the kernel runs: progressive tiles for "
-                    "l <= 128, else chunks plus a direct int32 share)",
+                    "packed 2 B/pair chunks expanded by host threads while the next chunk scores, the last "
+                    "~20 % stored directly)",
             "parallelism": "1 GPU",
             "kernel": w.kernel,
             "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},

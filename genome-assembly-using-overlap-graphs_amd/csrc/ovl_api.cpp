@@ -88,9 +88,10 @@ struct Knobs {
     int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
-    int32_t progressive = -1;     // OVL_PROGRESSIVE: whole-list calls into pinned arrays through the progressive
-                                  // transport (1), the chunked packed pipeline (0), or by read length (-1: W <= 4,
-                                  // where it measured faster; progressive_ok)
+    int32_t progressive = 0;      // OVL_PROGRESSIVE=1: whole-list calls into pinned arrays through the progressive
+                                  // transport (progressive_ok) instead of the chunked packed pipeline (measured,
+                                  // opt-in: interleaved on one box 0.167 vs 0.174 ms at the target point, but in
+                                  // six process pairs on two other boxes the chunked pipeline won every one)
     int32_t pg_store = 1;         // OVL_PG_STORE: progressive line/flag stores, 0 system write-through, 1 device
                                   // write-through, 2 non-temporal; +4 skips the wait before the flag (A/B knob;
                                   // tools/prog_probe.py, target kernel in the call: 0.35 / 0.12 / 0.13 ms, +4 no change)
@@ -628,7 +629,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_HEAVY_FIRST")) k.heavy_first = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PROGRESSIVE")) k.progressive = atoi(e) ? 1 : 0;  // (unset: automatic)
+    if (const char* e = getenv("OVL_PROGRESSIVE")) k.progressive = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PG_STORE")) k.pg_store = std::max(0, std::min(7, atoi(e)));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
@@ -644,7 +645,7 @@ Knobs read_knobs() {
 // Host copies between pageable caller arrays and the pinned staging rings, split over a few worker threads
 // (one thread copies ~10 GB/s; a 16 MB result column is ~1.5 ms alone).  The pool is created on first
 // use in each process (a forked joblib worker builds its own) and sized by OVL_HOST_THREADS (default:
-// min(15, hardware threads, the CPU quota share)).
+// min(12, hardware threads, the CPU quota share)).
 class CopyPool {
   public:
     static int threads() { return planned_threads(); }
@@ -704,17 +705,16 @@ class CopyPool {
         new (&get_mutex()) std::mutex();
         pool_ = nullptr;
     }
-    // Threads of the pool (the calling thread included): OVL_HOST_THREADS, else 15 (three processes each of
+    // Threads of the pool (the calling thread included): OVL_HOST_THREADS, else 12 (three processes each of
     // 6 / 8 / 12 threads on the box, a 16-CPU share: packed step 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms,
-    // profiles/r02_pool_threads_*.json; with the progressive transport, which the host expansion bounds,
-    // 12 / 15 threads alternating over three process pairs: 0.175 / 0.158, 0.208 / 0.163, 0.159 / 0.146 ms,
-    // profiles/r02_prog_threads_*.json), capped by the hardware threads and by this process's part of the
+    // profiles/r02_pool_threads_*.json; 15 threads, alternating with 12 over three process pairs on each of two
+    // boxes, won all three on one and lost two of three on the other: profiles/r02_prog_threads_*.json), capped by the hardware threads and by this process's part of the
     // job's CPU quota (cgroup cpu.max divided over LOCAL_WORLD_SIZE ranks, one CPU left for the rank's own
     // thread), at least 1.
     static int planned_threads() {
         static const int n = [] {
             if (const char* e = getenv("OVL_HOST_THREADS")) return std::max(1, std::min(64, atoi(e)));
-            int t = (int)std::min<unsigned>(15u, std::max(1u, std::thread::hardware_concurrency()));
+            int t = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
             long long quota = 0, period = 0;
             if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
                 if (fscanf(f, "%lld %lld", &quota, &period) != 2) quota = period = 0;  // "max ..." stays 0
@@ -1405,10 +1405,7 @@ bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) 
 // that lands after its flag is waited for; one that never matches fails the call (never silently).
 bool progressive_ok(const ovl_ctx* c, const Plan& p, int64_t lo, int64_t hi, bool out_pinned, bool pack) {
     const Dev* d = c->devs[0];
-    // automatic: reads of <= 128 bases (interleaved A/B, tools/pack_ab.py, seven rounds: target 0.167 against
-    // 0.174 ms for the chunked pipeline; cfg3, l = 150: 0.344 against 0.319, so longer reads keep the chunks)
-    const bool want = d->k.progressive > 0 || (d->k.progressive < 0 && d->wmax <= 4);
-    return pack && out_pinned && want && d->k.heavy_first && c->devs.size() == 1 && lo == 0 &&
+    return pack && out_pinned && d->k.progressive > 0 && d->k.heavy_first && c->devs.size() == 1 && lo == 0 &&
            hi == d->cand_n && hi - lo >= d->k.pack_min && d->split_override < 0 && d->planes == 2 && !p.key64 &&
            (hi + 63) / 64 > (int64_t)d->cu_count * 8;  // throughput mode (launch_score_chunk's rs_log2 == 0)
 }
