@@ -8,19 +8,25 @@ pair's (score, end) in host memory: the ABI call ``ovl_score_candidates`` runs t
 kernels, which store their results over the link into host memory packed (end and
 mismatch count, 2 B per pair) and host threads expand them into the caller's pinned
 int32 arrays: packed chunks expanded while the next chunk scores, and the last ~20 % of
-the pairs stored as int32 straight into the arrays (OVL_PROGRESSIVE=1 selects the measured
-alternative: one launch whose tiles publish packed lines as they finish).
+the pairs stored as int32 straight into the arrays.
 
-    python bench.py [--gpus 1 --steps K --warmup W --config target]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python bench.py [--gpus N --steps K --warmup W --config target --scaling weak|strong]
 
-N = 1: the north_star target point (PhiX N=50k l=100 p=0.01 k=5, ~2.0 M pairs).
-N > 1: one process per GPU, ONE shared list -- BASELINE configs[3] (cfg4: 1 Mbp genome,
-N=200k reads, ~38 M pairs) -- sharded by sum n*m; every rank copies its (score, end)
-slice into rank 0's shared pinned host buffer (ovlgraph.sharded.ShardedStep, dest="host"),
-so the step ends with the whole reference-ordered result on rank 0's host: strong
-scaling.  Time = max over ranks between barriers; value = pairs / time.  Rank 0 prints
-one JSON line.
+``--gpus N`` > 1 without a launcher: this process starts ``python -m torch.distributed.run
+--nproc-per-node N bench.py ...`` as a CHILD before touching the GPU, waits for it and exits
+with its status (the ranks print the line).  Launched by torch.distributed.run (WORLD_SIZE set),
+WORLD_SIZE must equal --gpus.
+
+Every N runs the same workload (--config, default the north_star target point: PhiX N=50k
+l=100 p=0.01 k=5, ~2.0 M pairs).  N = 1: one process, one GPU.  N > 1, one process per GPU:
+  weak (default): every rank scores its own read set of that workload (seed + rank) -- the
+    reference's own parallel shape, independent graph builds side by side (experiments.py:537
+    fans graph builds out over joblib workers); value = all ranks' pairs / max-over-ranks time;
+  strong: ONE read set, its candidate list sharded by sum n*m over the ranks, every rank's
+    (score, end) into rank 0's shared pinned host buffer (ovlgraph.sharded.ShardedStep); the
+    line also carries the same list scored by one GPU in the same run and the speed-up.
+The N > 1 weak line also carries BASELINE configs[3]'s shape (cfg4, 38 M pairs) strong-scaled
+the same way.  Time = max over ranks between barriers.  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -65,8 +71,17 @@ def algorithmic_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> int:
     return int(q[a].sum() + q[b].sum() + 16 * a.shape[0])
 
 
-def load_profile(workload: str):
-    """The committed PMC summary (profiles/*pmc*.json, newest round first) for this workload, or {}."""
+def _short_kernel(name: str) -> str:
+    """'void ovl::uniform_kernel<4, 0, false, 2>(...)' -> 'uniform_kernel<4, 0, false, 2>'."""
+    name = name.split("(")[0].strip()
+    for pre in ("void ", "ovl::"):
+        name = name.replace(pre, "")
+    return name
+
+
+def load_profile(workload: str, kernel: str = None):
+    """The committed PMC summary (profiles/*pmc*.json, newest round first) for this workload -- and, when
+    `kernel` is given, for that kernel (round-3 summaries hold one entry per kernel) -- or {}."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
         return {}
@@ -77,21 +92,29 @@ def load_profile(workload: str):
                     d = json.load(fh)
             except Exception:
                 continue
-            if d.get("workload") == workload:
+            if d.get("workload") != workload:
+                continue
+            if "kernels" in d:
+                ks = {_short_kernel(k): v for k, v in d["kernels"].items()}
+                want = kernel or d.get("headline_kernel")
+                if want in ks:
+                    return dict(d, **ks[want], kernel=want)
+                continue
+            if kernel is None or _short_kernel(d.get("kernel", "")) == kernel:
                 return d
     return {}
 
 
-def load_traffic(workload: str):
-    """HBM bytes per launch from the committed PMC summary for this workload."""
-    d = load_profile(workload)
+def load_traffic(workload: str, kernel: str = None):
+    """HBM bytes per launch of `kernel` from the committed PMC summary for this workload, or None."""
+    d = load_profile(workload, kernel)
     return int(d["hbm_bytes_per_launch"]) if d.get("hbm_bytes_per_launch") else None
 
 
-def valu_roofline(workload: str, kernel_ms: float):
+def valu_roofline(workload: str, kernel_ms: float, kernel: str = None):
     """Second bound next to HBM: VALU issue (what the ungapped kernel is limited by), against both the
     measured-mix issue model and the ISA peak (2 cycles per wave64 instruction)."""
-    d = load_profile(workload)
+    d = load_profile(workload, kernel)
     n = d.get("SQ_INSTS_VALU_per_launch")
     if not n or kernel_ms <= 0:
         return None
@@ -196,27 +219,48 @@ class Workload:
         self.name = name
         self.cfg = CONFIGS[name]
         self.dev = dev
+        from ovlgraph.engine import encode_reads
         t0 = time.perf_counter()
-        self.reads, _ = dedup_reads(config_reads(name, seed=seed))
+        raw = config_reads(name, seed=seed)
         self.t_sim = time.perf_counter() - t0
+        # the drop-in's per-build fixed cost, stage by stage (overlapGraphs.py:17-53 before the scoring)
+        st = {}
+        t = time.perf_counter()
+
+        def mark(k):
+            nonlocal t
+            now = time.perf_counter()
+            st[k] = round(now - t, 5)
+            t = now
+        self.reads, _ = dedup_reads(raw)
+        mark("dedup")
         self.eng = engine or OverlapEngine(dev.index)
-        t0 = time.perf_counter()
-        self.eng.set_reads(self.reads)
+        mark("engine")
+        enc = encode_reads(self.reads)
+        mark("encode")
+        self.eng.set_reads(self.reads, enc)
+        mark("set_reads_upload_pack")
         self.n_pairs = self.eng.enumerate_candidates(self.cfg["k"])
         torch.cuda.synchronize(dev)
-        self.t_setup = time.perf_counter() - t0
+        mark("enumerate_device")
         self.indel = INDEL_DEFAULT if indel is None else indel
         self.band = band
         self.kernel = self.eng.plan(10, -1, self.indel, band)
         self.a = self.b = None
         if host_list:
-            self.a, self.b = self.eng.candidates(self.cfg["k"])
+            self.a, self.b = self.eng.candidates_copy(self.n_pairs)
+            mark("candidates_to_host")
             self.a, self.b = np.array(self.a), np.array(self.b)
         self.pa, self.pb, _ = self.eng.candidates_device()
         self.ds = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
         self.de = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
         from ovlgraph.hostmem import pinned_empty
         self.out = (pinned_empty(self.n_pairs), pinned_empty(self.n_pairs))
+        t = time.perf_counter()
+        self.step()  # the first scoring call (code objects load, staging and heavy tiles built)
+        mark("first_call")
+        self.t_stages = st
+        self.t_setup = sum(st.values())
 
     def lens(self) -> np.ndarray:
         return np.fromiter((len(r) for r in self.reads), dtype=np.int64, count=len(self.reads))
@@ -339,13 +383,16 @@ def candidate_timing(w: Workload, reps: int = 5):
 
 def end_to_end(w: Workload, seed: int = 0):
     """``construct_overlap_graph_nx_k`` for this workload split into stages (not the metric): dedup +
-    device enumeration + scoring with results on the host; the DiGraph (direct builder vs networkx
-    ``add_edges_from``); then cycle removal (overlapGraphs.py:106-130) on that graph."""
+    encode + upload + device enumeration + scoring with results on the host (each stage itemised); the
+    DiGraph (direct builder vs networkx ``add_edges_from``); then cycle removal (overlapGraphs.py:106-130) on
+    that graph."""
     from ovlgraph import overlapGraphs as og
     from ovlgraph.reads import config_reads
     raw = config_reads(w.name, seed=seed)
+    og.overlap_edges_k(raw, w.cfg["k"], engine=w.eng)  # warm (allocations, pinned blocks)
+    stages = {}
     t0 = time.perf_counter()
-    edges = og.overlap_edges_k(raw, w.cfg["k"], engine=w.eng)
+    edges = og.overlap_edges_k(raw, w.cfg["k"], engine=w.eng, timing=stages)
     t1 = time.perf_counter()
     G = edges.to_digraph()
     t2 = time.perf_counter()
@@ -355,14 +402,16 @@ def end_to_end(w: Workload, seed: int = 0):
     assert n_e == G2.number_of_edges()
     del G2
     t4 = time.perf_counter()
-    stages = {}
-    og.remove_cycles_from_graph(G, timing=stages)
+    rc = {}
+    og.remove_cycles_from_graph(G, timing=rc)
     t5 = time.perf_counter()
     return {"reads": len(raw), "pairs": len(edges), "edges": n_e,
-            "dedup_enumerate_score_s": round(t1 - t0, 4), "digraph_direct_s": round(t2 - t1, 4),
+            "dedup_enumerate_score_s": round(t1 - t0, 4),
+            "dedup_enumerate_score_stages_s": {k: round(v, 5) for k, v in stages.items()},
+            "digraph_direct_s": round(t2 - t1, 4),
             "digraph_networkx_s": round(t3 - t2, 4), "end_to_end_s": round(t2 - t0, 4),
             "remove_cycles_s": round(t5 - t4, 4), "edges_removed": n_e - G.number_of_edges(),
-            "remove_cycles_stages_s": {k: round(stages[k], 4) for k in ("csr", "replay", "remove")}}
+            "remove_cycles_stages_s": {k: round(rc[k], 4) for k in ("csr", "replay", "remove")}}
 
 
 def local_alignment_timing(eng, reps: int = 5):
@@ -492,114 +541,263 @@ def single_process_all_gpus(rank: int, reads, k: int, steps: int, eng):
                     "store its slice into the caller's pinned arrays (no collective)"}
 
 
-def multi_gpu(args, world: int, rank: int, dev, backend: str):
-    """N > 1: one shared list (cfg4 by default) sharded over the ranks, results to rank 0's host."""
+def pair_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """SURVEY.md §8d algorithmic bytes of each pair (ceil(n/4) + ceil(m/4) + 16)."""
+    q = (lens + 3) // 4
+    return q[a] + q[b] + 16
+
+
+SINKS = {0: "int32 results in HBM (copy-engine transfer after)", 1: "int32 results stored into pinned host memory",
+         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)"}
+
+
+def kernel_name(w, sink: int, pairs: int) -> str:
+    """The uniform_kernel instantiation a launch of `pairs` pairs with result sink `sink` runs (ovl_plan
+    "ungapped", 2 bit planes, int32 keys; latency mode only at <= 8 tiles per CU)."""
+    if w.kernel != "ungapped":
+        return f"{w.kernel} kernel"
+    lmax = w.eng.info()["lmax"]
+    lat = (pairs + 63) // 64 <= 256 * 8
+    return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}>"
+
+
+def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
+    """The kernels that run INSIDE the timed step, each launch timed with HIP events on its stream
+    (ovl_set_timing / ovl_last_launches) over `reps` steps: per result sink, the median launch duration,
+    pairs and §8d algorithmic bytes per launch (the launch's own pair range), HBM fraction.  Returns
+    (roofline of the dominant in-step kernel, per-sink table, step-level roofline)."""
+    lens = w.lens()
+    cum = np.zeros(w.n_pairs + 1, dtype=np.int64)
+    np.cumsum(pair_bytes(lens, w.a, w.b), out=cum[1:])
+    w.eng.set_timing(True)
+    runs = []
+    for _ in range(reps):
+        w.step()
+        runs.append(w.eng.last_launches())
+    w.eng.set_timing(False)
+    by_sink = {}
+    for recs in runs:
+        off = 0
+        for r in recs:
+            lo, hi = off, off + r["pairs"]
+            off = hi
+            d = by_sink.setdefault(r["sink"], {"ms": [], "pairs": [], "bytes": []})
+            d["ms"].append(r["ms"])
+            d["pairs"].append(hi - lo)
+            d["bytes"].append(int(cum[hi] - cum[lo]))
+    table = []
+    for sink, d in sorted(by_sink.items()):
+        ms = float(np.median(d["ms"]))
+        pairs = int(np.median(d["pairs"]))
+        byts = int(np.median(d["bytes"]))
+        launches = len(d["ms"]) / reps
+        ach = byts / (ms * 1e-3) / 1e9
+        table.append({"sink": sink, "what": SINKS.get(sink, "?"), "kernel": kernel_name(w, sink, pairs),
+                      "launches_per_step": launches, "launch_ms": ms, "pairs_per_launch": pairs,
+                      "algorithmic_bytes_per_launch": byts, "achieved_gbs": ach, "frac": ach / HBM_PEAK_GBS,
+                      "ms_per_step": ms * launches})
+    dom = max(table, key=lambda t: t["ms_per_step"])
+    traffic = load_traffic(w.name, dom["kernel"])
+    roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"], "launch_ms": dom["launch_ms"],
+            "pairs_per_launch": dom["pairs_per_launch"],
+            "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
+            "launches_per_step": dom["launches_per_step"],
+            "what": "the step's dominant kernel (most kernel time inside ms_per_step): SURVEY §8d bytes of the "
+                    "pairs one launch scores / its median duration, HIP events on its launch stream inside the "
+                    "timed step's own call (ovl_last_launches); traffic: PMC FETCH+WRITE bytes per launch of "
+                    "that kernel (profiles/r03_*pmc*.json)"}
+    total = int(cum[-1])
+    step = {"bound": "hbm", "achieved": total / (ms_per_step * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "algorithmic_bytes_per_step": total,
+            "kernels_ms_per_step": sum(t["ms_per_step"] for t in table),
+            "what": "SURVEY §8d bytes of the whole list / ms_per_step (kernels, link and host expansion)"}
+    step["frac"] = step["achieved"] / HBM_PEAK_GBS
+    step["kernels_frac"] = total / (step["kernels_ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+    return roof, table, step
+
+
+def abi_one_shot(w, reps: int = 10):
+    """SURVEY.md §8(d) literally: the ABI call ``ovl_score_pairs`` with host-resident reads (raw bytes +
+    offsets) and a host pair list, results into host int32 arrays -- upload + pack of the reads, the pair
+    list over the link, kernels, results back -- at the workload's size; with the pair list in pinned and
+    in pageable host memory.  Checked against the resident-list step's results."""
+    from ovlgraph.engine import encode_reads
+    from ovlgraph.hostmem import pinned_empty
+    enc = encode_reads(w.reads)
+    out = (pinned_empty(w.n_pairs), pinned_empty(w.n_pairs))
+    pa, pb = pinned_empty(w.n_pairs), pinned_empty(w.n_pairs)
+    pa[:] = w.a
+    pb[:] = w.b
+    ga, gb = np.ascontiguousarray(w.a), np.ascontiguousarray(w.b)
+    res = {"reads_bytes": int(enc[0].nbytes), "pairs": w.n_pairs}
+    ref = (np.array(w.out[0]), np.array(w.out[1]))
+    for label, (x, y) in (("pinned_pair_list", (pa, pb)), ("pageable_pair_list", (ga, gb))):
+        w.eng.score_pairs(w.reads, x, y, out=out, encoded=enc)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            w.eng.score_pairs(w.reads, x, y, out=out, encoded=enc)
+        dt = (time.perf_counter() - t0) / reps
+        ok = bool(np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]))
+        res[label] = {"ms_per_call": dt * 1e3, "pairs_per_s": w.n_pairs / dt, "matches_step": ok,
+                      "link_bytes": w.eng.last_transfer()["link_bytes"]}
+    # the call's two halves: ovl_set_reads (upload + pack) and ovl_score_host
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        w.eng.set_reads(w.reads, enc)
+    res["set_reads_ms"] = (time.perf_counter() - t0) / reps * 1e3
+    w.eng.enumerate_candidates(w.cfg["k"])  # the resident list again (set_reads dropped it)
+    res["what"] = ("ovl_score_pairs(seqs, offsets, n_reads, a_idx, b_idx, ...) per call: reads uploaded and packed "
+                   "every call, pair list read from host memory, (score, end) into pinned host arrays")
+    return res
+
+
+def gather_floats(vals, world: int, dev, backend: str):
+    """Every rank's values (a list of floats) on every rank: list of per-rank lists."""
+    import torch
+    import torch.distributed as dist
+    where = dev if backend == "nccl" else "cpu"
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=where)
+    rows = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(rows, t)
+    return [r.cpu().tolist() for r in rows]
+
+
+def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: int, warmup: int):
+    """One read set of `name`, its candidate list sharded by sum n*m over the ranks, every rank's results into
+    rank 0's shared pinned host buffer (ShardedStep, dest="host"); then rank 0 alone scores the whole list
+    on its GPU (the one-GPU time of the same workload, same run) while the others wait; parity of the
+    gathered result against that."""
     import torch
     import torch.distributed as dist
     from ovlgraph import OverlapEngine
     from ovlgraph.candidates import dedup_reads
+    from ovlgraph.hostmem import pinned_empty
     from ovlgraph.reads import CONFIGS, config_reads
     from ovlgraph.sharded import ShardedStep
-
-    name = args.config or "cfg4"
-    cfg = CONFIGS[name]
     t0 = time.perf_counter()
     reads, _ = dedup_reads(config_reads(name, seed=0))  # the same list on every rank
     eng = OverlapEngine(dev.index)
-    st = ShardedStep(reads, k=cfg["k"], engine=eng, dest="host")
-    t_setup = time.perf_counter() - t0
-    n = st.n_pairs
-    elapsed = timed_steps(st.step, args.steps, args.warmup, dev, world)
-    # the dominant kernel on this rank's shard alone (HIP events on the launch stream)
-    stream = torch.cuda.current_stream(dev)
-    lo, hi = st.lo, st.hi
-    ds = torch.empty(max(1, hi - lo), dtype=torch.int32, device=dev)
-    de = torch.empty_like(ds)
-    pa, pb, _ = eng.candidates_device()
-    launch = lambda: eng.score_device(pa + 4 * lo, pb + 4 * lo, hi - lo, ds.data_ptr(), de.data_ptr(),  # noqa
-                                      stream=stream.cuda_stream)
-    launch()
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        launch()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
-    # parity of the gathered result: rank 0 scores the whole list alone and compares
-    ok = 1.0
+    st = ShardedStep(reads, k=CONFIGS[name]["k"], engine=eng, dest="host")
+    setup = time.perf_counter() - t0
+    el = timed_steps(st.step, steps, warmup, dev, world)
+    el_max = max(r[0] for r in gather_floats([el], world, dev, backend))
+    one = None
+    ok = None
     if rank == 0:
-        sc, en = st.results()
-        full = eng.score_candidates()
-        ok = float(np.array_equal(sc, full[0]) and np.array_equal(en, full[1]))
-    # the RCCL alternative: results gathered into rank 0's HBM (dist.gather), not to its host
-    rccl = None
-    if not args.no_gather:
-        st2 = ShardedStep(reads, k=cfg["k"], engine=eng, dest="rank0")
-        el2 = timed_steps(st2.step, max(5, args.steps), 2, dev, world)
-        rccl = el2
-        st2.close()
-    band_sweep_line = None
-    if not args.no_extra:
-        # BASELINE configs[4] (cfg5 band-width sweep, "4xMI355X"): the same sharded step per band
-        band_sweep_line = sharded_band_sweep(world, rank, dev, eng, [8, 16, 32, 64, -1], args.sweep_indel,
-                                             args.sweep_steps, backend)
-    red = torch.tensor([elapsed, kernel_ms, 0.0 if ok else 1.0, rccl or 0.0, t_setup], dtype=torch.float64,
-                       device=dev if backend == "nccl" else "cpu")
-    dist.all_reduce(red, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms, bad, rccl_el, t_setup = (float(x) for x in red.tolist())
-    lens = np.fromiter((len(r) for r in reads), dtype=np.int64, count=len(reads))
+        got = st.results()
+        out = (pinned_empty(st.n_pairs), pinned_empty(st.n_pairs))
+        one = timed_steps(lambda: eng.score_candidates(out=out), steps, warmup, dev, 1)
+        ok = bool(np.array_equal(got[0], out[0]) and np.array_equal(got[1], out[1]))
+    dist.barrier()
     st.close()
-    single = None
-    if not args.no_extra:
-        single = single_process_all_gpus(rank, reads, cfg["k"], args.steps, eng)
-        dist.barrier()
+    eng.close()
     if rank != 0:
         return None
-    algo_per_rank = (n // world) * (2 * int((lens.max() + 3) // 4) + 16)
-    achieved = algo_per_rank / (kernel_ms * 1e-3) / 1e9
+    return {"workload": f"{name}: {WORKLOAD_DESC[name]}", "reads": len(reads), "pairs": st.n_pairs,
+            "ms_per_step": el_max / steps * 1e3, "pairs_per_s": st.n_pairs * steps / el_max,
+            "one_gpu_ms_per_step": one / steps * 1e3, "one_gpu_pairs_per_s": st.n_pairs * steps / one,
+            "speedup_vs_one_gpu": one / el_max, "matches_one_gpu": ok, "setup_s": round(setup, 2),
+            "scaling": "strong",
+            "what": "one shared list sharded by sum n*m, each rank's (score, end) into rank 0's shared pinned host "
+                    "buffer; one_gpu: rank 0 alone scores the whole list in the same run (others idle)"}
+
+
+def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
+    """N > 1: every rank runs the same workload (weak: its own read set; strong: a shard of one list)."""
+    import torch
+    import torch.distributed as dist
+    name = args.config or "target"
+    ident = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+             "devices_visible": torch.cuda.device_count(), "devices_shared": shared}
+    if shared:
+        ident["note"] = ("more ranks than visible GPUs: ranks share devices (flow rehearsal, gloo barriers) -- "
+                         "not a scaling number")
+    if args.scaling == "strong":
+        res = strong_scaling(name, world, rank, dev, backend, args.steps, args.warmup)
+        if rank != 0:
+            return None
+        return {"metric": METRIC, "value": res["pairs_per_s"], "unit": "overlap-pairs/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
+                "data": "synthetic",
+                "config": {"workload": res["workload"], "reads": res["reads"], "pairs": res["pairs"],
+                           "parallelism": f"pair-sharded x{world}: one process per GPU, one shared device-enumerated "
+                                          f"list, shards balanced by sum n*m, results into rank 0's shared pinned "
+                                          f"host buffer"},
+                **ident, "one_gpu_ms_per_step": res["one_gpu_ms_per_step"],
+                "speedup_vs_one_gpu": res["speedup_vs_one_gpu"], "matches_one_gpu": res["matches_one_gpu"],
+                "roofline": None, "cpu_baseline": None,
+                "cpu_baseline_note": "the CPU baseline runs on rank 0 at N = 1 only (bench contract)"}
+    # weak: every rank its own read set of the workload
+    w = Workload(name, seed=args.seed + rank, dev=dev)
+    el = timed_steps(w.step, args.steps, args.warmup, dev, world)
+    roof, table, step_roof = in_step_rooflines(w, el / args.steps * 1e3)
+    kms = kernel_timing(w, max(args.steps, 20), dev)
+    rows = gather_floats([el, w.n_pairs, len(w.reads), kms], world, dev, backend)
+    el_max = max(r[0] for r in rows)
+    pairs = [int(r[1]) for r in rows]
+    strong = None
+    if not args.no_extra:
+        strong = strong_scaling("cfg4", world, rank, dev, backend, max(5, args.steps // 2), 2)
+    if rank != 0:
+        return None
+    total = sum(pairs)
+    algo = w.algo_bytes()
+    ach = algo / (kms * 1e-3) / 1e9
     line = {
-        "metric": METRIC, "value": n * args.steps / elapsed, "unit": "overlap-pairs/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-        "data": "synthetic",
-        "config": {"workload": f"{name}: {WORKLOAD_DESC[name]}", "reads": len(reads), "pairs": n,
-                   "read_length": cfg["l"],
-                   "parallelism": f"pair-sharded x{world}: one process per GPU, one shared device-enumerated "
-                                  f"list, shards balanced by sum n*m, each rank's (score, end) DMA'd into rank 0's "
-                                  f"shared pinned host buffer",
-                   "kernel": eng.plan(), "scoring": {"match": 10, "mismatch": -1, "indel": -2 ** 31, "band": -1}},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_launch": algo_per_rank,
-                     "what": "slowest rank's shard kernel (uniform-length estimate of SURVEY §8d bytes)"},
-        "gather": {"dest": "rank 0 host (shared memory, per-rank DMA)", "bytes_per_step": 8 * n,
-                   "matches_single_gpu": bad == 0.0},
-        "setup_s": round(t_setup, 2),
+        "metric": METRIC, "value": total * args.steps / el_max, "unit": "overlap-pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el_max / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": f"{name}: {WORKLOAD_DESC[name]}", "pairs": total, "pairs_per_rank": pairs,
+                   "reads_per_rank": [int(r[2]) for r in rows], "read_length": w.cfg["l"],
+                   "seeds": [args.seed + r for r in range(world)],
+                   "parallelism": f"x{world} weak: one process per GPU, each scoring its own read set's "
+                                  f"device-enumerated list (graph builds side by side, as the reference's joblib "
+                                  f"workers), results into each rank's pinned host arrays; no data-path collective",
+                   "kernel": w.kernel, "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band}},
+        **ident,
+        "per_rank_ms_per_step": [r[0] / args.steps * 1e3 for r in rows],
+        "roofline": roof,
+        "in_step_kernels": table,
+        "step_roofline": step_roof,
+        "kernel_only_roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": ach / HBM_PEAK_GBS, "kernel_ms": max(r[3] for r in rows),
+                                 "algorithmic_bytes_per_launch": algo, "traffic": load_traffic(name, kernel_name(w, 0, w.n_pairs)),
+                                 "what": "rank 0's list through the HBM-output kernel alone (not in the step)"},
         "cpu_baseline": None,
+        "cpu_baseline_note": "the CPU baseline runs on rank 0 at N = 1 only (bench contract); see the N = 1 line",
     }
-    if band_sweep_line is not None:
-        line["cfg5_band_sweep_sharded"] = band_sweep_line
-    if single is not None:
-        line["single_process_all_gpus"] = single
-    if rccl_el:
-        line["rccl_gather_to_rank0_hbm"] = {"ms_per_step": rccl_el / max(5, args.steps) * 1e3,
-                                            "pairs_per_s": n * max(5, args.steps) / rccl_el,
-                                            "collective": "dist.gather (RCCL send/recv over xGMI)"
-                                            if backend == "nccl" else "dist.gather (gloo)"}
+    if strong is not None:
+        line["cfg4_strong_scaling"] = strong
     return line
 
 
-def main() -> None:
+def spawn_ranks(n: int) -> int:
+    """--gpus N > 1 without a launcher: run torch.distributed.run with N ranks of this script as a child
+    process (never an exec: nothing here has touched the GPU) and return its exit status."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default=None, choices=sorted(WORKLOAD_DESC),
-                    help="workload (default: target at N=1, cfg4 at N>1)")
+                    help="workload at every N (default: the north_star target point)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="N > 1: weak = a read set per rank, strong = one list sharded over the ranks")
+    ap.add_argument("--seed", type=int, default=0, help="read-set seed (weak scaling: rank r uses seed + r)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the extra single-GPU configs and stages")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra configs and stages")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of all-core CPU-baseline work")
     ap.add_argument("--indel", type=int, default=None, help="indel score (default: the reference's -2**31)")
     ap.add_argument("--band", type=int, default=-1, help="band half-width (-1 = full DP, the reference)")
@@ -607,8 +805,61 @@ def main() -> None:
                     help="comma list of bands (-1 = full) timed on the same workload at --sweep-indel")
     ap.add_argument("--sweep-indel", type=int, default=-2)
     ap.add_argument("--sweep-steps", type=int, default=5)
-    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the RCCL gather-to-rank-0 timing")
-    args = ap.parse_args()
+    # launcher checks without a GPU (tests/test_bench_launch.py): ranks join a gloo group, rank 0 prints the
+    # identity line, and --dry-run-fail-rank R makes rank R exit with status 3
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    return args
+
+
+def launch_plan(gpus: int, env) -> str:
+    """What this process does: "spawn" (start gpus ranks as a child launcher), "rank" (one rank of a
+    launched job), "single" (N = 1), or an error message when --gpus and WORLD_SIZE disagree."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "single"
+    try:
+        w = int(ws)
+    except ValueError:
+        return f"error: WORLD_SIZE={ws!r} is not an integer"
+    if w != gpus:
+        return f"error: --gpus {gpus} but WORLD_SIZE={w} (launch N ranks with --gpus N)"
+    return "rank" if w > 1 else "single"
+
+
+def dry_run(args) -> int:
+    """The launch path alone (no GPU): join the process group over gloo, report what the ranks saw."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    if rank == args.dry_run_fail_rank:
+        return 3
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"n_gpus": args.gpus, "world_size": dist.get_world_size() if world > 1 else 1,
+                          "backend": dist.get_backend() if world > 1 else None, "config": args.config,
+                          "scaling": args.scaling, "steps": args.steps, "warmup": args.warmup}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def main() -> int:
+    args = parse_args()
+    plan = launch_plan(args.gpus, os.environ)
+    if plan.startswith("error"):
+        print(f"bench.py: {plan}", file=sys.stderr)
+        return 2
+    if plan == "spawn":
+        return spawn_ranks(args.gpus)
+    if args.dry_run:
+        return dry_run(args)
 
     import torch
     import torch.distributed as dist
@@ -616,27 +867,31 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; ranks beyond the visible devices (flow rehearsal on a 1-GPU box) share them
-    local = local % max(1, torch.cuda.device_count())
+    n_dev = torch.cuda.device_count()  # (does not initialise the GPU)
+    shared = world > max(1, n_dev)
+    # one process per GPU; ranks beyond the visible devices (flow rehearsal on a 1-GPU box) share them, and
+    # RCCL refuses two ranks on one GPU, so those run gloo
+    local = local % max(1, n_dev)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    backend = os.environ.get("OVL_BENCH_BACKEND", "nccl")  # nccl = RCCL on ROCm; gloo only for rehearsal
+    backend = os.environ.get("OVL_BENCH_BACKEND") or ("gloo" if shared else "nccl")  # nccl = RCCL on ROCm
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-        line = multi_gpu(args, world, rank, dev, backend)
+        line = multi_gpu(args, world, rank, dev, backend, shared)
         if rank == 0:
             print(json.dumps(line), flush=True)
         dist.barrier()
         dist.destroy_process_group()
-        return
+        return 0
 
     name = args.config or "target"
-    w = Workload(name, seed=0, dev=dev, indel=args.indel, band=args.band)
+    w = Workload(name, seed=args.seed, dev=dev, indel=args.indel, band=args.band)
     elapsed = timed_steps(w.step, args.steps, args.warmup, dev, 1)
     ms_step = elapsed / args.steps * 1e3
+    roof, table, step_roof = in_step_rooflines(w, ms_step)
     kernel_ms = kernel_timing(w, max(args.steps, 20), dev)
     algo = w.algo_bytes()
     achieved = algo / (kernel_ms * 1e-3) / 1e9
@@ -650,7 +905,7 @@ def main() -> None:
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -659,6 +914,7 @@ def main() -> None:
             "reads": len(w.reads),
             "pairs": w.n_pairs,
             "read_length": w.cfg["l"],
+            "seed": args.seed,
             "step": "ovl_score_candidates: resident reads + device-enumerated list -> kernels storing over the "
                     "link -> (score, end) in pinned host int32 arrays (SURVEY.md §8d, results in host memory; "
                     "packed 2 B/pair chunks expanded by host threads while the next chunk scores, the last "
@@ -667,24 +923,23 @@ def main() -> None:
             "kernel": w.kernel,
             "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": load_traffic(name),
-            "kernel_ms": kernel_ms,
-            "algorithmic_bytes_per_launch": algo,
-            "what": "dominant kernel alone over the whole list (HIP events on its launch stream)",
-        },
-        "valu_roofline": valu_roofline(name, kernel_ms),
+        "roofline": roof,
+        "in_step_kernels": table,
+        "step_roofline": step_roof,
+        "kernel_only_roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(name, kernel_name(w, 0, w.n_pairs)), "kernel_ms": kernel_ms,
+            "algorithmic_bytes_per_launch": algo, "kernel": kernel_name(w, 0, w.n_pairs),
+            "what": "the same list through the kernel with HBM outputs alone (not in the step; HIP events on its "
+                    "launch stream)"},
+        "valu_roofline": valu_roofline(name, kernel_ms, kernel_name(w, 0, w.n_pairs)),
         "kernel_only_pairs_per_s": w.n_pairs / (kernel_ms * 1e-3),
         "step_breakdown": step_breakdown(w, ms_step),
-        "occupancy": load_profile(name).get("occupancy"),
-        "host_setup_s": {"read_simulation": round(w.t_sim, 3), "upload_pack_enumerate": round(w.t_setup, 4)},
+        "occupancy": load_profile(name, kernel_name(w, 0, w.n_pairs)).get("occupancy"),
+        "host_setup_s": dict(w.t_stages, read_simulation=round(w.t_sim, 4)),
     }
     if not args.no_extra:
+        line["abi_one_shot"] = abi_one_shot(w)
         line["host_paths"] = host_paths(w)
         line["candidates"] = candidate_timing(w)
         line["end_to_end"] = end_to_end(w)
@@ -717,7 +972,8 @@ def main() -> None:
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -19,6 +19,9 @@
 
 #include <emmintrin.h>
 #include <pthread.h>
+#include <sched.h>
+#include <sys/socket.h>
+#include <sys/un.h>
 #include <unistd.h>
 
 #include <new>
@@ -88,13 +91,6 @@ struct Knobs {
     int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
-    int32_t progressive = 0;      // OVL_PROGRESSIVE=1: whole-list calls into pinned arrays through the progressive
-                                  // transport (progressive_ok) instead of the chunked packed pipeline (measured,
-                                  // opt-in: interleaved on one box 0.167 vs 0.174 ms at the target point, but in
-                                  // six process pairs on two other boxes the chunked pipeline won every one)
-    int32_t pg_store = 1;         // OVL_PG_STORE: progressive line/flag stores, 0 system write-through, 1 device
-                                  // write-through, 2 non-temporal; +4 skips the wait before the flag (A/B knob;
-                                  // tools/prog_probe.py, target kernel in the call: 0.35 / 0.12 / 0.13 ms, +4 no change)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -174,17 +170,6 @@ struct Dev {
     int32_t out_mode = 0;            // result sink of the next ungapped launches (OvlUngappedArgs::host_out):
                                      // 0 HBM, 1 host-mapped int32 arrays, 2 host-mapped packed uint16
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
-    // progressive transport (sink 3): fine-grained pinned packed lines, escapes and tile flags, by list tile
-    uint16_t* pg_pk = nullptr;
-    int32_t* pg_esc = nullptr;
-    unsigned long long* pg_flag = nullptr;
-    uint16_t* pg_pk_dev = nullptr;
-    int32_t* pg_esc_dev = nullptr;
-    unsigned long long* pg_flag_dev = nullptr;
-    int64_t pg_tiles = 0;                // capacity in tiles
-    uint32_t pg_epoch = 0;               // last call's flag tag
-    std::vector<uint8_t> pg_heavy;       // per list tile: 1 = heavy (no flag; stored as int32 by the kernel)
-    int64_t pg_heavy_for = -1;           // cand_n pg_heavy was built for
 };
 
 struct ovl_ctx {
@@ -193,6 +178,12 @@ struct ovl_ctx {
     std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
     int32_t timing = 0;          // ovl_set_timing
     double t_kernel_ms = 0.0, t_call_ms = 0.0;
+    struct Launch {
+        int32_t device, sink;
+        int64_t pairs;
+        double ms;
+    };
+    std::vector<Launch> t_launches;  // timing on: every scoring launch of the last host-array call
     int64_t x_link_bytes = 0, x_packed_pairs = 0;  // ovl_last_transfer
 };
 
@@ -464,13 +455,6 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
         g.host_out = c->out_mode;
-        if (g.host_out == 3) {
-            g.pg_pk = c->pg_pk_dev;
-            g.pg_esc = c->pg_esc_dev;
-            g.pg_flag = c->pg_flag_dev;
-            g.pg_epoch = c->pg_epoch;
-            g.pg_mode = (uint32_t)c->k.pg_store;
-        }
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
         if (c->k.heavy_first && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
@@ -629,8 +613,6 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_HEAVY_FIRST")) k.heavy_first = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PROGRESSIVE")) k.progressive = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PG_STORE")) k.pg_store = std::max(0, std::min(7, atoi(e)));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
         k.pack_adapt = 0;  // a fixed share
@@ -642,13 +624,125 @@ Knobs read_knobs() {
     return k;
 }
 
-// Host copies between pageable caller arrays and the pinned staging rings, split over a few worker threads
-// (one thread copies ~10 GB/s; a 16 MB result column is ~1.5 ms alone).  The pool is created on first
-// use in each process (a forked joblib worker builds its own) and sized by OVL_HOST_THREADS (default:
-// min(12, hardware threads, the CPU quota share)).
+// Processes that share this process's CPUs and drive libovl (the reference's joblib workers, experiments.py:537
+// n_jobs=-1, or torch.distributed ranks).  Each such process holds one abstract unix socket bound to
+// "\0ovl-share-<uid>-<cpu set hash>-<slot>": binding fails while another live process holds the slot and the
+// kernel releases it when the holder exits, so nothing is left behind.  The count is refreshed at setup calls
+// (context creation, ovl_set_reads, ovl_candidates, ovl_host_pool), never inside a scoring call.
+class CpuShare {
+  public:
+    static constexpr int kSlots = 64;
+    static CpuShare& get() {
+        static std::mutex mu;
+        std::lock_guard<std::mutex> lk(mu);
+        static CpuShare* one = nullptr;
+        if (!one || one->pid_ != getpid()) {  // a forked child holds no slot of its own yet
+            if (one && one->fd_ >= 0) close(one->fd_);  // (the parent's slot stays bound through its own fd)
+            one = new CpuShare();
+        }
+        return *one;
+    }
+    // CPUs this process may run on: its affinity set, capped by the cgroup quota (cpu.max)
+    int cpus() const { return cpus_; }
+    int sharers() const { return sharers_.load(std::memory_order_relaxed); }
+    // join (once per process) and recount: max(bound slots, LOCAL_WORLD_SIZE), at least 1
+    int refresh() {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (fd_ < 0) fd_ = bind_slot(-1);
+        int bound = 0;
+        for (int i = 0; i < kSlots; ++i) {
+            if (i == slot_) {
+                ++bound;
+                continue;
+            }
+            const int f = bind_slot(i);
+            if (f == -2) ++bound;  // in use: a live process holds it
+            else if (f >= 0) close(f);
+        }
+        int ranks = 1;
+        if (const char* e = getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, atoi(e));
+        const int n = std::max(std::max(bound, ranks), 1);
+        sharers_.store(n, std::memory_order_relaxed);
+        return n;
+    }
+
+  private:
+    CpuShare() : pid_(getpid()) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        int n = 0;
+        uint64_t h = 1469598103934665603ull ^ (uint64_t)getuid();
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+            n = CPU_COUNT(&set);
+            for (int c = 0; c < CPU_SETSIZE; ++c)
+                if (CPU_ISSET(c, &set)) h = (h ^ (uint64_t)c) * 1099511628211ull;
+        }
+        if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+        long long quota = 0, period = 0;
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            if (fscanf(f, "%lld %lld", &quota, &period) != 2) quota = period = 0;  // "max ..." stays 0
+            fclose(f);
+        }
+        if (quota > 0 && period > 0) n = std::min<int>(n, (int)std::max<long long>(1, quota / period));
+        cpus_ = n;
+        snprintf(key_, sizeof(key_), "ovl-share-%u-%016llx", (unsigned)getuid(), (unsigned long long)h);
+    }
+    // slot < 0: bind the first free slot and keep it (returns its fd, or -1); slot >= 0: probe it (returns a
+    // bound fd the caller closes, -2 when it is in use, -1 on any other failure)
+    int bind_slot(int slot) {
+        for (int i = slot < 0 ? 0 : slot; i < (slot < 0 ? kSlots : slot + 1); ++i) {
+            const int fd = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+            if (fd < 0) return -1;
+            sockaddr_un a;
+            memset(&a, 0, sizeof(a));
+            a.sun_family = AF_UNIX;
+            const int len = snprintf(a.sun_path + 1, sizeof(a.sun_path) - 1, "%s-%d", key_, i);
+            if (bind(fd, reinterpret_cast<sockaddr*>(&a), (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + len)) == 0) {
+                if (slot < 0) slot_ = i;
+                return fd;
+            }
+            const int err = errno;
+            close(fd);
+            if (err != EADDRINUSE) return -1;
+            if (slot >= 0) return -2;
+        }
+        return -1;
+    }
+    pid_t pid_;
+    int cpus_ = 1;
+    int fd_ = -1, slot_ = -1;
+    char key_[64];
+    std::atomic<int> sharers_{1};
+    std::mutex mu_;
+};
+
+// Threads of the host pool for `cpus` CPUs shared by `sharers` processes: OVL_POOL_THREADS (or the older
+// OVL_HOST_THREADS) when set, else 12 (three processes each of 6 / 8 / 12 threads on the box, a 16-CPU share:
+// packed step 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms, profiles/r02_pool_threads_*.json), at most the
+// process's part of the CPUs less one for its own thread, at least 1.
+int pool_rule(int cpus, int sharers, int env_threads) {
+    if (env_threads > 0) return std::min(64, env_threads);
+    return std::max(1, std::min(12, cpus / std::max(1, sharers) - 1));
+}
+
+int env_pool_threads() {
+    for (const char* k : {"OVL_POOL_THREADS", "OVL_HOST_THREADS"})
+        if (const char* e = getenv(k)) return std::max(0, atoi(e));
+    return 0;
+}
+
+// Host copies between pageable caller arrays and the pinned staging rings, and the expansion of packed results,
+// split over a pool of worker threads (one thread copies ~10 GB/s; a 16 MB result column is ~1.5 ms alone).  The
+// pool is created on first use in each process (a forked joblib worker builds its own) with the threads the
+// rule gives one process alone; a call uses the threads the rule gives with the current sharer count, and the
+// workers and the caller poll for work only while this process has its CPUs to itself.
 class CopyPool {
   public:
-    static int threads() { return planned_threads(); }
+    // threads a call uses now (the calling thread included)
+    static int threads() {
+        const CpuShare& cs = CpuShare::get();
+        return pool_rule(cs.cpus(), cs.sharers(), env_pool_threads());
+    }
     static CopyPool& get() {
         static const int registered = pthread_atfork(nullptr, nullptr, &CopyPool::after_fork);
         (void)registered;
@@ -659,7 +753,9 @@ class CopyPool {
     // f(lo, hi) over [0, n) cut into parts of >= min_part items (multiples of 64), on the workers and the
     // calling thread
     void parallel(size_t n, size_t min_part, const std::function<void(size_t, size_t)>& f) {
-        const size_t parts = std::min<size_t>(workers_.size() + 1, n / std::max<size_t>(min_part, 1));
+        const size_t use = (size_t)std::min<int>(threads(), (int)workers_.size() + 1);
+        spin_us_.store(CpuShare::get().sharers() > 1 ? 0 : spin_cfg_, std::memory_order_relaxed);
+        const size_t parts = std::min<size_t>(use, n / std::max<size_t>(min_part, 1));
         if (parts <= 1) {
             f(0, n);
             return;
@@ -705,31 +801,11 @@ class CopyPool {
         new (&get_mutex()) std::mutex();
         pool_ = nullptr;
     }
-    // Threads of the pool (the calling thread included): OVL_HOST_THREADS, else 12 (three processes each of
-    // 6 / 8 / 12 threads on the box, a 16-CPU share: packed step 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms,
-    // profiles/r02_pool_threads_*.json; 15 threads, alternating with 12 over three process pairs on each of two
-    // boxes, won all three on one and lost two of three on the other: profiles/r02_prog_threads_*.json), capped by the hardware threads and by this process's part of the
-    // job's CPU quota (cgroup cpu.max divided over LOCAL_WORLD_SIZE ranks, one CPU left for the rank's own
-    // thread), at least 1.
-    static int planned_threads() {
-        static const int n = [] {
-            if (const char* e = getenv("OVL_HOST_THREADS")) return std::max(1, std::min(64, atoi(e)));
-            int t = (int)std::min<unsigned>(12u, std::max(1u, std::thread::hardware_concurrency()));
-            long long quota = 0, period = 0;
-            if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-                if (fscanf(f, "%lld %lld", &quota, &period) != 2) quota = period = 0;  // "max ..." stays 0
-                fclose(f);
-            }
-            int ranks = 1;
-            if (const char* e = getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, atoi(e));
-            if (quota > 0 && period > 0) t = std::min<int>(t, (int)(quota / period / ranks) - 1);
-            return std::max(1, t);
-        }();
-        return n;
-    }
     CopyPool() : pid_(getpid()) {
-        const int n = planned_threads();
-        if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_us_ = std::max(0, std::min(100000, atoi(e)));
+        // workers for this process alone (sharers 1); calls with more sharers use fewer of them
+        const int n = pool_rule(CpuShare::get().cpus(), 1, env_pool_threads());
+        if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_cfg_ = std::max(0, std::min(100000, atoi(e)));
+        spin_us_.store(spin_cfg_, std::memory_order_relaxed);
         for (int i = 0; i + 1 < n; ++i) {
             std::thread t([this] { run(); });
             t.detach();  // lives with the process; never joined at exit
@@ -740,8 +816,9 @@ class CopyPool {
     template <typename F>
     bool spin_until(F ready) const {
         if (ready()) return true;
-        if (spin_us_ <= 0) return false;
-        const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us_);
+        const int us = spin_us_.load(std::memory_order_relaxed);
+        if (us <= 0) return false;
+        const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
         for (int i = 1;; ++i) {
             _mm_pause();
             if (ready()) return true;
@@ -774,7 +851,8 @@ class CopyPool {
     std::vector<std::function<void()>> tasks_;
     std::atomic<size_t> queued_{0};   // tasks_.size(), readable without mu_ by polling workers
     std::atomic<size_t> pending_{0};  // tasks of the current batch not finished yet
-    int spin_us_ = 100;               // OVL_POOL_SPIN_US
+    int spin_cfg_ = 100;              // OVL_POOL_SPIN_US
+    std::atomic<int> spin_us_{100};   // 0 while other processes share this CPU set
     std::mutex mu_, call_mu_;
     std::condition_variable cv_, done_;
 };
@@ -824,8 +902,6 @@ void destroy_dev(Dev* d) {
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
     free_staging(d->st_out);
-    for (void* q : {(void*)d->pg_pk, (void*)d->pg_esc, (void*)d->pg_flag})
-        if (q) (void)hipHostFree(q);
     if (d->h_flag) (void)hipHostFree(d->h_flag);
     for (int i = 0; i < kSlots; ++i)
         for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i]})
@@ -886,6 +962,7 @@ int create_on(const int32_t* ids, int32_t n, ovl_ctx** out) {
             if (ids[j] == ids[i]) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "device %d listed twice", ids[i]);
     }
     DeviceGuard guard;
+    CpuShare::get().refresh();
     ovl_ctx* c = new ovl_ctx();
     const Knobs knobs = read_knobs();
     for (int32_t i = 0; i < n; ++i) {
@@ -1298,6 +1375,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     }
     trace.mark('y', 0);
     double kms = 0.0;
+    c->t_launches.clear();
     for (Job& J : jobs) {
         Dev* d = J.d;
         if (J.nchunks == 0) continue;
@@ -1310,6 +1388,10 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
             for (int64_t k = 0; k < J.nchunks; ++k) {
                 float ms = 0.f;
                 if (hipEventElapsedTime(&ms, d->t_ev[2 * k], d->t_ev[2 * k + 1]) == hipSuccess) s += ms;
+                // the chunk's result sink (issue_chunk_direct): packed staging, int32 into host memory; copy-engine
+                // mode stores into HBM
+                const int32_t sink = !C.direct ? 0 : (C.pack && k < J.n_packed ? 2 : 1);
+                c->t_launches.push_back({d->device, sink, J.cb[(size_t)k + 1] - J.cb[(size_t)k], (double)ms});
             }
             kms = std::max(kms, s);
         }
@@ -1388,169 +1470,12 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
 bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) {
     const Dev* d = c->devs[0];
     const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 4;
-    // (the expansion needs the host pool: with fewer than 6 threads, e.g. many ranks on one CPU quota, the
-    // int32 stores over the link are faster)
+    // (the expansion needs the host pool: with fewer than 6 threads -- several processes on one CPU set, e.g.
+    // joblib workers or many ranks on one quota (CpuShare) -- the int32 stores over the link are faster)
     return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
            p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
-}
-
-// Progressive transport (sink 3) for a whole-list call into pinned arrays on one device: ONE launch of the
-// uniform kernel; each tile without side pairs publishes its packed results (one 128-B line of uint16, put_pair's
-// sink-2 encoding) and then a 64-bit flag (epoch << 32 | checksum) into fine-grained host memory with
-// write-through stores as it finishes, and the host pool expands tiles into the caller's int32 arrays as their
-// flags arrive, while the kernel still runs (the chunked pipeline waits for a whole chunk's launch).  Heavy tiles
-// (side pairs) store int32 straight into the arrays.  A flag is taken only with the line's checksum, so a line
-// that lands after its flag is waited for; one that never matches fails the call (never silently).
-bool progressive_ok(const ovl_ctx* c, const Plan& p, int64_t lo, int64_t hi, bool out_pinned, bool pack) {
-    const Dev* d = c->devs[0];
-    return pack && out_pinned && d->k.progressive > 0 && d->k.heavy_first && c->devs.size() == 1 && lo == 0 &&
-           hi == d->cand_n && hi - lo >= d->k.pack_min && d->split_override < 0 && d->planes == 2 && !p.key64 &&
-           (hi + 63) / 64 > (int64_t)d->cu_count * 8;  // throughput mode (launch_score_chunk's rs_log2 == 0)
-}
-
-int run_progressive(ovl_ctx* c, const Call& C, int64_t n) {
-    Dev* d = c->devs[0];
-    const auto t0 = std::chrono::steady_clock::now();
-    PipeTrace trace;  // OVL_TRACE_PIPE: s setup, i launched, f first flag seen, x expanded, y synchronised
-    HIPCHK(c, hipSetDevice(d->device));
-    int rc = ensure_heavy(d);
-    if (rc != OVL_OK) return rc;
-    const int64_t n_tiles = (n + 63) / 64;
-    if (d->pg_tiles < n_tiles) {
-        for (void* q : {(void*)d->pg_pk, (void*)d->pg_esc, (void*)d->pg_flag})
-            if (q) (void)hipHostFree(q);
-        d->pg_pk = nullptr;
-        d->pg_esc = nullptr;
-        d->pg_flag = nullptr;
-        d->pg_tiles = 0;
-        HIPCHK(c, hipHostMalloc((void**)&d->pg_pk, (size_t)n_tiles * 64 * sizeof(uint16_t), kHostShared));
-        HIPCHK(c, hipHostMalloc((void**)&d->pg_esc, (size_t)n_tiles * 64 * sizeof(int32_t), kHostShared));
-        HIPCHK(c, hipHostMalloc((void**)&d->pg_flag, (size_t)n_tiles * sizeof(unsigned long long), kHostShared));
-        memset(d->pg_flag, 0, (size_t)n_tiles * sizeof(unsigned long long));
-        HIPCHK(c, hipHostGetDevicePointer((void**)&d->pg_pk_dev, d->pg_pk, 0));
-        HIPCHK(c, hipHostGetDevicePointer((void**)&d->pg_esc_dev, d->pg_esc, 0));
-        HIPCHK(c, hipHostGetDevicePointer((void**)&d->pg_flag_dev, d->pg_flag, 0));
-        d->pg_tiles = n_tiles;
-    }
-    if (d->pg_heavy_for != d->cand_n) {
-        d->pg_heavy.assign((size_t)n_tiles, 0);
-        for (int32_t t : d->h_heavy) d->pg_heavy[(size_t)t] = 1;
-        d->pg_heavy_for = d->cand_n;
-    }
-    if (++d->pg_epoch == 0) d->pg_epoch = 1;
-    const uint32_t epoch = d->pg_epoch;
-    void* ps = nullptr;
-    void* pe = nullptr;
-    HIPCHK(c, hipHostGetDevicePointer(&ps, C.out_s, 0));
-    HIPCHK(c, hipHostGetDevicePointer(&pe, C.out_e, 0));
-    *(volatile uint32_t*)d->h_flag = 0;
-    d->cur_flag = d->h_flag_dev;
-    d->out_mode = 3;
-    trace.mark('s', 0);
-    if (C.timing) {
-        while (d->t_ev.size() < 2) {
-            hipEvent_t ev;
-            HIPCHK(c, hipEventCreate(&ev));
-            d->t_ev.push_back(ev);
-        }
-        HIPCHK(c, hipEventRecord(d->t_ev[0], d->stream));
-    }
-    rc = launch_score(d, *C.plan, as<int32_t>(d->cand_a), as<int32_t>(d->cand_b), n, C.match, C.mismatch, C.indel,
-                      reinterpret_cast<int32_t*>(ps), reinterpret_cast<int32_t*>(pe), d->stream);
-    d->cur_flag = as<uint32_t>(d->err_flag);
-    d->out_mode = 0;
-    if (rc != OVL_OK) {
-        (void)hipStreamSynchronize(d->stream);
-        return rc;
-    }
-    if (C.timing) HIPCHK(c, hipEventRecord(d->t_ev[1], d->stream));
-    HIPCHK(c, hipEventRecord(d->ev_last, d->stream));
-    trace.mark('i', 0);
-    // the pool's threads take blocks of kB tiles round-robin in list order (the kernel finishes tiles roughly
-    // in that order); a block is expanded once all its light tiles' flags and checksums match
-    static const ovl_expand::Fn fx = [] {
-        const ovl_expand::Fn g = ovl_expand::pick(getenv("OVL_EXPAND_ISA"));
-        return g ? g : ovl_expand::pick(nullptr);
-    }();
-    constexpr int64_t kB = 8;
-    const int64_t n_blocks = (n_tiles + kB - 1) / kB;
-    const int P = std::max(1, CopyPool::threads());
-    std::atomic<int64_t> lost{0};
-    std::atomic<int> done{0};  // the kernel is known to have finished (set by whichever thread saw it first)
-    const uint16_t* pk = d->pg_pk;
-    const volatile unsigned long long* fl = d->pg_flag;
-    const uint8_t* heavy = d->pg_heavy.data();
-    std::vector<uint8_t> bad((size_t)n_tiles, 0);
-    auto ready = [&](int64_t t) {
-        std::atomic_signal_fence(std::memory_order_seq_cst);  // reload the line on every poll
-        const unsigned long long f = fl[t];
-        if ((uint32_t)(f >> 32) != epoch) return false;
-        const uint16_t* q = pk + t * 64;
-        uint32_t cs = 0;
-        for (uint32_t l = 0; l < 64; ++l) cs += (uint32_t)q[l] * (2 * l + 1);
-        return cs == (uint32_t)f;
-    };
-    CopyPool::get().parallel((size_t)P * 64, 64, [&](size_t lo_, size_t) {
-        const int64_t me = (int64_t)(lo_ / 64);
-        for (int64_t blk = me; blk < n_blocks; blk += P) {
-            const int64_t t0b = blk * kB, t1b = std::min(n_tiles, t0b + kB);
-            for (int64_t t = t0b; t < t1b; ++t) {
-                if (heavy[t]) continue;
-                for (int64_t spin = 1; !ready(t); ++spin) {
-                    _mm_pause();
-                    if ((spin & 1023) == 0) {
-                        if (!done.load(std::memory_order_acquire)) {
-                            if (hipEventQuery(d->ev_last) != hipErrorNotReady) done.store(1, std::memory_order_release);
-                        } else if (spin > 4096) {  // finished for a while and still no match: left to the check below
-                            bad[(size_t)t] = 1;
-                            lost.fetch_add(1, std::memory_order_relaxed);
-                            break;
-                        }
-                    }
-                }
-            }
-            // the block's pairs, light tiles only (heavy tiles' int32 results are the kernel's)
-            for (int64_t t = t0b; t < t1b; ++t) {
-                if (heavy[t] || bad[(size_t)t]) continue;
-                int64_t t1 = t + 1;
-                while (t1 < t1b && !heavy[t1] && !bad[(size_t)t1]) ++t1;
-                fx(C.out_s, C.out_e, pk, d->pg_esc, C.match, C.mismatch, d->k.pack_nt != 0, (size_t)(t * 64),
-                   (size_t)std::min(n, t1 * 64));
-                t = t1 - 1;
-            }
-        }
-    });
-    trace.mark('x', 0);
-    HIPCHK(c, hipStreamSynchronize(d->stream));
-    trace.mark('y', 0);
-    if (lost.load()) {  // the kernel is done: every light tile's line and flag must match now
-        for (int64_t t = 0; t < n_tiles; ++t) {
-            if (!bad[(size_t)t]) continue;
-            if (!ready(t))
-                return fail(c, OVL_E_HIP, "progressive transport: tile %lld never published its results", (long long)t);
-            fx(C.out_s, C.out_e, pk, d->pg_esc, C.match, C.mismatch, d->k.pack_nt != 0, (size_t)(t * 64),
-               (size_t)std::min(n, t * 64 + 64));
-        }
-    }
-    if (d->k.pack_nt) _mm_sfence();
-    if (*(volatile uint32_t*)d->h_flag) {
-        *d->h_flag = 0;
-        rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
-    }
-    double kms = 0.0;
-    if (C.timing) {
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, d->t_ev[0], d->t_ev[1]) == hipSuccess) kms = ms;
-    }
-    c->t_kernel_ms = kms;
-    c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    int64_t heavy_pairs = 0;
-    for (int32_t t : d->h_heavy) heavy_pairs += std::min<int64_t>(64, n - (int64_t)t * 64);
-    c->x_link_bytes = 2 * (n - heavy_pairs) + 8 * heavy_pairs + 8 * (n_tiles - (int64_t)d->h_heavy.size());
-    c->x_packed_pairs = n - heavy_pairs;
-    return rc;
 }
 
 int check_scoring_args(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* p) {
@@ -1649,6 +1574,21 @@ OVL_API int ovl_host_unregister(void* ptr) {
     return OVL_OK;
 }
 
+OVL_API int ovl_host_pool(int32_t* threads, int32_t* sharers, int32_t* cpus, int32_t* packed) {
+    CpuShare& cs = CpuShare::get();
+    const int n = cs.refresh();
+    const int t = CopyPool::threads();
+    if (threads) *threads = t;
+    if (sharers) *sharers = n;
+    if (cpus) *cpus = cs.cpus();
+    if (packed) *packed = t >= 6 ? 1 : 0;
+    return OVL_OK;
+}
+
+OVL_API int32_t ovl_host_pool_rule(int32_t cpus, int32_t sharers, int32_t env_threads) {
+    return pool_rule(cpus, sharers, env_threads);
+}
+
 OVL_API int ovl_set_timing(ovl_ctx* c, int32_t on) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     c->timing = on ? 1 : 0;
@@ -1659,6 +1599,22 @@ OVL_API int ovl_last_transfer(const ovl_ctx* c, int64_t* link_bytes, int64_t* pa
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (link_bytes) *link_bytes = c->x_link_bytes;
     if (packed_pairs) *packed_pairs = c->x_packed_pairs;
+    return OVL_OK;
+}
+
+OVL_API int ovl_last_launches(const ovl_ctx* c, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs,
+                              double* ms, int32_t* out_n) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (cap < 0) return fail(c, OVL_E_ARG, "cap < 0");
+    const int32_t n = (int32_t)c->t_launches.size();
+    if (out_n) *out_n = n;
+    for (int32_t i = 0; i < n && i < cap; ++i) {
+        const auto& L = c->t_launches[(size_t)i];
+        if (device) device[i] = L.device;
+        if (sink) sink[i] = L.sink;
+        if (pairs) pairs[i] = L.pairs;
+        if (ms) ms[i] = L.ms;
+    }
     return OVL_OK;
 }
 
@@ -1766,6 +1722,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
     if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
     DeviceGuard guard;
+    CpuShare::get().refresh();
     HostReads h;
     int rc = prep_reads(c, seqs, offsets, n_reads, h);
     if (rc != OVL_OK) return rc;
@@ -2030,6 +1987,7 @@ OVL_API int ovl_candidates(ovl_ctx* ctx, int32_t k, int64_t* out_n_pairs) {
         return fail(ctx, OVL_E_UNSUPPORTED, "k=%d with %d-bit symbols does not fit a 64-bit key (k * bits <= 58)", k,
                     bits);
     DeviceGuard guard;
+    CpuShare::get().refresh();
     // every device enumerates the same list from its own copy of the reads (no list broadcast); the
     // phases overlap across devices
     int rc = OVL_OK;
@@ -2124,7 +2082,6 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.timing = ctx->timing != 0;
     C.direct = ctx->devs[0]->k.pipe_direct != 0;
     C.pack = pack_ok(ctx, p, hi - lo, C.out_pinned);
-    if (C.direct && progressive_ok(ctx, p, lo, hi, C.out_pinned, C.pack)) return run_progressive(ctx, C, hi - lo);
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);

@@ -36,14 +36,7 @@ struct OvlUngappedArgs {
     int64_t tile_base;          // the launch's first pair / 64 within the list
     int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
                          // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
-                         // out_score as uint16, the score of the few pairs that need it in out_end; 3 progressive
-                         // packed: throughput-mode tiles without side pairs publish a packed line in pg_pk and a
-                         // flag in pg_flag (pg_epoch << 32 | checksum) as they finish, the rest as sink 1
-    uint16_t* pg_pk;     // sink 3: packed results by launch pair (host-mapped, fine-grained)
-    int32_t* pg_esc;     // sink 3: escaped scores by launch pair
-    unsigned long long* pg_flag;  // sink 3: one flag per launch tile
-    uint32_t pg_epoch;   // sink 3: this call's flag tag (nonzero)
-    uint32_t pg_mode;    // sink 3 store form: 0 system-scope write-through, 1 device-scope write-through, 2 nt
+                         // out_score as uint16, the score of the few pairs that need it in out_end
 };
 
 // kernels of the band knob (ovl_launch_dp); OVL_BAND_FORM env picks one for tests

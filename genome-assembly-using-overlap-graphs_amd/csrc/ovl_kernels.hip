@@ -96,52 +96,6 @@ __device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
     return match != mismatch ? 1.0f / (float)(match - mismatch) : 0.f;
 }
 
-// Sink 3 (progressive packed results): system-scope write-through vector stores into fine-grained host memory, so
-// the bytes leave for the link as they are issued (plain and non-temporal stores keep host-mapped lines in L2 until
-// the kernel's end; narrow write-through stores are slow per byte: each tile goes out as whole 16-B pieces).
-typedef unsigned int ovl_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store16_sys(void* p, ovl_u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store8_sys(void* p, unsigned long long v) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-// the progressive sink's line / flag stores by mode (OvlUngappedArgs::pg_mode): 0 system-scope write-through,
-// 1 device-scope write-through, 2 non-temporal (A/B knob OVL_PG_STORE)
-__device__ __forceinline__ void store16_pg(void* p, ovl_u32x4 v, uint32_t mode) {
-    if (mode == 0) store16_sys(p, v);
-    else if (mode == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    else __builtin_nontemporal_store(v, reinterpret_cast<ovl_u32x4*>(p));
-}
-__device__ __forceinline__ void store8_pg(void* p, unsigned long long v, uint32_t mode) {
-    if (mode == 0) store8_sys(p, v);
-    else if (mode == 1) asm volatile("global_store_dwordx2 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-    else __builtin_nontemporal_store(v, reinterpret_cast<unsigned long long*>(p));
-}
-__device__ __forceinline__ void store4_sys(void* p, uint32_t v) {
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
-}
-
-// The packed uint16 of one pair (put_pair's sink 2 encoding); an escaped score goes to esc[p] (write-through)
-__device__ __forceinline__ uint32_t pack_pair_sys(int32_t sc, int32_t en, int32_t n, int32_t match, float inv,
-                                                  int32_t* esc, int64_t p) {
-    if (en < 0) return 0xFFFFu;
-    if (en > n) {
-        store4_sys(esc + p, (uint32_t)sc);
-        return ((uint32_t)en << 8) | 0xFFu;
-    }
-    const uint32_t x = (uint32_t)__builtin_rintf((float)(match * en - sc) * inv);
-    return ((uint32_t)en << 8) | x;
-}
-
-// Tile checksum of the progressive transport: sum over lanes of v * (2 * lane + 1) (< 2^32), on every lane.
-__device__ __forceinline__ uint32_t tile_checksum(uint32_t v, int lane) {
-    uint32_t c = v * (uint32_t)(2 * lane + 1);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-    return c;
-}
-
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
 // would otherwise sum a block's word counts with an extra v_add3)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t v, uint32_t acc) {
@@ -684,14 +638,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     int32_t lw, const uint32_t* __restrict__ full, int32_t match, int32_t mismatch,
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag,
     const int32_t* __restrict__ heavy_ids, const uint8_t* __restrict__ tile_flags, int32_t heavy_n,
-    int64_t tile_base, uint16_t* __restrict__ pg_pk, int32_t* __restrict__ pg_esc,
-    unsigned long long* __restrict__ pg_flag, uint32_t pg_epoch, uint32_t pg_mode) {
+    int64_t tile_base) {
     using T = typename Key<KM>::T;
-    // sink 3 (OM == 3, throughput mode, int32 keys): the tiles without side pairs publish their packed results as one
-    // 128-B line (pg_pk, by launch tile) then a 64-bit flag (pg_epoch << 32 | tile checksum) the host polls; heavy tiles
-    // and the ring drains store int32 straight into the host-mapped arrays (sink 1), seen after the kernel's end
-    static_assert(OM != 3 || (KM == 0 && !LAT), "progressive sink: throughput mode, int32 keys");
-    constexpr int OD = OM == 3 ? 1 : OM;  // the sink of the drains and heavy tiles
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = (W * P + 3) & ~3;
@@ -704,7 +652,6 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     __shared__ int4 ring_all[LAT ? 1 : 4][RING];   // throughput mode: 8 KiB per block
     __shared__ int4 side_ent[LAT ? 2 : 1][64];     // latency mode: (p, -, n, m) per side pair
     __shared__ uint4 side_rows[LAT ? 2 * 64 * ROWQ : 1];
-    __shared__ ovl_u32x4 pg_line[OM == 3 ? 4 * 8 : 1];  // sink 3: a wavefront's 64 packed results (128 B)
     const int lane = threadIdx.x & 63;
     const int wib = threadIdx.x >> 6;              // wavefront in block
     // latency mode: 0 = sweep, 1 = side pairs; the side wave is the first of each pair in the block
@@ -724,7 +671,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         const bool mine = slot < count;
         int4 e = make_int4(0, 0, 0, 0);
         if (mine) e = ring[(head + slot) & (RING - 1)];
-        general_unit<P, W, KM, OD>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
+        general_unit<P, W, KM, OM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
                                      mismatch, out_score, out_end, err_flag);
         head += count;
     };
@@ -856,32 +803,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, 0u, 32u, tmask, tm);
 #endif
         OVL_TR_CLOCK(3, (uint32_t)best);
-        if constexpr (OM == 3) {
-            if (hf && item < heavy_n) {  // a heavy tile (wave-uniform): int32 straight into the host arrays
-                if (mine && (uni || tt || !ok)) {
-                    int32_t sc, en;
-                    Key<KM>::decode(best, sc, en);
-                    put_pair<1>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1);
-                }
-            } else {  // no side pairs here: every live lane is uniform, t-truncated or bad
-                uint32_t v = 0;
-                if (mine && (uni || tt || !ok)) {
-                    int32_t sc, en;
-                    Key<KM>::decode(best, sc, en);
-                    v = pack_pair_sys(ok ? sc : -1, ok ? en : -1, lw, match, pack_inv(match, mismatch), pg_esc, p);
-                }
-                const uint32_t cs = tile_checksum(v, lane);
-                uint16_t* line = reinterpret_cast<uint16_t*>(pg_line + wib * 8);
-                line[lane] = (uint16_t)v;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                const uint32_t form = pg_mode & 3u;
-                if (lane < 8) store16_pg(pg_pk + tile * 64 + lane * 8, pg_line[wib * 8 + lane], form);
-                // the line (and any escape) acknowledged before the flag goes out; mode bit 4 skips the wait (the
-                // host's checksum then waits for a line that lands after its flag)
-                if (!(pg_mode & 4u)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) store8_pg(pg_flag + tile, ((unsigned long long)pg_epoch << 32) | cs, form);
-            }
-        } else if (mine && (uni || tt || (!LAT && !ok))) {
+        if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
             put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, lw, match, pack_inv(match, mismatch));
@@ -1424,8 +1346,7 @@ static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStrea
     uniform_kernel<W, KM, LAT, OM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
                                                                 g.n_pairs, g.lw, g.full, g.match, g.mismatch,
                                                                 g.out_score, g.out_end, g.err_flag, g.heavy_ids,
-                                                                g.tile_flags, g.heavy_n, g.tile_base, g.pg_pk,
-                                                                g.pg_esc, g.pg_flag, g.pg_epoch, g.pg_mode);
+                                                                g.tile_flags, g.heavy_n, g.tile_base);
 }
 
 template <int W, int KM, bool LAT>
@@ -1436,12 +1357,6 @@ static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStrea
         case 2:
             if constexpr (KM == 0) {  // packed results: int32 keys only (the host asks for them only then)
                 launch_uniform_4<W, KM, LAT, 2>(g, blocks, stream);
-                return true;
-            }
-            return false;
-        case 3:
-            if constexpr (KM == 0 && !LAT) {  // progressive packed results (throughput mode)
-                launch_uniform_4<W, KM, LAT, 3>(g, blocks, stream);
                 return true;
             }
             return false;
@@ -1545,7 +1460,6 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->host_out >= 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
-    if (g->host_out == 3 && (g->rs_log2 != 0 || !g->pg_pk || !g->pg_esc || !g->pg_flag)) return hipErrorInvalidValue;
     if (g->lw > 0) {
         // rs_log2 > 0 here selects the latency mode
         const unsigned nb = grid_for((g->n_pairs << (g->rs_log2 > 0 ? 1 : 0)) +

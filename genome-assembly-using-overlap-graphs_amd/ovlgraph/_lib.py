@@ -42,8 +42,11 @@ SIGNATURES = {
     "ovl_host_free": (ctypes.c_int, [_P]),
     "ovl_host_register": (ctypes.c_int, [_P, _i64]),
     "ovl_host_unregister": (ctypes.c_int, [_P]),
+    "ovl_host_pool": (ctypes.c_int, [_pi32, _pi32, _pi32, _pi32]),
+    "ovl_host_pool_rule": (ctypes.c_int32, [_i32, _i32, _i32]),
     "ovl_set_timing": (ctypes.c_int, [_P, _i32]),
     "ovl_last_timing": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "ovl_last_launches": (ctypes.c_int, [_P, _i32, _P, _P, _P, _P, _pi32]),
     "ovl_last_transfer": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "ovl_last_error": (ctypes.c_char_p, [_P]),
     "ovl_score_pairs": (ctypes.c_int, [_P, _P, _P, _i32, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P]),

@@ -19,16 +19,18 @@ Indices refer to positions in the de-duplicated read list.
 """
 from __future__ import annotations
 
+from collections import Counter
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 
 
 def dedup_reads(reads: Sequence[str]) -> Tuple[List[str], List[int]]:
-    """Distinct reads in first-occurrence order plus their copy counts (overlapGraphs.py:18-20)."""
-    counts: Dict[str, int] = {}
-    for r in reads:
-        counts[r] = counts.get(r, 0) + 1
+    """Distinct reads in first-occurrence order plus their copy counts (overlapGraphs.py:18-20).
+
+    ``Counter`` counts in C and keeps first-insertion order, the order of the reference's
+    ``read_copies[read] = read_copies.get(read, 0) + 1`` loop."""
+    counts = Counter(reads)
     return list(counts.keys()), list(counts.values())
 
 

@@ -68,6 +68,13 @@ def _outputs(n: int, out) -> Tuple[np.ndarray, np.ndarray]:
     return sc[:n], en[:n]
 
 
+def host_pool() -> Dict[str, int]:
+    """The host thread pool's plan, recounted now (ovl_host_pool): {threads, sharers, cpus, packed}."""
+    v = [ctypes.c_int32() for _ in range(4)]
+    check(_lib.load().ovl_host_pool(*[ctypes.byref(x) for x in v]))
+    return dict(zip(("threads", "sharers", "cpus", "packed"), (x.value for x in v)))
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     rc = _lib.load().ovl_device_count(ctypes.byref(n))
@@ -98,6 +105,17 @@ class OverlapEngine:
             check(self._L.ovl_create_on_devices(_ptr(ids), 1, ctypes.byref(ctx)))
         self._ctx = ctx
         self._reads_key = None
+        self._dev0 = self.devices[0]  # device pointers given to score_device / score_tensors live here
+
+    def _check_tensors(self, what: str, *ts) -> None:
+        """Contiguous int32 tensors on this engine's first device (kernels there read and write them)."""
+        import torch
+        for t in ts:
+            if t.dtype != torch.int32 or not t.is_cuda or not t.is_contiguous():
+                raise OvlError(-1, f"{what} needs contiguous int32 device tensors")
+            if t.device.index != self._dev0:
+                raise OvlError(-1, f"{what}: tensor on cuda:{t.device.index}, but this engine's kernels run on "
+                                   f"cuda:{self._dev0}")
 
     @property
     def devices(self) -> List[int]:
@@ -116,6 +134,19 @@ class OverlapEngine:
         k, w = ctypes.c_double(), ctypes.c_double()
         check(self._L.ovl_last_timing(self._ctx, ctypes.byref(k), ctypes.byref(w)), self._ctx)
         return {"kernel_ms": k.value, "call_ms": w.value}
+
+    def last_launches(self) -> List[Dict[str, float]]:
+        """The scoring launches of the last host-array call made with timing on (ovl_last_launches):
+        [{device, sink (0 HBM, 1 int32 into host memory, 2 packed into host staging), pairs, ms}]."""
+        n = ctypes.c_int32()
+        check(self._L.ovl_last_launches(self._ctx, 0, None, None, None, None, ctypes.byref(n)), self._ctx)
+        k = n.value
+        dev, sink = np.zeros(max(k, 1), np.int32), np.zeros(max(k, 1), np.int32)
+        pairs, ms = np.zeros(max(k, 1), np.int64), np.zeros(max(k, 1), np.float64)
+        check(self._L.ovl_last_launches(self._ctx, k, _ptr(dev), _ptr(sink), _ptr(pairs), _ptr(ms),
+                                        ctypes.byref(n)), self._ctx)
+        return [{"device": int(dev[i]), "sink": int(sink[i]), "pairs": int(pairs[i]), "ms": float(ms[i])}
+                for i in range(min(k, n.value))]
 
     def last_transfer(self) -> Dict[str, int]:
         """{link_bytes, packed_pairs} of the last host-array scoring call (ovl_last_transfer)."""
@@ -168,7 +199,10 @@ class OverlapEngine:
         Same list and order as ``candidates.enumerate_candidates`` (overlapGraphs.py:30-52);
         the list also stays resident for ``score_candidates``.
         """
-        n = self.enumerate_candidates(k)
+        return self.candidates_copy(self.enumerate_candidates(k))
+
+    def candidates_copy(self, n: int) -> Tuple[np.ndarray, np.ndarray]:
+        """The resident candidate list (``n`` pairs, from ``enumerate_candidates``) in pinned host arrays."""
         a = pinned_empty(n)
         b = pinned_empty(n)
         if n:
@@ -239,6 +273,22 @@ class OverlapEngine:
         return sc, ei, ej, si, sj, (ops[: k.value] if traceback else None)
 
     # ---------------------------------------------------------------- scoring
+    def score_pairs(self, reads: Sequence[str], a_idx, b_idx, match: int = 10, mismatch: int = -1,
+                    indel: int = INDEL_DEFAULT, band: int = -1, out=None,
+                    encoded: Optional[Tuple[np.ndarray, np.ndarray]] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """The one-shot ABI call ``ovl_score_pairs``: host reads + host pair list -> host
+        (score, end); the reads are uploaded, packed and left resident (as ``set_reads``)."""
+        buf, offs = encoded if encoded is not None else encode_reads(reads)
+        a = np.ascontiguousarray(a_idx, dtype=np.int32)
+        b = np.ascontiguousarray(b_idx, dtype=np.int32)
+        if a.shape != b.shape or a.ndim != 1:
+            raise OvlError(-1, "a_idx and b_idx must be 1-D arrays of equal length")
+        sc, en = _outputs(a.shape[0], out)
+        check(self._L.ovl_score_pairs(self._ctx, _ptr(buf), _ptr(offs), offs.shape[0] - 1, _ptr(a), _ptr(b),
+                                      a.shape[0], match, mismatch, indel, band, _ptr(sc), _ptr(en)), self._ctx)
+        self._reads_key = id(reads)
+        return sc, en
+
     def score(self, a_idx, b_idx, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
               band: int = -1, out=None) -> Tuple[np.ndarray, np.ndarray]:
         """Score pairs (host arrays) against the resident reads -> (score, end) int32 arrays
@@ -264,9 +314,7 @@ class OverlapEngine:
                       indel: int = INDEL_DEFAULT, band: int = -1, stream=None) -> None:
         """torch int32 device tensors in/out, launched on torch's current stream (or `stream`)."""
         import torch
-        for t in (a, b, out_score, out_end):
-            if t.dtype != torch.int32 or not t.is_cuda or not t.is_contiguous():
-                raise OvlError(-1, "score_tensors needs contiguous int32 device tensors")
+        self._check_tensors("score_tensors", a, b, out_score, out_end)
         n = a.numel()
         if b.numel() != n or out_score.numel() < n or out_end.numel() < n:
             raise OvlError(-1, "tensor sizes disagree")
@@ -283,9 +331,7 @@ class OverlapEngine:
         The tensors must stay alive while the launcher is used.
         """
         import torch
-        for t in (a, b, out_score, out_end):
-            if t.dtype != torch.int32 or not t.is_cuda or not t.is_contiguous():
-                raise OvlError(-1, "launcher needs contiguous int32 device tensors")
+        self._check_tensors("launcher", a, b, out_score, out_end)
         n = a.numel()
         if b.numel() != n or out_score.numel() < n or out_end.numel() < n:
             raise OvlError(-1, "tensor sizes disagree")

@@ -38,16 +38,32 @@ CANDIDATE_MODES = ("auto", "device", "host")
 
 
 def _score(distinct: Sequence[str], a: np.ndarray, b: np.ndarray, engine: Optional[OverlapEngine],
-           scorer=None) -> Tuple[List[int], List[int]]:
+           scorer=None, encoded=None) -> Tuple[np.ndarray, np.ndarray]:
+    """(score, end) int32 arrays of the pairs (a, b) in one batched call (or through ``scorer``)."""
     if a.shape[0] == 0:
-        return [], []
+        return np.zeros(0, np.int32), np.zeros(0, np.int32)
     if scorer is not None:  # (score, end) arrays from another backend, e.g. the sharded path
         sc, en = scorer(distinct, a, b)
     else:
         eng = engine or default_engine()
-        eng.set_reads(distinct)
+        eng.set_reads(distinct, encoded)
         sc, en = eng.score(a, b, 10, -1, INDEL_DEFAULT)
-    return np.asarray(sc).tolist(), np.asarray(en).tolist()
+    return np.asarray(sc, dtype=np.int32), np.asarray(en, dtype=np.int32)
+
+
+class _Stages:
+    """Wall-clock stages of a graph build into a caller's dict (``timing=``), or nothing."""
+
+    def __init__(self, out: Optional[dict]):
+        import time
+        self.out, self._clock = out, time.perf_counter
+        self._t = self._clock()
+
+    def __call__(self, name: str) -> None:
+        if self.out is not None:
+            t = self._clock()
+            self.out[name] = self.out.get(name, 0.0) + (t - self._t)
+            self._t = t
 
 
 def _node_names(distinct: Sequence[str], counts: Sequence[int]) -> List[List[str]]:
@@ -86,32 +102,48 @@ def assemble_graph(distinct: Sequence[str], counts: Sequence[int], a, b, score, 
 
 
 def candidates_and_scores(distinct: Sequence[str], k: int, engine: Optional[OverlapEngine] = None, scorer=None,
-                          candidates: str = "auto"):
-    """Candidate pairs (overlapGraphs.py:30-52) and their (score, end) (:53), in reference order.
+                          candidates: str = "auto", timing: Optional[dict] = None):
+    """Candidate pairs (overlapGraphs.py:30-52) and their (score, end) (:53), in reference order, as
+    int32 arrays.
 
     ``candidates``: "device" enumerates on the GPU (list kept resident and scored
     without a host round trip), "host" uses ``enumerate_candidates``, "auto" is
     "device" unless the k-mer keys do not fit the device path (OVL_E_UNSUPPORTED).
     A custom ``scorer`` (e.g. the sharded path) always gets host-enumerated pairs.
+    ``timing``: a dict that receives the stage times (s): encode, set_reads, enumerate,
+    candidates_copy, score (host enumeration: enumerate_host).
     """
+    from .engine import encode_reads
     if candidates not in CANDIDATE_MODES:
         raise ValueError(f"candidates must be one of {CANDIDATE_MODES}")
+    st = _Stages(timing)
     if scorer is not None or candidates == "host":
         a, b = enumerate_candidates(distinct, k)
+        st("enumerate_host")
         sc, en = _score(distinct, a, b, engine, scorer)
+        st("score")
         return a, b, sc, en
     eng = engine or default_engine()
-    eng.set_reads(distinct)
+    enc = encode_reads(distinct)
+    st("encode")
+    eng.set_reads(distinct, enc)
+    st("set_reads")
     try:
-        a, b = eng.candidates(k)
+        n = eng.enumerate_candidates(k)
     except OvlError as e:
         if e.code != -4 or candidates == "device":
             raise
         a, b = enumerate_candidates(distinct, k)
-        sc, en = _score(distinct, a, b, eng, None)
+        st("enumerate_host")
+        sc, en = _score(distinct, a, b, eng, None, enc)
+        st("score")
         return a, b, sc, en
+    st("enumerate")
+    a, b = eng.candidates_copy(n)
+    st("candidates_copy")
     sc, en = eng.score_candidates(10, -1, INDEL_DEFAULT)
-    return a, b, sc.tolist(), en.tolist()
+    st("score")
+    return a, b, sc, en
 
 
 def assemble_graph_direct(distinct: Sequence[str], counts: Sequence[int], a, b, score, end,
@@ -304,13 +336,16 @@ def engine_on(devices) -> OverlapEngine:
 
 
 def overlap_edges_k(reads, k=5, engine: Optional[OverlapEngine] = None, scorer=None,
-                    candidates: str = "auto", devices=None) -> OverlapEdges:
-    """Scored k-mer candidates of ``construct_overlap_graph_nx_k`` as columns (no networkx)."""
+                    candidates: str = "auto", devices=None, timing: Optional[dict] = None) -> OverlapEdges:
+    """Scored k-mer candidates of ``construct_overlap_graph_nx_k`` as columns (no networkx).
+    ``timing``: a dict that receives the stage times (s), dedup first (candidates_and_scores)."""
     assert k >= 0, "k-mer length must be non-negative"
     if engine is None and devices is not None:
         engine = engine_on(devices)
+    st = _Stages(timing)
     distinct, counts = dedup_reads(reads)
-    a, b, sc, en = candidates_and_scores(distinct, k, engine, scorer, candidates)
+    st("dedup")
+    a, b, sc, en = candidates_and_scores(distinct, k, engine, scorer, candidates, timing)
     return OverlapEdges(distinct, counts, a, b, sc, en)
 
 
@@ -353,7 +388,7 @@ def construct_string_graph(reads, engine: Optional[OverlapEngine] = None, scorer
         a = b = np.zeros(0, dtype=np.int32)
     sc, en = _score(distinct, np.ascontiguousarray(a), np.ascontiguousarray(b), engine, scorer)
     G.add_edges_from((distinct[x], distinct[y], {"weight": s, "end_position": e})
-                     for x, y, s, e in zip(a.tolist(), b.tolist(), sc, en) if s > 0)
+                     for x, y, s, e in zip(a.tolist(), b.tolist(), sc.tolist(), en.tolist()) if s > 0)
     print(f"graph: {G.edges}")
     return G
 

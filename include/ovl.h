@@ -84,14 +84,29 @@ int ovl_host_free(void* ptr);
 int ovl_host_register(void* ptr, int64_t bytes);
 int ovl_host_unregister(void* ptr);
 
+/* Host thread pool of the result transport (expansion of packed results, copies of pageable arrays), recounted
+ * now: *cpus = this process's CPUs (affinity set, capped by the cgroup quota), *sharers = processes driving
+ * libovl on the same CPU set (other libovl processes of this user with the same affinity, e.g. joblib workers,
+ * or LOCAL_WORLD_SIZE when larger), *threads = threads a call uses (ovl_host_pool_rule), *packed = 1 when the
+ * packed transport may be used (>= 6 threads; otherwise results cross as int32 and the pool does not poll).
+ * Any output pointer may be NULL. */
+int ovl_host_pool(int32_t* threads, int32_t* sharers, int32_t* cpus, int32_t* packed);
+/* The sizing rule: env_threads > 0 (OVL_POOL_THREADS) wins, else min(12, cpus / sharers - 1), at least 1. */
+int32_t ovl_host_pool_rule(int32_t cpus, int32_t sharers, int32_t env_threads);
+
 /* Per-call timing of host-array scoring calls (off by default; on adds HIP timing events):
  * kernel_ms = summed kernel time of the busiest device, call_ms = wall time of the call. */
 int ovl_set_timing(ovl_ctx* ctx, int32_t on);
 int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
+/* The scoring launches of the last host-array call made with timing on, in issue order: *out_n = count;
+ * entry i < cap gives the device ordinal, the result sink (0 HBM, then copied by the copy engine; 1 int32
+ * stored into host memory; 2 packed 2 B/pair into host staging, expanded by host threads), the pairs and
+ * the launch's duration in ms (HIP events on its stream).  Any output pointer may be NULL. */
+int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs, double* ms,
+                      int32_t* out_n);
 /* Link traffic of the last host-array scoring call (always recorded): link_bytes = pair-list bytes the
  * devices read from host memory + result bytes they stored there (2 per pair in packed chunks, 8 per pair
- * otherwise; the few packed pairs whose score travels separately add 4 each and are not counted; a
- * progressive call adds 8 per published tile flag); packed_pairs = pairs whose results crossed packed and
+ * otherwise; the few packed pairs whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose results crossed packed and
  * were expanded on the host. */
 int ovl_last_transfer(const ovl_ctx* ctx, int64_t* link_bytes, int64_t* packed_pairs);
 

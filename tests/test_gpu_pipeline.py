@@ -556,67 +556,60 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
     np.testing.assert_array_equal(le[idx], re_)
 
 
-# ----------------------------------------------------------------------------- progressive transport
+# ----------------------------------------------------------------------------- the step's transport
 @pytest.mark.parametrize("cfg", ["target", "cfg3"])
-def test_progressive_transport_vs_oracle(oracle_mod, cfg):
-    """Whole resident list into pinned arrays (the bench step): the progressive transport (one launch; light tiles
-    publish a packed line + flag that the host expands while the kernel runs, heavy tiles store int32) equals
-    the oracle and the chunked packed pipeline (OVL_PROGRESSIVE=0), call after call (flag epochs), into fresh
-    and reused arrays; ovl_last_transfer counts 2 B per light pair and 8 B per heavy pair plus the flags."""
+def test_step_transport_vs_oracle(oracle_mod, cfg):
+    """Whole resident list into pinned arrays (the bench step: packed chunks expanded on the host plus a direct
+    int32 chunk) equals the oracle call after call, into reused and fresh arrays; ovl_last_transfer counts
+    2 B per packed pair and 8 B per direct pair."""
     from ovlgraph.candidates import dedup_reads
     from ovlgraph.hostmem import pinned_empty
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
-    prog = _engine_env({"OVL_PROGRESSIVE": "1"})
-    chunked = _engine_env({"OVL_PROGRESSIVE": "0"})
+    eng = _engine_env({})
     try:
-        for e in (prog, chunked):
-            e.set_reads(reads)
-        a, b = prog.candidates(5)
-        chunked.candidates(5)
+        eng.set_reads(reads)
+        a, b = eng.candidates(5)
         ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
         n = a.shape[0]
         out = (pinned_empty(n), pinned_empty(n))
         for it in range(6):
             out[0][:] = -7
             out[1][:] = -7
-            prog.score_candidates(out=out)
+            eng.score_candidates(out=out)
             np.testing.assert_array_equal(out[0], ref_s, err_msg=f"call {it}")
             np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
-        x = prog.last_transfer()
-        lens = np.array([len(r) for r in reads])
-        side = lens[a] != lens.max()
-        tiles = (n + 63) // 64
-        heavy = np.zeros(tiles, bool)
-        np.logical_or.at(heavy, np.arange(n) // 64, side)
-        heavy_pairs = int(sum(min(64, n - 64 * t) for t in np.flatnonzero(heavy)))
-        assert x["packed_pairs"] == n - heavy_pairs, x
-        assert x["link_bytes"] == 2 * (n - heavy_pairs) + 8 * heavy_pairs + 8 * int((~heavy).sum()), x
-        cs, ce = chunked.score_candidates()
-        np.testing.assert_array_equal(cs, ref_s)
-        np.testing.assert_array_equal(ce, ref_e)
-        fresh = prog.score_candidates()
+            x = eng.last_transfer()
+            assert 0 < x["packed_pairs"] < n, x
+            assert x["link_bytes"] == 2 * x["packed_pairs"] + 8 * (n - x["packed_pairs"]), x
+        fresh = eng.score_candidates()
         np.testing.assert_array_equal(fresh[0], ref_s)
         np.testing.assert_array_equal(fresh[1], ref_e)
     finally:
-        prog.close()
-        chunked.close()
+        eng.close()
 
 
-def test_progressive_transport_without_heavy_tiles(oracle_mod):
-    """A list with no side pairs (every read of one length: no heavy tiles, no heavy-first ids) and one whose
-    list changes between calls (the tile flags and heavy map follow the new list)."""
-    from ovlgraph.candidates import dedup_reads
+def test_heavy_tiles_follow_the_list(oracle_mod):
+    """Heavy tiles (tiles holding a side pair, scheduled first) are rebuilt for every new list, also when the
+    new list has the same length: two read sets with the same count and different length mixes at k = 0
+    (n (n - 1) pairs each), then a set with no side pairs at all."""
     from ovlgraph.hostmem import pinned_empty
-    from ovlgraph.reads import config_reads
-    reads, _ = dedup_reads(config_reads("target", seed=3))
-    lw = max(len(r) for r in reads)
-    uniform = [r for r in reads if len(r) == lw]
-    eng = _engine_env({"OVL_PROGRESSIVE": "1"})
+    rng = np.random.default_rng(5)
+    n_reads, lw = 700, 100
+
+    def reads_with(short_at):
+        rs = ["".join(rng.choice(list("ACGT"), lw)) for _ in range(n_reads)]
+        for i in short_at:
+            rs[i] = rs[i][: int(rng.integers(10, lw))]
+        return rs
+
+    sets = [reads_with([3, 50, 51, 400]), reads_with([10, 600, 699]), reads_with([])]
+    eng = _engine_env({})
     try:
-        for rs in (uniform, reads, uniform):
+        for rs in sets:
             eng.set_reads(rs)
-            a, b = eng.candidates(5)
+            a, b = eng.candidates(0)
+            assert a.shape[0] == n_reads * (n_reads - 1)
             ref_s, ref_e = oracle_mod.batch_closed_form(rs, a, b)
             out = (pinned_empty(a.shape[0]), pinned_empty(a.shape[0]))
             for _ in range(2):

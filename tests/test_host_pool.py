@@ -1,0 +1,56 @@
+"""Host pool sizing for multi-process callers (no GPU): the rule, and the sharer count when several processes
+drive libovl on one CPU set -- the reference's joblib workers (experiments.py:481-539, n_jobs=-1)."""
+import multiprocessing as mp
+import os
+
+from ovlgraph import _lib
+from ovlgraph.engine import host_pool
+
+
+def test_rule():
+    rule = _lib.load().ovl_host_pool_rule
+    assert rule(16, 1, 0) == 12           # the box's 16-CPU share, one process: 12 threads
+    assert rule(256, 1, 0) == 12
+    assert rule(16, 4, 0) == 3            # four joblib workers on 16 CPUs: 16 / 4 - 1
+    assert rule(128, 8, 0) == 12          # eight ranks on a 128-CPU node quota
+    assert rule(16, 8, 0) == 1            # never below one thread
+    assert rule(8, 1, 0) == 7
+    assert rule(16, 4, 5) == 5            # OVL_POOL_THREADS wins
+    assert rule(1, 1, 0) == 1
+
+
+def _worker(barrier, q):
+    # a fresh interpreter (spawn) per worker, like loky's workers
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "genome-assembly-using-overlap-graphs_amd"))
+    from ovlgraph.engine import host_pool as hp
+    hp()                      # joins the CPU set's registry
+    barrier.wait()            # every worker has joined
+    got = hp()
+    barrier.wait()            # nobody leaves before everyone has counted
+    q.put(got)
+
+
+def test_four_processes_share_the_cpus():
+    alone = host_pool()
+    assert alone["sharers"] >= 1 and alone["cpus"] >= 1
+    ctx = mp.get_context("spawn")
+    barrier = ctx.Barrier(4)
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(barrier, q)) for _ in range(4)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in res:
+        # this test process holds a slot too (host_pool above), so at least the four workers + 1
+        assert r["sharers"] >= 5, res
+        assert r["threads"] <= max(1, r["cpus"] // 4), res
+        assert r["threads"] == max(1, min(12, r["cpus"] // r["sharers"] - 1)), res
+        if r["threads"] < 6:
+            assert r["packed"] == 0
+    # the workers' slots are gone with them: the count drops back
+    assert host_pool()["sharers"] <= alone["sharers"] + 0

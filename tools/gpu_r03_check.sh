@@ -1,0 +1,26 @@
+#!/bin/bash
+# round 3: GPU tests, smoke, the default bench (N = 1), the processes left after it, the N = 2 launcher
+# rehearsal on the one GPU (bench.py --gpus 2 spawns its ranks; gloo, both on GPU 0) and the cfg4 N = 1 point
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/${1:-r03}
+mkdir -p $OUT
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > $OUT/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -60 $OUT/gpu_tests.log; exit 1; }
+tail -3 $OUT/gpu_tests.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+  || { echo "smoke failed"; tail -30 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+ps -u "$(id -u)" -o pid,ppid,stat,etime,cmd > $OUT/ps_before.txt
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err \
+  || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
+echo "bench ok"
+sleep 2
+ps -u "$(id -u)" -o pid,ppid,stat,etime,cmd > $OUT/ps_after.txt
+ls /dev/shm > $OUT/shm_after.txt 2>&1
+timeout -k 10 400 python -u bench.py --gpus 2 --config cfg4 --steps 10 --warmup 2 \
+  > $OUT/n2_cfg4.json 2> $OUT/n2_cfg4.err || { echo "n2 failed"; tail -30 $OUT/n2_cfg4.err; exit 1; }
+echo "n2 ok"
+timeout -k 10 400 python -u bench.py --gpus 1 --config cfg4 --steps 10 --warmup 2 --no-extra --no-cpu-baseline \
+  > $OUT/n1_cfg4.json 2> $OUT/n1_cfg4.err || { echo "n1 cfg4 failed"; tail -30 $OUT/n1_cfg4.err; exit 1; }
+echo "n1 cfg4 ok"

@@ -14,12 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
 import numpy as np  # noqa: E402
 
-KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN", "OVL_PROGRESSIVE",
-         "OVL_PG_STORE")
+KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
 SETTINGS = (("int32", {"OVL_PACK": "0"}),
-            ("packed_adaptive", {"OVL_PROGRESSIVE": "0"}),
-            ("packed_pct18", {"OVL_PACK_DIRECT_PCT": "18", "OVL_PROGRESSIVE": "0"}),
-            ("progressive", {"OVL_PROGRESSIVE": "1"}))
+            ("packed_adaptive", {}),
+            ("packed_pct18", {"OVL_PACK_DIRECT_PCT": "18"}))
 
 
 def main():
