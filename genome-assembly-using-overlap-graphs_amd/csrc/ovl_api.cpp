@@ -27,6 +27,7 @@
 #include <new>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -91,6 +92,9 @@ struct Knobs {
     int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
+    int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
+                                  // instead of the compact encoding (encode_chunk; A/B knob)
+    int64_t compact_min = 1 << 16;  // OVL_PAIRS_COMPACT_MIN: compact encoding from this many pairs per call
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -170,10 +174,26 @@ struct Dev {
     int32_t out_mode = 0;            // result sink of the next ungapped launches (OvlUngappedArgs::host_out):
                                      // 0 HBM, 1 host-mapped int32 arrays, 2 host-mapped packed uint16
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
+    // compact host pair lists (encode_chunk): pinned encoding buffer (8 bytes per pair + slack), its device
+    // address, a decode event per chunk, and the encoded bytes of the last call
+    char* cp_host = nullptr;
+    char* cp_dev = nullptr;
+    size_t cp_bytes = 0;
+    std::vector<hipEvent_t> dec_ev;
+    int64_t cp_link = 0;
+};
+
+// The host side of a read-set upload in one pinned block (grown on demand, kept by the context): offsets,
+// lengths, the length bitmap, the code table and the bytes (stage_reads).
+struct ReadStage {
+    char* p = nullptr;
+    size_t bytes = 0;
+    size_t o_off = 0, o_len = 0, o_full = 0, o_lut = 0, o_raw = 0;
 };
 
 struct ovl_ctx {
     std::vector<Dev*> devs;
+    ReadStage stage;             // pinned upload stage of ovl_set_reads
     std::string err;
     std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
     int32_t timing = 0;          // ovl_set_timing
@@ -617,6 +637,8 @@ Knobs read_knobs() {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
         k.pack_adapt = 0;  // a fixed share
     }
+    if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PAIRS_COMPACT_MIN")) k.compact_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -750,38 +772,49 @@ class CopyPool {
         if (!pool_ || pool_->pid_ != getpid()) pool_ = new CopyPool();  // a forked child starts a fresh pool
         return *pool_;
     }
-    // f(lo, hi) over [0, n) cut into parts of >= min_part items (multiples of 64), on the workers and the
-    // calling thread
-    void parallel(size_t n, size_t min_part, const std::function<void(size_t, size_t)>& f) {
+    // [0, n) cut into parts of >= min_part items (multiples of 64), one per thread a call may use:
+    // part i is [b[i], b[i + 1])
+    std::vector<size_t> cut(size_t n, size_t min_part) const {
         const size_t use = (size_t)std::min<int>(threads(), (int)workers_.size() + 1);
+        const size_t parts = std::max<size_t>(1, std::min<size_t>(use, n / std::max<size_t>(min_part, 1)));
+        std::vector<size_t> b(1, 0);
+        if (parts > 1) {
+            const size_t step = (n / parts + 63) & ~size_t(63);
+            for (size_t i = 1; i < parts && i * step < n; ++i) b.push_back(i * step);
+        }
+        b.push_back(n);
+        return b;
+    }
+    // f(i, lo, hi) for every part i of `b` (from cut), on the workers and the calling thread (part 0)
+    void parallel_parts(const std::vector<size_t>& b, const std::function<void(size_t, size_t, size_t)>& f) {
         spin_us_.store(CpuShare::get().sharers() > 1 ? 0 : spin_cfg_, std::memory_order_relaxed);
-        const size_t parts = std::min<size_t>(use, n / std::max<size_t>(min_part, 1));
+        const size_t parts = b.size() - 1;
         if (parts <= 1) {
-            f(0, n);
+            f(0, b[0], b[parts]);
             return;
         }
-        const size_t step = (n / parts + 63) & ~size_t(63);
         std::lock_guard<std::mutex> one_call(call_mu_);  // calls from several host threads take turns
         {
             std::lock_guard<std::mutex> lk(mu_);
-            size_t k = 0;
             for (size_t i = 1; i < parts; ++i) {
-                const size_t lo = i * step, hi = std::min(n, lo + step);
-                if (lo >= hi) break;
-                tasks_.push_back([&f, lo, hi] { f(lo, hi); });
-                ++k;
+                const size_t lo = b[i], hi = b[i + 1];
+                tasks_.push_back([&f, i, lo, hi] { f(i, lo, hi); });
             }
-            pending_.store(k, std::memory_order_release);
+            pending_.store(parts - 1, std::memory_order_release);
             queued_.store(tasks_.size(), std::memory_order_release);
         }
         cv_.notify_all();
-        f(0, std::min(step, n));
+        f(0, b[0], b[1]);
         // the batch's end: polled for a while (the workers finish within microseconds of the caller), then
         // a blocking wait
         if (!spin_until([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
             std::unique_lock<std::mutex> lk(mu_);
             done_.wait(lk, [&] { return pending_.load(std::memory_order_acquire) == 0; });
         }
+    }
+    // f(lo, hi) over [0, n) cut into parts of >= min_part items (multiples of 64)
+    void parallel(size_t n, size_t min_part, const std::function<void(size_t, size_t)>& f) {
+        parallel_parts(cut(n, min_part), [&f](size_t, size_t lo, size_t hi) { f(lo, hi); });
     }
     // dst[i] = src[i] for [0, bytes)
     void copy(void* dst, const void* src, size_t bytes) {
@@ -903,6 +936,9 @@ void destroy_dev(Dev* d) {
     free_staging(d->st_in);
     free_staging(d->st_out);
     if (d->h_flag) (void)hipHostFree(d->h_flag);
+    if (d->cp_host) (void)hipHostFree(d->cp_host);
+    for (hipEvent_t e : d->dec_ev)
+        if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < kSlots; ++i)
         for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i]})
             if (e) (void)hipEventDestroy(e);
@@ -1039,6 +1075,8 @@ struct Call {
     bool pack = false;             // direct: results cross the link packed (2 bytes per pair) into the staging
                                    // slots and are expanded into the caller's arrays on the host (all chunks for
                                    // pageable arrays; for pinned ones all but a last direct chunk, Job::n_packed)
+    bool compact = false;          // direct, one device: the host pair list is encoded per chunk (encode_chunk)
+                                   // and decoded into HBM by kernels reading it through the host mapping
     bool timing = false;
 };
 
@@ -1070,7 +1108,7 @@ int setup_job(const Call& C, Job& J) {
     J.nchunks = J.n_packed = 0;
     if (n <= 0) return OVL_OK;
     HIPCHK(d, hipSetDevice(d->device));
-    const bool need_in = C.h_a && !C.in_pinned, need_out = !C.out_pinned || C.pack;
+    const bool need_in = C.h_a && !C.in_pinned && !C.compact, need_out = !C.out_pinned || C.pack;
     J.chunk = pick_chunk(d, n, need_in || need_out, C.direct, C.pack);
     // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
@@ -1092,13 +1130,36 @@ int setup_job(const Call& C, Job& J) {
     J.nchunks = (int64_t)J.cb.size() - 1;
     for (int64_t k = 0; k < J.nchunks; ++k) J.chunk = std::max(J.chunk, J.cb[(size_t)k + 1] - J.cb[(size_t)k]);
     const size_t bytes = sizeof(int32_t) * (size_t)n;
+    if (C.compact) {
+        // decoded pair list in HBM, the pinned encoding buffer (chunk k at align16(8 * cb[k] + 32 * k)) and
+        // the chunks' decode events
+        HIPCHK(d, ensure(d->a, bytes));
+        HIPCHK(d, ensure(d->b, bytes));
+        J.ka = as<int32_t>(d->a);
+        J.kb = as<int32_t>(d->b);
+        const size_t need = 8 * (size_t)n + 32 * (size_t)J.nchunks + 64;
+        if (d->cp_bytes < need) {
+            if (d->cp_host) (void)hipHostFree(d->cp_host);
+            d->cp_host = d->cp_dev = nullptr;
+            d->cp_bytes = 0;
+            HIPCHK(d, hipHostMalloc((void**)&d->cp_host, need, kHostShared));
+            HIPCHK(d, hipHostGetDevicePointer((void**)&d->cp_dev, d->cp_host, 0));
+            d->cp_bytes = need;
+        }
+        while ((int64_t)d->dec_ev.size() < J.nchunks) {
+            hipEvent_t ev;
+            HIPCHK(d, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            d->dec_ev.push_back(ev);
+        }
+        d->cp_link = 0;
+    }
     if (C.h_a && !C.direct) {
         HIPCHK(d, ensure(d->a, bytes));
         HIPCHK(d, ensure(d->b, bytes));
         J.ka = as<int32_t>(d->a);
         J.kb = as<int32_t>(d->b);
     }
-    if (C.h_a && C.direct && C.in_pinned) {
+    if (C.h_a && C.direct && C.in_pinned && !C.compact) {
         // the kernels read this device's slice of the caller's pinned pair arrays in place
         void* pa = nullptr;
         void* pb = nullptr;
@@ -1139,6 +1200,100 @@ int setup_job(const Call& C, Job& J) {
     return OVL_OK;
 }
 
+// Compact host pair list, chunk k (C.compact): the host pool encodes the caller's int32 pairs into the pinned
+// encoding buffer and kernels on the device's second stream decode them into HBM (ovl_pairs.hip), reading the
+// encoding through the host mapping; the chunk's scoring launch waits for dec_ev[k].  Encoding of chunk k:
+//   b: uint16 when n_reads <= 65,535 (an index outside [0, n_reads) becomes 0xFFFF, decoded to -1, which the
+//      scoring kernels report as OVL_E_INDEX like any bad index), else the int32 values;
+//   a: runs (value, chunk-relative start; starts[R] = n) when 8 R + 4 < n * width -- the candidate lists of
+//      overlapGraphs.py:43-52 are a-major, ~55 pairs per run at the target point --, else like b.
+// At the target point 4.3 MB cross the link instead of 16 MB.
+int encode_chunk(const Call& C, Job& J, int64_t k) {
+    Dev* d = J.d;
+    const int64_t off = J.cb[(size_t)k];
+    const int64_t n = J.cb[(size_t)k + 1] - off;
+    const int64_t g = J.lo + off;
+    const int32_t* A = C.h_a + g;
+    const int32_t* B = C.h_b + g;
+    const int32_t nr = d->n_reads;
+    const int wd = nr <= 65535 ? 2 : 4;
+    const size_t base = (8 * (size_t)off + 32 * (size_t)k + 15) & ~size_t(15);
+    char* hb = d->cp_host + base;                  // b area
+    const size_t b_bytes = ((size_t)n * wd + 15) & ~size_t(15);
+    char* ha = hb + b_bytes;                       // a area: runs, or a like b
+    CopyPool& pool = CopyPool::get();
+    const std::vector<size_t> parts = pool.cut((size_t)n, size_t(1) << 15);
+    std::vector<int64_t> starts_in(parts.size(), 0);
+    // pass 1: b, and the run starts of a in each part (a[i] != a[i - 1], and i == 0)
+    pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
+        if (wd == 2) {
+            uint16_t* o = reinterpret_cast<uint16_t*>(hb);
+            for (size_t p = lo; p < hi; ++p) {
+                const int32_t v = B[p];
+                o[p] = (v >= 0 && v < nr) ? (uint16_t)v : (uint16_t)0xFFFF;
+            }
+        } else {
+            memcpy(reinterpret_cast<int32_t*>(hb) + lo, B + lo, sizeof(int32_t) * (hi - lo));
+        }
+        int64_t c = 0;
+        int32_t prev = lo ? A[lo - 1] : (int32_t)~A[0];
+        for (size_t p = lo; p < hi; ++p) {
+            const int32_t v = A[p];
+            c += v != prev;
+            prev = v;
+        }
+        starts_in[i] = c;
+    });
+    int64_t R = 0;
+    std::vector<int64_t> first(parts.size(), 0);
+    for (size_t i = 0; i + 1 < parts.size(); ++i) {
+        first[i] = R;
+        R += starts_in[i];
+    }
+    const bool runs = 8 * R + 4 < n * wd && n < (int64_t(1) << 31);
+    int32_t* vals = reinterpret_cast<int32_t*>(ha);
+    int32_t* starts = vals + ((R + 3) & ~int64_t(3));  // 16-byte aligned
+    // pass 2: the runs, or a like b
+    pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
+        if (runs) {
+            int64_t r = first[i];
+            int32_t prev = lo ? A[lo - 1] : (int32_t)~A[0];
+            for (size_t p = lo; p < hi; ++p) {
+                const int32_t v = A[p];
+                if (v != prev) {
+                    vals[r] = v;
+                    starts[r] = (int32_t)p;
+                    ++r;
+                }
+                prev = v;
+            }
+        } else if (wd == 2) {
+            uint16_t* o = reinterpret_cast<uint16_t*>(ha);
+            for (size_t p = lo; p < hi; ++p) {
+                const int32_t v = A[p];
+                o[p] = (v >= 0 && v < nr) ? (uint16_t)v : (uint16_t)0xFFFF;
+            }
+        } else {
+            memcpy(reinterpret_cast<int32_t*>(ha) + lo, A + lo, sizeof(int32_t) * (hi - lo));
+        }
+    });
+    if (runs) starts[R] = (int32_t)n;
+    // decode on the second stream (host-mapped reads) into this chunk's slice of the HBM list
+    char* db = d->cp_dev + base;
+    char* da = db + b_bytes;
+    HIPCHK(d, hipSetDevice(d->device));
+    HIPCHK(d, ovl_launch_widen(db, wd, n, J.kb + off, d->s_in));
+    if (runs) {
+        HIPCHK(d, ovl_launch_runs(reinterpret_cast<int32_t*>(da), reinterpret_cast<int32_t*>(da) + ((R + 3) & ~int64_t(3)),
+                                  R, J.ka + off, d->s_in));
+    } else {
+        HIPCHK(d, ovl_launch_widen(da, wd, n, J.ka + off, d->s_in));
+    }
+    HIPCHK(d, hipEventRecord(d->dec_ev[(size_t)k], d->s_in));
+    d->cp_link += (int64_t)n * wd + (runs ? 8 * R + 4 : (int64_t)n * wd);
+    return OVL_OK;
+}
+
 // Direct mode: the kernels read the pair list and store the results through host mappings (no copy-engine
 // transfers); pageable arrays are copied into / out of the pinned staging slots on the host.
 int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
@@ -1151,12 +1306,17 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     const size_t nb = sizeof(int32_t) * (size_t)n;
     const int slot = (int)(k % kSlots);
     const size_t so = (size_t)slot * 2 * (size_t)d->st_cap;
-    const bool staged_in = C.h_a && !C.in_pinned;
+    const bool staged_in = C.h_a && !C.in_pinned && !C.compact;
     // the slot's previous user, chunk k - kSlots, must be done (its staged results were drained already)
     if (staged_in && k >= kSlots && !chunk_staged(C, J, k - kSlots)) HIPCHK(d, wait_event(d, d->ev_k[slot]));
     const int32_t* ka;
     const int32_t* kb;
-    if (C.h_a) {
+    if (C.compact) {
+        // decoded into HBM by encode_chunk's kernels on the second stream
+        HIPCHK(d, hipStreamWaitEvent(d->stream, d->dec_ev[(size_t)k], 0));
+        ka = J.ka + off;
+        kb = J.kb + off;
+    } else if (C.h_a) {
         if (staged_in) {
             host_copy(d->st_in + so, C.h_a + g, nb);
             host_copy(d->st_in + so + d->st_cap, C.h_b + g, nb);
@@ -1334,11 +1494,16 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     trace.mark('s', 0);
     int64_t maxch = 0;
     for (const Job& J : jobs) maxch = std::max(maxch, J.nchunks);
+    if (C.compact)
+        for (Job& J : jobs)
+            if (J.nchunks > 0 && (rc = encode_chunk(C, J, 0)) != OVL_OK) return rc;
     for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
             if ((rc = issue_chunk(C, J, k)) != OVL_OK) break;
             trace.mark('i', k);
+            // the next chunk's encoding (host) while this one decodes and scores
+            if (C.compact && k + 1 < J.nchunks && (rc = encode_chunk(C, J, k + 1)) != OVL_OK) break;
             const int64_t j = k - (kSlots - 1);
             if (j >= 0 && chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
         }
@@ -1404,7 +1569,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         if (n <= 0) continue;
         const int64_t np = J.n_packed ? J.cb[(size_t)J.n_packed] : 0;
         packed += np;
-        link += (C.h_a ? 8 * n : 0) + 2 * np + 8 * (n - np);
+        link += (C.compact ? J.d->cp_link : (C.h_a ? 8 * n : 0)) + 2 * np + 8 * (n - np);
     }
     c->x_link_bytes = link;
     c->x_packed_pairs = packed;
@@ -1537,6 +1702,7 @@ OVL_API int ovl_destroy(ovl_ctx* c) {
     if (!c) return OVL_OK;
     DeviceGuard guard;
     for (Dev* d : c->devs) destroy_dev(d);
+    if (c->stage.p) (void)hipHostFree(c->stage.p);
     delete c;
     return OVL_OK;
 }
@@ -1634,7 +1800,7 @@ struct HostReads {
     std::vector<int32_t> len;
     std::vector<uint32_t> full;
     uint8_t lut[256];
-    const uint8_t* src = nullptr;
+    const uint8_t* src = nullptr;  // the caller's bytes, then (stage_reads) their pinned copy
     int64_t total = 0;
     int32_t n_reads = 0, lmax = 0, planes = 2, wmax = 0, srow = 0, trow = 0;
 };
@@ -1658,10 +1824,29 @@ int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t 
     for (int32_t r = 0; r < n_reads; ++r)
         if (h.len[(size_t)r] == h.lmax) h.full[(size_t)r >> 5] |= 1u << (r & 31);
     if (h.total > 0 && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
-    // alphabet: dense codes in byte order (equality-preserving)
+    // alphabet: dense codes in byte order (equality-preserving); the bytes seen, split over the host pool
     bool present[256] = {false};
     h.src = seqs ? seqs + base : nullptr;
-    for (int64_t i = 0; i < h.total; ++i) present[h.src[i]] = true;
+    if (h.total > 0) {
+        CopyPool& pool = CopyPool::get();
+        const std::vector<size_t> parts = pool.cut((size_t)h.total, size_t(1) << 18);
+        std::vector<std::array<uint8_t, 256>> seen(parts.size());
+        const uint8_t* src = h.src;
+        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
+            uint8_t t[4][256] = {};  // four tables: independent stores
+            size_t q = lo;
+            for (; q + 4 <= hi; q += 4) {
+                t[0][src[q]] = 1;
+                t[1][src[q + 1]] = 1;
+                t[2][src[q + 2]] = 1;
+                t[3][src[q + 3]] = 1;
+            }
+            for (; q < hi; ++q) t[0][src[q]] = 1;
+            for (int v = 0; v < 256; ++v) seen[i][(size_t)v] = t[0][v] | t[1][v] | t[2][v] | t[3][v];
+        });
+        for (const auto& t : seen)
+            for (int v = 0; v < 256; ++v) present[v] = present[v] || t[(size_t)v];
+    }
     memset(h.lut, 0, sizeof(h.lut));
     int k = 0;
     for (int v = 0; v < 256; ++v)
@@ -1675,8 +1860,34 @@ int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t 
     return OVL_OK;
 }
 
-// Asynchronous upload + pack of one device's copy; the caller synchronises d->stream.
-hipError_t upload_reads(Dev* d, const HostReads& h) {
+// Fill the pinned upload stage (the bytes copied in by the host pool), so the uploads are DMA from pinned
+// memory instead of the runtime's staging of pageable memory.
+int stage_reads(ovl_ctx* c, ReadStage& st, HostReads& h) {
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    st.o_off = 0;
+    st.o_len = al(st.o_off + sizeof(int64_t) * h.off.size());
+    st.o_full = al(st.o_len + sizeof(int32_t) * h.len.size());
+    st.o_lut = al(st.o_full + sizeof(uint32_t) * h.full.size());
+    st.o_raw = al(st.o_lut + 256);
+    const size_t need = al(st.o_raw + (size_t)h.total + 1);
+    if (st.bytes < need) {
+        if (st.p) (void)hipHostFree(st.p);
+        st.p = nullptr;
+        st.bytes = 0;
+        HIPCHK(c, hipHostMalloc((void**)&st.p, need, hipHostMallocPortable));
+        st.bytes = need;
+    }
+    memcpy(st.p + st.o_off, h.off.data(), sizeof(int64_t) * h.off.size());
+    memcpy(st.p + st.o_len, h.len.data(), sizeof(int32_t) * h.len.size());
+    memcpy(st.p + st.o_full, h.full.data(), sizeof(uint32_t) * h.full.size());
+    memcpy(st.p + st.o_lut, h.lut, 256);
+    if (h.total > 0) host_copy(st.p + st.o_raw, h.src, (size_t)h.total);
+    h.src = reinterpret_cast<const uint8_t*>(st.p + st.o_raw);
+    return OVL_OK;
+}
+
+// Asynchronous upload + pack of one device's copy from the pinned stage; the caller synchronises d->stream.
+hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
     hipError_t e = hipSetDevice(d->device);
     if (e != hipSuccess) return e;
     d->n_reads = -1;  // invalid until fully built
@@ -1690,12 +1901,12 @@ hipError_t upload_reads(Dev* d, const HostReads& h) {
     if ((e = ensure(d->raw, (size_t)h.total)) != hipSuccess) return e;
     if ((e = ensure(d->full, sizeof(uint32_t) * h.full.size())) != hipSuccess) return e;
     hipStream_t s = d->stream;
-    if ((e = hipMemcpyAsync(d->off.p, h.off.data(), sizeof(int64_t) * h.off.size(), hipMemcpyHostToDevice, s)))
+    if ((e = hipMemcpyAsync(d->off.p, st.p + st.o_off, sizeof(int64_t) * h.off.size(), hipMemcpyHostToDevice, s)))
         return e;
-    if ((e = hipMemcpyAsync(d->len.p, h.len.data(), sizeof(int32_t) * h.len.size(), hipMemcpyHostToDevice, s)))
+    if ((e = hipMemcpyAsync(d->len.p, st.p + st.o_len, sizeof(int32_t) * h.len.size(), hipMemcpyHostToDevice, s)))
         return e;
-    if ((e = hipMemcpyAsync(d->lut.p, h.lut, 256, hipMemcpyHostToDevice, s))) return e;
-    if ((e = hipMemcpyAsync(d->full.p, h.full.data(), sizeof(uint32_t) * h.full.size(), hipMemcpyHostToDevice, s)))
+    if ((e = hipMemcpyAsync(d->lut.p, st.p + st.o_lut, 256, hipMemcpyHostToDevice, s))) return e;
+    if ((e = hipMemcpyAsync(d->full.p, st.p + st.o_full, sizeof(uint32_t) * h.full.size(), hipMemcpyHostToDevice, s)))
         return e;
     if (h.total > 0) {
         if ((e = hipMemcpyAsync(d->raw.p, h.src, (size_t)h.total, hipMemcpyHostToDevice, s))) return e;
@@ -1733,14 +1944,16 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
         d->cand_n = -1;
         d->heavy_for = -1;
     }
-    // upload to every device, then wait for all (the uploads and packs overlap across devices)
+    // the pinned stage (the previous upload from it is complete: ovl_set_reads synchronises), then the upload
+    // to every device, then wait for all (the uploads and packs overlap across devices)
+    rc = stage_reads(c, c->stage, h);
+    if (rc != OVL_OK) return rc;
     for (Dev* d : c->devs)
-        if ((e = upload_reads(d, h)) != hipSuccess) break;
+        if ((e = upload_reads(d, h, c->stage)) != hipSuccess) break;
     for (Dev* d : c->devs) {
         (void)hipSetDevice(d->device);
         hipError_t e2 = hipStreamSynchronize(d->stream);
         if (e == hipSuccess) e = e2;
-        release(d->raw);
     }
     if (e != hipSuccess)
         return fail(c, e == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP, "ovl_set_reads: %s", hipGetErrorString(e));
@@ -1842,6 +2055,7 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.timing = c->timing != 0;
     C.direct = c->devs[0]->k.pipe_direct != 0;
     C.pack = pack_ok(c, p, n_pairs, C.out_pinned);
+    C.compact = C.direct && c->devs.size() == 1 && c->devs[0]->k.compact && n_pairs >= c->devs[0]->k.compact_min;
     const int32_t S = (int32_t)c->devs.size();
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);

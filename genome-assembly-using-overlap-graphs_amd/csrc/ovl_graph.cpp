@@ -153,6 +153,8 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<int32_t> seen_list;
     std::vector<Event> log;
     std::vector<int32_t> tail_of;          // path edge -> its tail (the node whose iterator yielded it)
+    std::vector<int64_t> path_w;           // path edge -> its weight (the cycle's minimum scans this, contiguous)
+    std::vector<int64_t> tail_pos(n_nodes, 0);  // node -> index of the path edge leaving it (valid while active)
     int64_t nrem = 0;
 
     // reverse CSR: rtail[k] / ralive[k] for the k-th edge into its head; rpos[e] = k (a removal clears both)
@@ -184,6 +186,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
         path.clear();
         ckpt.clear();
         tail_of.clear();
+        path_w.clear();
         seen_list.clear();
         stack.assign(1, s);
         int32_t root = s;  // find_cycle's path root (the start node; a reset re-roots at the tail)
@@ -257,20 +260,28 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                     path.pop_back();
                     ckpt.pop_back();
                     tail_of.pop_back();
+                    path_w.pop_back();
                     active[head[pe]] = 0;
                     if (!path.empty() && head[path.back()] == cur) break;
                 }
             }
+            tail_pos[cur] = (int64_t)path.size();
             path.push_back(q);
             ckpt.push_back(mark);
             tail_of.push_back(cur);
+            path_w.push_back(weight[q]);
             if (active[h]) {
-                // cycle: the path suffix from the first edge leaving h; remove its weakest edge
-                size_t i0 = 0;
-                while (i0 < path.size() && tail_of[i0] != h) ++i0;
+                // cycle: the path suffix from the first edge leaving h (the path is simple, so that edge is
+                // tail_pos[h]); remove its weakest edge, the first minimum in cycle order
+                const size_t i0 = (size_t)tail_pos[h];
                 size_t kmin = i0;
+                int64_t wmin = path_w[i0];
+                const int64_t* pw = path_w.data();
                 for (size_t k = i0 + 1; k < path.size(); ++k)
-                    if (weight[path[k]] < weight[path[kmin]]) kmin = k;
+                    if (pw[k] < wmin) {
+                        wmin = pw[k];
+                        kmin = k;
+                    }
                 const int64_t dead = path[kmin];
                 const int32_t tail_of_dead = tail_of[kmin];
                 removed[nrem++] = dead;
@@ -297,6 +308,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 path.resize(kmin);
                 ckpt.resize(kmin);
                 tail_of.resize(kmin);
+                path_w.resize(kmin);
                 // the edge_dfs stack at that moment: the root (= the start node: only it can be on the
                 // stack without being a path head) and the surviving path heads
                 stack.resize(kmin + 1);

@@ -82,6 +82,11 @@ extern "C" hipError_t ovl_launch_tile_flags(const int32_t* a_idx, int64_t n_pair
                                             int32_t n_reads, uint8_t* flags, hipStream_t stream);
 
 extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);
+// compact host pair lists (ovl_pairs.hip): dst[i] = src[i] from 2- or 4-byte elements (uint16 0xFFFF -> -1; src and
+// dst 16-byte aligned), and runs: dst[starts[r] .. starts[r + 1]) = vals[r]
+extern "C" hipError_t ovl_launch_widen(const void* src, int32_t width, int64_t n, int32_t* dst, hipStream_t stream);
+extern "C" hipError_t ovl_launch_runs(const int32_t* vals, const int32_t* starts, int64_t n_runs, int32_t* dst,
+                                      hipStream_t stream);
 extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out);
 // lane-per-pair full DP (ovl_dp_lane.hip): colbuf holds slots x ovl_dp_lane_rcap(mcap) x 64 dwords
 struct OvlLaneArgs {

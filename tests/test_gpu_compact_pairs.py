@@ -1,0 +1,143 @@
+"""GPU: host pair lists in compact form (ovl_pairs.hip, ovl_api.cpp encode_chunk).
+
+ovl_score_host / ovl_score_pairs encode the caller's int32 pairs per pipeline chunk -- b as uint16 when
+n_reads <= 65,535, a as runs when the list is a-major (overlapGraphs.py:43-52) -- and kernels decode them into
+HBM.  Every result is compared with the oracle and with the uncompressed path (OVL_PAIRS_COMPACT=0): a-major
+and shuffled lists (runs / no runs), uint16 and int32 widths, pinned and pageable lists, odd chunk sizes, and
+bad indices (OVL_E_INDEX, -1 results, the rest exact).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine_env(env):
+    from ovlgraph import OverlapEngine
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return OverlapEngine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def target():
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("target", seed=0))
+    a, b = enumerate_candidates(reads, 5)
+    return reads, a, b
+
+
+@pytest.mark.parametrize("order", ["reference", "shuffled"])
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("chunk", [None, "300007"])
+def test_compact_vs_oracle_and_plain(oracle_mod, target, order, pinned, chunk):
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = target
+    if order == "shuffled":
+        perm = np.random.default_rng(1).permutation(a.shape[0])
+        a, b = a[perm], b[perm]
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+    if pinned:
+        pa, pb = pinned_empty(a.shape[0]), pinned_empty(b.shape[0])
+        pa[:], pb[:] = a, b
+        a, b = pa, pb
+    env = {"OVL_PIPE_CHUNK": chunk} if chunk else {}
+    comp = _engine_env(env)
+    plain = _engine_env(dict(env, OVL_PAIRS_COMPACT="0"))
+    try:
+        for e in (comp, plain):
+            e.set_reads(reads)
+        for _ in range(2):
+            s, en = comp.score(a, b)
+            np.testing.assert_array_equal(s, ref_s)
+            np.testing.assert_array_equal(en, ref_e)
+        x = comp.last_transfer()
+        s2, e2 = plain.score(a, b)
+        np.testing.assert_array_equal(s2, ref_s)
+        np.testing.assert_array_equal(e2, ref_e)
+        y = plain.last_transfer()
+        # the compact list moves fewer bytes over the link (b in 16 bits, a-major lists as runs)
+        assert x["link_bytes"] < y["link_bytes"], (x, y)
+    finally:
+        comp.close()
+        plain.close()
+
+
+def test_compact_int32_width_cfg4_sample(oracle_mod):
+    """More than 65,535 reads: b (and a when not in runs) cross as int32; the a-major runs still apply."""
+    from ovlgraph import OverlapEngine
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("cfg4", seed=0))
+    assert len(reads) > 65535
+    with OverlapEngine(0) as eng:
+        eng.set_reads(reads)
+        a, b = eng.candidates(5)
+        a, b = np.array(a[:3_000_000]), np.array(b[:3_000_000])
+        s, e = eng.score(a, b)
+        idx = np.linspace(0, a.shape[0] - 1, 200_000).astype(np.int64)
+        rs, re_ = oracle_mod.batch_closed_form(reads, a[idx], b[idx])
+        np.testing.assert_array_equal(s[idx], rs)
+        np.testing.assert_array_equal(e[idx], re_)
+        cs, ce = eng.score_candidates_range(0, 3_000_000)
+        np.testing.assert_array_equal(s, cs)
+        np.testing.assert_array_equal(e, ce)
+
+
+@pytest.mark.parametrize("bad", [-1, "n", 70000, -(2 ** 31), 2 ** 31 - 1])
+def test_compact_bad_indices(oracle_mod, target, bad):
+    from ovlgraph import OverlapEngine, OvlError
+    reads, a, b = target
+    n = len(reads)
+    v = n if bad == "n" else bad
+    a, b = a.copy(), b.copy()
+    hit_a = np.array([0, 5, 123_457, a.shape[0] - 1])
+    hit_b = np.array([77, 400_001, 1_500_000])
+    a[hit_a] = v
+    b[hit_b] = v
+    bad_mask = np.zeros(a.shape[0], bool)
+    bad_mask[hit_a] = True
+    bad_mask[hit_b] = True
+    ok = ~bad_mask
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a[ok], b[ok])
+    with OverlapEngine(0) as eng:
+        eng.set_reads(reads)
+        out = (np.full(a.shape[0], 7, np.int32), np.full(a.shape[0], 7, np.int32))
+        with pytest.raises(OvlError, match="OVL_E_INDEX"):
+            eng.score(a, b, out=out)
+        np.testing.assert_array_equal(out[0][bad_mask], -1)
+        np.testing.assert_array_equal(out[1][bad_mask], -1)
+        np.testing.assert_array_equal(out[0][ok], ref_s)
+        np.testing.assert_array_equal(out[1][ok], ref_e)
+        # the context recovers: a clean call right after
+        s, e = eng.score(a[ok][:100_000], b[ok][:100_000])
+        np.testing.assert_array_equal(s, ref_s[:100_000])
+
+
+def test_one_shot_abi_call(oracle_mod, target):
+    """ovl_score_pairs (reads + pair list in host memory) through the compact path, twice (stage reuse),
+    then a smaller read set on the same context."""
+    from ovlgraph import OverlapEngine
+    reads, a, b = target
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+    with OverlapEngine(0) as eng:
+        for _ in range(2):
+            s, e = eng.score_pairs(reads, a, b)
+            np.testing.assert_array_equal(s, ref_s)
+            np.testing.assert_array_equal(e, ref_e)
+        small = reads[:3000]
+        keep = (a < 3000) & (b < 3000)
+        s, e = eng.score_pairs(small, a[keep], b[keep])
+        rs, re_ = oracle_mod.batch_closed_form(small, a[keep], b[keep])
+        np.testing.assert_array_equal(s, rs)
+        np.testing.assert_array_equal(e, re_)
