@@ -18,10 +18,20 @@
  * ovl_graph.cpp), the two per-edge passes around the replay:
  *   csr(nodes, adj) -> (off, heads, weights)          the successor lists as CSR, in DFS visiting order
  *   remove_edges(succ, pred, nodes, tails, heads)      the replay's removals, in order, as remove_edge does
+ *
+ * Straight from the scored pair columns (ovlgraph.overlapGraphs.OverlapEdges; the lazy DiGraph), with no edge
+ * arrays in between:
+ *   overlap_csr(counts, a, b, score[, keep]) -> (off, heads, weights)
+ *       the graph's successor lists as CSR: node first[r] + c is copy c of read r (overlapGraphs.py:25-28);
+ *       its row is, for each kept pair p with a[p] == r in list order, the copies of b[p] (:55-60)
+ *   build_overlap(names, counts, a, b, score, end[, keep[, alive[, shared]]]) -> (node, succ, pred)
+ *       the dicts build() makes from the expanded edges, for the edges whose CSR index is alive only (the
+ *       survivors of the cycle removal, in the reference's insertion order)
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <stdint.h>
+#include <string.h>
 
 static int take(PyObject* obj, Py_buffer* view, Py_ssize_t itemsize, const char* what) {
     if (PyObject_GetBuffer(obj, view, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) return -1;
@@ -264,7 +274,307 @@ done:
     return ret;
 }
 
+/* The CSR layout of the overlap graph from the pair columns.  Pairs are grouped by read a (counting sort,
+ * list order kept inside a group); row u = first[r] + c of read r has len rowlen[r] = sum of counts[b[p]] over
+ * the group, the same for every copy c; pair p's edges sit at off[u] + pstart[p] + cb.  Returns 0, or -1 with
+ * an exception set. */
+typedef struct {
+    Py_ssize_t R, P, N;
+    int64_t E;
+    int64_t* first;   /* R + 1 */
+    int64_t* goff;    /* R + 1: group offsets into plist */
+    int64_t* plist;   /* kept pairs grouped by a */
+    int64_t* rowlen;  /* R */
+    int64_t* pstart;  /* P (kept pairs) */
+    int64_t* off;     /* N + 1 */
+} Layout;
+
+static void layout_free(Layout* L) {
+    PyMem_Free(L->first);
+    PyMem_Free(L->goff);
+    PyMem_Free(L->plist);
+    PyMem_Free(L->rowlen);
+    PyMem_Free(L->pstart);
+    PyMem_Free(L->off);
+    memset(L, 0, sizeof(*L));
+}
+
+static int layout(Layout* L, const int32_t* counts, Py_ssize_t R, const int32_t* a, const int32_t* b, Py_ssize_t P,
+                  const uint8_t* keep) {
+    memset(L, 0, sizeof(*L));
+    L->R = R;
+    L->P = P;
+    L->first = (int64_t*)PyMem_Calloc((size_t)R + 1, sizeof(int64_t));
+    L->goff = (int64_t*)PyMem_Calloc((size_t)R + 1, sizeof(int64_t));
+    L->plist = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(P ? P : 1));
+    L->rowlen = (int64_t*)PyMem_Calloc((size_t)(R ? R : 1), sizeof(int64_t));
+    L->pstart = (int64_t*)PyMem_Calloc((size_t)(P ? P : 1), sizeof(int64_t));
+    if (!L->first || !L->goff || !L->plist || !L->rowlen || !L->pstart) { PyErr_NoMemory(); return -1; }
+    for (Py_ssize_t r = 0; r < R; ++r) {
+        if (counts[r] < 0) { PyErr_SetString(PyExc_ValueError, "negative copy count"); return -1; }
+        L->first[r + 1] = L->first[r] + counts[r];
+    }
+    L->N = (Py_ssize_t)L->first[R];
+    for (Py_ssize_t p = 0; p < P; ++p) {
+        if (a[p] < 0 || a[p] >= R || b[p] < 0 || b[p] >= R) {
+            PyErr_Format(PyExc_IndexError, "pair %zd: read index outside [0, %zd)", p, R);
+            return -1;
+        }
+        if (keep && !keep[p]) continue;
+        ++L->goff[a[p] + 1];
+    }
+    for (Py_ssize_t r = 0; r < R; ++r) L->goff[r + 1] += L->goff[r];
+    int64_t* fill = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(R ? R : 1));
+    if (!fill) { PyErr_NoMemory(); return -1; }
+    memcpy(fill, L->goff, sizeof(int64_t) * (size_t)R);
+    for (Py_ssize_t p = 0; p < P; ++p) {
+        if (keep && !keep[p]) continue;
+        const int32_t r = a[p];
+        L->plist[fill[r]++] = p;
+        L->pstart[p] = L->rowlen[r];
+        L->rowlen[r] += counts[b[p]];
+    }
+    PyMem_Free(fill);
+    L->off = (int64_t*)PyMem_Malloc(sizeof(int64_t) * ((size_t)L->N + 1));
+    if (!L->off) { PyErr_NoMemory(); return -1; }
+    L->off[0] = 0;
+    for (Py_ssize_t r = 0; r < R; ++r)
+        for (int64_t u = L->first[r]; u < L->first[r + 1]; ++u) L->off[u + 1] = L->off[u] + L->rowlen[r];
+    L->E = L->off[L->N];
+    return 0;
+}
+
+/* the columns of overlap_csr / build_overlap: counts, a, b (int32) and the optional keep mask (uint8 or None) */
+typedef struct {
+    Py_buffer c, a, b, k;
+    int has_k;
+} Cols;
+
+static void cols_release(Cols* C) {
+    if (C->c.obj) PyBuffer_Release(&C->c);
+    if (C->a.obj) PyBuffer_Release(&C->a);
+    if (C->b.obj) PyBuffer_Release(&C->b);
+    if (C->has_k && C->k.obj) PyBuffer_Release(&C->k);
+}
+
+static int cols_take(Cols* C, PyObject* oc, PyObject* oa, PyObject* ob, PyObject* ok) {
+    memset(C, 0, sizeof(*C));
+    if (take(oc, &C->c, 4, "counts") || take(oa, &C->a, 4, "a") || take(ob, &C->b, 4, "b")) return -1;
+    if (C->a.len != C->b.len) { PyErr_SetString(PyExc_ValueError, "a and b must have the same length"); return -1; }
+    if (ok && ok != Py_None) {
+        if (take(ok, &C->k, 1, "keep")) return -1;
+        C->has_k = 1;
+        if (C->k.len != C->a.len / 4) { PyErr_SetString(PyExc_ValueError, "keep must have one entry per pair"); return -1; }
+    }
+    return 0;
+}
+
+static PyObject* overlap_csr(PyObject* self, PyObject* args) {
+    (void)self;
+    PyObject *oc, *oa, *ob, *os, *ok = NULL;
+    if (!PyArg_ParseTuple(args, "OOOO|O", &oc, &oa, &ob, &os, &ok)) return NULL;
+    Cols C;
+    Py_buffer bs;
+    memset(&bs, 0, sizeof(bs));
+    Layout L;
+    memset(&L, 0, sizeof(L));
+    PyObject *boff = NULL, *bh = NULL, *bw = NULL, *out = NULL;
+    if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score")) goto done;
+    if (bs.len != C.a.len) { PyErr_SetString(PyExc_ValueError, "score must have one entry per pair"); goto done; }
+    {
+        const int32_t* counts = (const int32_t*)C.c.buf;
+        const int32_t* a = (const int32_t*)C.a.buf;
+        const int32_t* b = (const int32_t*)C.b.buf;
+        const int32_t* sc = (const int32_t*)bs.buf;
+        if (layout(&L, counts, C.c.len / 4, a, b, C.a.len / 4, C.has_k ? (const uint8_t*)C.k.buf : NULL)) goto done;
+        boff = PyByteArray_FromStringAndSize((const char*)L.off, (Py_ssize_t)(8 * ((size_t)L.N + 1)));
+        bh = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(4 * (L.E ? L.E : 1)));
+        bw = PyByteArray_FromStringAndSize(NULL, (Py_ssize_t)(8 * (L.E ? L.E : 1)));
+        if (!boff || !bh || !bw) goto done;
+        int32_t* heads = (int32_t*)PyByteArray_AS_STRING(bh);
+        int64_t* wts = (int64_t*)PyByteArray_AS_STRING(bw);
+        for (Py_ssize_t r = 0; r < L.R; ++r) {
+            if (L.first[r + 1] == L.first[r]) continue;
+            const int64_t u0 = L.first[r];
+            int64_t e = L.off[u0];
+            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                const int64_t p = L.plist[g];
+                const int64_t v0 = L.first[b[p]];
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb, ++e) {
+                    heads[e] = (int32_t)(v0 + cb);
+                    wts[e] = sc[p];
+                }
+            }
+            /* every other copy of read r has the same row */
+            for (int64_t u = u0 + 1; u < L.first[r + 1]; ++u) {
+                memcpy(heads + L.off[u], heads + L.off[u0], sizeof(int32_t) * (size_t)L.rowlen[r]);
+                memcpy(wts + L.off[u], wts + L.off[u0], sizeof(int64_t) * (size_t)L.rowlen[r]);
+            }
+        }
+        out = PyTuple_Pack(3, boff, bh, bw);
+    }
+done:
+    layout_free(&L);
+    cols_release(&C);
+    if (bs.obj) PyBuffer_Release(&bs);
+    Py_XDECREF(boff);
+    Py_XDECREF(bh);
+    Py_XDECREF(bw);
+    return out;
+}
+
+static PyObject* build_overlap(PyObject* self, PyObject* args) {
+    (void)self;
+    PyObject *names, *oc, *oa, *ob, *os, *oe, *ok = NULL, *oalive = NULL, *shared = NULL;
+    if (!PyArg_ParseTuple(args, "O!OOOOO|OOO!", &PyList_Type, &names, &oc, &oa, &ob, &os, &oe, &ok, &oalive,
+                          &PyDict_Type, &shared))
+        return NULL;
+    Cols C;
+    Py_buffer bs, be, bal;
+    memset(&bs, 0, sizeof(bs));
+    memset(&be, 0, sizeof(be));
+    memset(&bal, 0, sizeof(bal));
+    Layout L;
+    memset(&L, 0, sizeof(L));
+    PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
+    PyObject **sin = NULL, **pin = NULL, **dptr = NULL;
+    int64_t *dout = NULL, *din = NULL;
+    if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end")) goto done;
+    if (bs.len != C.a.len || be.len != C.a.len) {
+        PyErr_SetString(PyExc_ValueError, "score and end must have one entry per pair");
+        goto done;
+    }
+    {
+        const int32_t* counts = (const int32_t*)C.c.buf;
+        const int32_t* a = (const int32_t*)C.a.buf;
+        const int32_t* b = (const int32_t*)C.b.buf;
+        const int32_t* sc = (const int32_t*)bs.buf;
+        const int32_t* en = (const int32_t*)be.buf;
+        const uint8_t* keep = C.has_k ? (const uint8_t*)C.k.buf : NULL;
+        if (layout(&L, counts, C.c.len / 4, a, b, C.a.len / 4, keep)) goto done;
+        const Py_ssize_t n_nodes = PyList_GET_SIZE(names);
+        if (n_nodes != L.N) {
+            PyErr_Format(PyExc_ValueError, "%zd names for %zd nodes", n_nodes, L.N);
+            goto done;
+        }
+        const uint8_t* alive = NULL;
+        if (oalive && oalive != Py_None) {
+            if (take(oalive, &bal, 1, "alive")) goto done;
+            if (bal.len != L.E) { PyErr_SetString(PyExc_ValueError, "alive must have one entry per edge"); goto done; }
+            alive = (const uint8_t*)bal.buf;
+        }
+        /* live degrees: every dict is created at its final size */
+        dout = (int64_t*)PyMem_Calloc((size_t)(L.N ? L.N : 1), sizeof(int64_t));
+        din = (int64_t*)PyMem_Calloc((size_t)(L.N ? L.N : 1), sizeof(int64_t));
+        dptr = (PyObject**)PyMem_Calloc((size_t)(L.E ? L.E : 1), sizeof(PyObject*));
+        sin = (PyObject**)PyMem_Malloc(sizeof(PyObject*) * (size_t)(L.N ? L.N : 1));
+        pin = (PyObject**)PyMem_Malloc(sizeof(PyObject*) * (size_t)(L.N ? L.N : 1));
+        if (!dout || !din || !dptr || !sin || !pin) { PyErr_NoMemory(); goto done; }
+        for (Py_ssize_t g = 0; g < (Py_ssize_t)L.goff[L.R]; ++g) {
+            const int64_t p = L.plist[g];
+            for (int64_t u = L.first[a[p]]; u < L.first[a[p] + 1]; ++u) {
+                const int64_t e0 = L.off[u] + L.pstart[p];
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
+                    if (!alive || alive[e0 + cb]) {
+                        ++dout[u];
+                        ++din[L.first[b[p]] + cb];
+                    }
+            }
+        }
+        node = PyDict_New();
+        succ = PyDict_New();
+        pred = PyDict_New();
+        kw = PyUnicode_InternFromString("weight");
+        ke = PyUnicode_InternFromString("end_position");
+        if (!node || !succ || !pred || !kw || !ke) goto done;
+        for (Py_ssize_t i = 0; i < n_nodes; ++i) {
+            PyObject* name = PyList_GET_ITEM(names, i);
+            PyObject* x = PyDict_New();
+            PyObject* sd = _PyDict_NewPresized(dout[i]);
+            PyObject* pd = _PyDict_NewPresized(din[i]);
+            if (!x || !sd || !pd || PyDict_SetItem(node, name, x) || PyDict_SetItem(succ, name, sd) ||
+                PyDict_SetItem(pred, name, pd)) {
+                Py_XDECREF(x); Py_XDECREF(sd); Py_XDECREF(pd);
+                goto done;
+            }
+            Py_DECREF(x);
+            Py_DECREF(sd);
+            Py_DECREF(pd);
+            sin[i] = sd;
+            pin[i] = pd;
+        }
+        if (shared && PyDict_GET_SIZE(shared) == 2 && PyDict_Contains(shared, kw) == 1 && PyDict_Contains(shared, ke) == 1) {
+            tmpl = shared;
+            Py_INCREF(tmpl);
+        } else {
+            tmpl = PyDict_New();
+            if (!tmpl || PyDict_SetItem(tmpl, kw, Py_None) || PyDict_SetItem(tmpl, ke, Py_None)) goto done;
+        }
+        /* successors: row by row in CSR order (for a node, the global insertion order of its out-edges) */
+        for (Py_ssize_t r = 0; r < L.R; ++r) {
+            for (int64_t u = L.first[r]; u < L.first[r + 1]; ++u) {
+                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                    const int64_t p = L.plist[g];
+                    const int64_t e0 = L.off[u] + L.pstart[p];
+                    PyObject *wv = NULL, *ev = NULL;
+                    for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
+                        if (alive && !alive[e0 + cb]) continue;
+                        if (!wv) {
+                            wv = PyLong_FromLong(sc[p]);
+                            ev = PyLong_FromLong(en[p]);
+                            if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
+                        }
+                        PyObject* d = PyDict_Copy(tmpl);
+                        const int bad = !d || PyDict_SetItem(d, kw, wv) || PyDict_SetItem(d, ke, ev) ||
+                                        PyDict_SetItem(sin[u], PyList_GET_ITEM(names, L.first[b[p]] + cb), d);
+                        Py_XDECREF(d);
+                        if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
+                        dptr[e0 + cb] = d;  /* borrowed: the successor dict holds it */
+                    }
+                    Py_XDECREF(wv);
+                    Py_XDECREF(ev);
+                }
+            }
+        }
+        /* predecessors: edges in global insertion order (pair, copy of a, copy of b: overlapGraphs.py:43-60) */
+        for (Py_ssize_t p = 0; p < L.P; ++p) {
+            if (keep && !keep[p]) continue;
+            for (int64_t u = L.first[a[p]]; u < L.first[a[p] + 1]; ++u) {
+                const int64_t e0 = L.off[u] + L.pstart[p];
+                PyObject* un = PyList_GET_ITEM(names, u);
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
+                    PyObject* d = dptr[e0 + cb];
+                    if (d && PyDict_SetItem(pin[L.first[b[p]] + cb], un, d)) goto done;
+                }
+            }
+        }
+        out = PyTuple_Pack(3, node, succ, pred);
+    }
+done:
+    layout_free(&L);
+    cols_release(&C);
+    if (bs.obj) PyBuffer_Release(&bs);
+    if (be.obj) PyBuffer_Release(&be);
+    if (bal.obj) PyBuffer_Release(&bal);
+    PyMem_Free(dout);
+    PyMem_Free(din);
+    PyMem_Free(dptr);
+    PyMem_Free(sin);
+    PyMem_Free(pin);
+    Py_XDECREF(node);
+    Py_XDECREF(succ);
+    Py_XDECREF(pred);
+    Py_XDECREF(tmpl);
+    Py_XDECREF(kw);
+    Py_XDECREF(ke);
+    return out;
+}
+
 static PyMethodDef methods[] = {
+    {"overlap_csr", overlap_csr, METH_VARARGS,
+     "overlap_csr(counts, a, b, score[, keep]) -> (off int64, heads int32, weights int64) bytearrays"},
+    {"build_overlap", build_overlap, METH_VARARGS,
+     "build_overlap(names, counts, a, b, score, end[, keep[, alive[, shared]]]) -> (node, succ, pred)"},
     {"build", build, METH_VARARGS, "build(names, u, v, weight, end) -> (node, succ, pred) dicts of a networkx DiGraph"},
     {"csr", csr, METH_VARARGS, "csr(nodes, adj[, more int types]) -> (off int64, heads int32, weights int64) bytearrays"},
     {"remove_edges", remove_edges, METH_VARARGS, "remove_edges(succ, pred, nodes, tails, heads): bulk remove_edge"},

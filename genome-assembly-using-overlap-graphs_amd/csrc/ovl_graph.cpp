@@ -48,83 +48,128 @@ struct Event {
     int64_t old;
 };
 
-// settled[v] = 1 iff v cannot reach a cycle over the live edges.  roff/rtail/ralive: reverse CSR (edges
-// grouped by head: their tails, and whether they are live, kept contiguous so the reverse pass streams
-// instead of gathering edge ids).  Iterative Tarjan, then reverse reachability from the cyclic nodes.
-// Nodes already settled or explored cannot reach a cycle (explored nodes were all reached by a start
-// whose DFS found none), so they and the edges into them are left out.
-void settle(const int64_t* off, const int32_t* head, const uint8_t* alive, int32_t n,
-            const std::vector<int32_t>& rtail, const std::vector<int64_t>& roff, const std::vector<uint8_t>& ralive,
-            const std::vector<uint8_t>& explored, std::vector<uint8_t>& settled) {
-    if ((int32_t)settled.size() != n) settled.assign(n, 0);
-    std::vector<uint8_t> done(n);
-    for (int32_t v = 0; v < n; ++v) done[v] = settled[v] | explored[v];
-    std::vector<int32_t> idx(n, -1), low(n, 0), st;
-    std::vector<uint8_t> on(n, 0), bad(n, 0);
-    std::vector<int64_t> it(n, 0);
-    std::vector<int32_t> call;
-    int32_t counter = 0;
-    for (int32_t r = 0; r < n; ++r) {
-        if (idx[r] >= 0 || done[r]) continue;
-        call.push_back(r);
-        idx[r] = low[r] = counter++;
-        it[r] = off[r];
-        st.push_back(r);
-        on[r] = 1;
-        while (!call.empty()) {
-            const int32_t v = call.back();
-            bool descended = false;
-            while (it[v] < off[v + 1]) {
-                const int64_t e = it[v]++;
-                if (!alive[e]) continue;
-                const int32_t w = head[e];
-                if (done[w]) continue;
-                if (w == v) { bad[v] = 1; continue; }   // self-loop
-                if (idx[w] < 0) {
-                    idx[w] = low[w] = counter++;
-                    it[w] = off[w];
-                    st.push_back(w);
-                    on[w] = 1;
-                    call.push_back(w);
-                    descended = true;
-                    break;
+// settled[v] = 1 iff v cannot reach a cycle over the live edges.  Iterative Tarjan, then reverse reachability
+// from the cyclic nodes.  Nodes already settled or explored cannot reach a cycle (explored nodes were all
+// reached by a start whose DFS found none), and both sets only grow, as do the removed edges: so each call
+// first compacts the previous call's edge set to the live edges between nodes that are neither (forward CSR
+// plus its reverse), and the work of a call shrinks with the graph that is left.
+class Settler {
+  public:
+    Settler(const int64_t* off, const int32_t* head, int32_t n) : n_(n) {
+        const int64_t E = off[n];
+        coff_.assign(off, off + n + 1);
+        chead_.assign(head, head + E);
+        cid_.resize((size_t)E);
+        for (int64_t e = 0; e < E; ++e) cid_[(size_t)e] = e;
+    }
+    void run(const uint8_t* alive, const std::vector<uint8_t>& explored, std::vector<uint8_t>& settled) {
+        const int32_t n = n_;
+        if ((int32_t)settled.size() != n) settled.assign(n, 0);
+        std::vector<uint8_t> done(n);
+        for (int32_t v = 0; v < n; ++v) done[v] = settled[v] | explored[v];
+        // compact: live edges between nodes that are not done, in each row's order
+        {
+            int64_t w = 0;
+            int64_t start = 0;
+            for (int32_t v = 0; v < n; ++v) {
+                const int64_t e0 = start, e1 = coff_[(size_t)v + 1];
+                start = e1;
+                coff_[(size_t)v] = w;
+                if (done[v]) continue;
+                for (int64_t e = e0; e < e1; ++e) {
+                    const int32_t h = chead_[(size_t)e];
+                    const int64_t id = cid_[(size_t)e];
+                    if (!alive[id] || done[h]) continue;
+                    chead_[(size_t)w] = h;
+                    cid_[(size_t)w] = id;
+                    ++w;
                 }
-                if (on[w] && idx[w] < low[v]) low[v] = idx[w];
             }
-            if (descended) continue;
-            call.pop_back();
-            if (!call.empty()) {
-                const int32_t u = call.back();
-                if (low[v] < low[u]) low[u] = low[v];
-            }
-            if (low[v] == idx[v]) {  // v roots a component: pop it
-                size_t size = 0, top = st.size();
-                while (true) {
-                    const int32_t w = st[--top];
-                    on[w] = 0;
-                    ++size;
-                    if (w == v) break;
+            coff_[(size_t)n] = w;
+            chead_.resize((size_t)w);
+            cid_.resize((size_t)w);
+        }
+        const int64_t* off = coff_.data();
+        const int32_t* head = chead_.data();
+        std::vector<int32_t> idx(n, -1), low(n, 0), st;
+        std::vector<uint8_t> on(n, 0), bad(n, 0);
+        std::vector<int64_t> it(n, 0);
+        std::vector<int32_t> call;
+        int32_t counter = 0;
+        for (int32_t r = 0; r < n; ++r) {
+            if (idx[r] >= 0 || done[r]) continue;
+            call.push_back(r);
+            idx[r] = low[r] = counter++;
+            it[r] = off[r];
+            st.push_back(r);
+            on[r] = 1;
+            while (!call.empty()) {
+                const int32_t v = call.back();
+                bool descended = false;
+                while (it[v] < off[v + 1]) {
+                    const int32_t w = head[it[v]++];
+                    if (w == v) { bad[v] = 1; continue; }   // self-loop
+                    if (idx[w] < 0) {
+                        idx[w] = low[w] = counter++;
+                        it[w] = off[w];
+                        st.push_back(w);
+                        on[w] = 1;
+                        call.push_back(w);
+                        descended = true;
+                        break;
+                    }
+                    if (on[w] && idx[w] < low[v]) low[v] = idx[w];
                 }
-                if (size > 1)
-                    for (size_t k = top; k < st.size(); ++k) bad[st[k]] = 1;
-                st.resize(top);
+                if (descended) continue;
+                call.pop_back();
+                if (!call.empty()) {
+                    const int32_t u = call.back();
+                    if (low[v] < low[u]) low[u] = low[v];
+                }
+                if (low[v] == idx[v]) {  // v roots a component: pop it
+                    size_t size = 0, top = st.size();
+                    while (true) {
+                        const int32_t w = st[--top];
+                        on[w] = 0;
+                        ++size;
+                        if (w == v) break;
+                    }
+                    if (size > 1)
+                        for (size_t k = top; k < st.size(); ++k) bad[st[k]] = 1;
+                    st.resize(top);
+                }
             }
         }
-    }
-    // everything that reaches a cyclic node
-    std::vector<int32_t> queue;
-    for (int32_t v = 0; v < n; ++v)
-        if (bad[v]) queue.push_back(v);
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-        const int32_t v = queue[qi];
-        for (int64_t k = roff[v]; k < roff[v + 1]; ++k) {
-            if (!ralive[k]) continue;
-            const int32_t u = rtail[k];
-            if (!bad[u] && !done[u]) { bad[u] = 1; queue.push_back(u); }
+        // everything that reaches a cyclic node: BFS over the reverse of the compact edges
+        std::vector<int64_t> roff((size_t)n + 1, 0);
+        const int64_t E = off[n];
+        for (int64_t e = 0; e < E; ++e) ++roff[(size_t)head[e] + 1];
+        for (int32_t v = 0; v < n; ++v) roff[(size_t)v + 1] += roff[(size_t)v];
+        std::vector<int32_t> rtail((size_t)E);
+        {
+            std::vector<int64_t> fill(roff.begin(), roff.end() - 1);
+            for (int32_t v = 0; v < n; ++v)
+                for (int64_t e = off[v]; e < off[v + 1]; ++e) rtail[(size_t)fill[(size_t)head[e]]++] = v;
         }
+        std::vector<int32_t> queue;
+        for (int32_t v = 0; v < n; ++v)
+            if (bad[v]) queue.push_back(v);
+        for (size_t qi = 0; qi < queue.size(); ++qi) {
+            const int32_t v = queue[qi];
+            for (int64_t k = roff[(size_t)v]; k < roff[(size_t)v + 1]; ++k) {
+                const int32_t u = rtail[(size_t)k];
+                if (!bad[u]) { bad[u] = 1; queue.push_back(u); }
+            }
+        }
+        for (int32_t v = 0; v < n; ++v) settled[v] = !bad[v];
     }
-    for (int32_t v = 0; v < n; ++v) settled[v] = !bad[v];
-}
+
+  private:
+    int32_t n_;
+    std::vector<int64_t> coff_;   // compact forward CSR (row v: [coff_[v], coff_[v + 1]))
+    std::vector<int32_t> chead_;
+    std::vector<int64_t> cid_;    // compact edge -> CSR index of the input
+};
 
 }  // namespace
 
@@ -157,23 +202,9 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<int64_t> tail_pos(n_nodes, 0);  // node -> index of the path edge leaving it (valid while active)
     int64_t nrem = 0;
 
-    // reverse CSR: rtail[k] / ralive[k] for the k-th edge into its head; rpos[e] = k (a removal clears both)
-    std::vector<int64_t> roff(n_nodes + 1, 0), rpos(n_edges);
-    std::vector<int32_t> rtail(n_edges);
-    std::vector<uint8_t> ralive(n_edges, 1);
-    for (int64_t e = 0; e < n_edges; ++e) ++roff[head[e] + 1];
-    for (int32_t v = 0; v < n_nodes; ++v) roff[v + 1] += roff[v];
-    {
-        std::vector<int64_t> fill(roff.begin(), roff.end() - 1);
-        for (int32_t v = 0; v < n_nodes; ++v)
-            for (int64_t e = off[v]; e < off[v + 1]; ++e) {
-                const int64_t k = fill[head[e]]++;
-                rtail[k] = v;
-                rpos[e] = k;
-            }
-    }
+    Settler settler(off, head, n_nodes);
     std::vector<uint8_t> settled;
-    settle(off, head, alive.data(), n_nodes, rtail, roff, ralive, explored, settled);
+    settler.run(alive.data(), explored, settled);
     // yields between recomputations (OVL_CYCLES_SETTLE_EVERY: a test knob, e.g. 1 = after every yield)
     int64_t every = n_edges / 2;
     if (const char* env = getenv("OVL_CYCLES_SETTLE_EVERY")) every = atoll(env);
@@ -242,7 +273,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
             pos[cur] = q + 1;
             const int32_t h = head[q];
             if (--budget < 0) {
-                settle(off, head, alive.data(), n_nodes, rtail, roff, ralive, explored, settled);
+                settler.run(alive.data(), explored, settled);
                 budget = every;
                 if (settled[h]) continue;
             }
@@ -286,7 +317,6 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 const int32_t tail_of_dead = tail_of[kmin];
                 removed[nrem++] = dead;
                 alive[dead] = 0;
-                ralive[rpos[dead]] = 0;
                 skip[dead] = dead + 1;
                 // rewind the DFS to the moment `dead` was about to be yielded
                 const int64_t target = ckpt[kmin];

@@ -274,16 +274,17 @@ class OverlapEdges:
     ``reads`` / ``counts`` are ``read_copies`` (overlapGraphs.py:18-20) as two lists;
     ``a``, ``b``, ``score``, ``end`` are int32 arrays in the reference's pair order
     (overlapGraphs.py:43-53).  Every pair stands for ``counts[a] * counts[b]`` edges
-    (one per copy pair, :55-60).  ``to_digraph()`` materialises the reference's DiGraph.
+    (one per copy pair, :55-60).  ``to_digraph()`` gives the reference's DiGraph: lazy (its dicts
+    are built on first use) unless ``lazy=False``.
     """
 
     def __init__(self, reads, counts, a, b, score, end, min_score: Optional[int] = None):
         self.reads = list(reads)
         self.counts = list(counts)
-        self.a = np.asarray(a, dtype=np.int32)
-        self.b = np.asarray(b, dtype=np.int32)
-        self.score = np.asarray(score, dtype=np.int32)
-        self.end = np.asarray(end, dtype=np.int32)
+        self.a = np.ascontiguousarray(a, dtype=np.int32)
+        self.b = np.ascontiguousarray(b, dtype=np.int32)
+        self.score = np.ascontiguousarray(score, dtype=np.int32)
+        self.end = np.ascontiguousarray(end, dtype=np.int32)
         self.min_score = min_score  # edges kept only when score > min_score (overlapGraphs.py:225)
 
     def __len__(self) -> int:
@@ -297,6 +298,9 @@ class OverlapEdges:
 
     def kept(self) -> np.ndarray:
         return np.ones(len(self), bool) if self.min_score is None else self.score > self.min_score
+
+    def n_nodes(self) -> int:
+        return int(sum(self.counts))
 
     def n_edges(self) -> int:
         c = np.asarray(self.counts, dtype=np.int64)
@@ -319,9 +323,125 @@ class OverlapEdges:
         cb = c[b][pid]
         return (first[a][pid] + q // cb, first[b][pid] + q % cb, self.score[k][pid], self.end[k][pid])
 
-    def to_digraph(self) -> nx.DiGraph:
+    def _keep_mask(self):
+        return None if self.min_score is None else np.ascontiguousarray(self.kept(), dtype=np.uint8)
+
+    def csr(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """The graph's successor lists as CSR (off int64, heads int32, weights int64) in node order and, per
+        node, insertion order -- what ``remove_cycles_from_graph`` replays -- straight from the columns."""
+        mod = _digraph()
+        if mod is None:
+            raise RuntimeError("ovlgraph._digraph is not built (make -C genome-assembly-using-overlap-graphs_amd/csrc)")
+        boff, bh, bw = mod.overlap_csr(np.ascontiguousarray(self.counts, dtype=np.int32), self.a, self.b, self.score,
+                                       self._keep_mask())
+        off = np.frombuffer(boff, dtype=np.int64)
+        n = int(off[-1])
+        return off, np.frombuffer(bh, dtype=np.int32, count=n), np.frombuffer(bw, dtype=np.int64, count=n)
+
+    def _dicts(self, alive: Optional[np.ndarray] = None):
+        """(node, succ, pred) dicts of the DiGraph, for the edges whose CSR index (``csr()``) is alive."""
+        mod = _digraph()
+        gc_was = gc.isenabled()
+        gc.disable()  # millions of new dicts with no cycles: no collector passes over them while they are built
+        try:
+            if mod is not None:
+                return mod.build_overlap(self.node_names(), np.ascontiguousarray(self.counts, dtype=np.int32),
+                                         self.a, self.b, self.score, self.end, self._keep_mask(),
+                                         None if alive is None else np.ascontiguousarray(alive, dtype=np.uint8),
+                                         _attr_template())
+            if alive is not None:
+                raise RuntimeError("ovlgraph._digraph is not built: no survivors-only build")
+            G = _assemble_direct(self.reads, self.counts, self.a, self.b, self.score, self.end, self.min_score,
+                                 False)
+            return G._node, G._succ, G._pred
+        finally:
+            if gc_was:
+                gc.enable()
+
+    def to_digraph(self, lazy: bool = True) -> nx.DiGraph:
+        """The reference's DiGraph (overlapGraphs.py:22-60): a ``LazyOverlapDiGraph`` over these columns, or
+        with ``lazy=False`` one whose dicts are built now."""
+        if lazy and _digraph() is not None:
+            return LazyOverlapDiGraph._over(self)
         return assemble_graph_direct(self.reads, self.counts, self.a, self.b, self.score, self.end,
                                      self.min_score)
+
+
+class _Materialise:
+    """Data descriptor for a DiGraph dict attribute of ``LazyOverlapDiGraph``: the first read builds the
+    dicts from the columns (and the object becomes a plain ``nx.DiGraph``); a write (networkx's own
+    ``__init__``, or a caller replacing the dicts) makes it a plain DiGraph first."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __get__(self, obj, owner=None):
+        if obj is None:
+            return self
+        obj._materialise()
+        return obj.__dict__[self.name]
+
+    def __set__(self, obj, value):
+        if "_ovl_edges" in obj.__dict__:
+            obj._materialise()
+        obj.__class__ = nx.DiGraph
+        setattr(obj, self.name, value)
+
+
+class LazyOverlapDiGraph(nx.DiGraph):
+    """The overlap graph of ``construct_overlap_graph_nx_k`` before its dicts exist.
+
+    It is an ``nx.DiGraph`` over the columns of ``OverlapEdges``: the node / successor / predecessor dicts
+    (the structure ``add_edge`` builds, overlapGraphs.py:22-60) are built in C on the first access to any
+    of them, after which the object *is* a plain ``nx.DiGraph`` (its class is switched), so every view,
+    mutation and networkx algorithm behaves as on the reference's graph.  Until then node and edge counts
+    come from the columns, and ``remove_cycles_from_graph`` replays the cycle removal on a CSR built from
+    the columns and materialises only the surviving edges.
+    """
+
+    _node = _Materialise("_node")
+    _adj = _Materialise("_adj")
+    _succ = _adj
+    _pred = _Materialise("_pred")
+
+    @classmethod
+    def _over(cls, edges: "OverlapEdges") -> "LazyOverlapDiGraph":
+        G = cls.__new__(cls)
+        od = G.__dict__
+        od["graph"] = {}
+        od["__networkx_cache__"] = {}
+        od["_ovl_edges"] = edges
+        return G
+
+    def _materialise(self, alive: Optional[np.ndarray] = None) -> None:
+        od = self.__dict__
+        edges = od.get("_ovl_edges")
+        if edges is None:
+            return
+        node, succ, pred = edges._dicts(alive)
+        del od["_ovl_edges"]
+        self.__class__ = nx.DiGraph
+        self._node = node
+        self._succ = succ   # (networkx's descriptor: sets _adj and _succ, drops cached views)
+        self._pred = pred
+        nx._clear_cache(self)
+
+    @property
+    def is_materialised(self) -> bool:
+        return "_ovl_edges" not in self.__dict__
+
+    def __len__(self) -> int:
+        e = self.__dict__.get("_ovl_edges")
+        return e.n_nodes() if e is not None else super().__len__()
+
+    def number_of_nodes(self) -> int:
+        return len(self)
+
+    def number_of_edges(self, u=None, v=None) -> int:
+        e = self.__dict__.get("_ovl_edges")
+        if e is not None and u is None and v is None:
+            return e.n_edges()
+        return super().number_of_edges(u, v)
 
 
 _engines: Dict[Tuple[int, ...], OverlapEngine] = {}
@@ -426,9 +546,24 @@ def remove_cycles_from_graph(overlap_graph, native_edges: Optional[bool] = None,
     from . import _lib
     G = overlap_graph
     t0 = time.perf_counter()
+    mod = _digraph() if native_edges is not False else None
+    if native_edges and mod is None:
+        raise RuntimeError("ovlgraph._digraph is not built (make -C genome-assembly-using-overlap-graphs_amd/csrc)")
+    if mod is not None and type(G) is LazyOverlapDiGraph and not G.is_materialised:
+        # still columns: the replay's CSR straight from them, then the dicts of the surviving edges only
+        off, heads, weights = G.__dict__["_ovl_edges"].csr()
+        t1 = time.perf_counter()
+        removed, n_removed = _replay(off, heads, weights)
+        t2 = time.perf_counter()
+        alive = np.ones(heads.shape[0], dtype=np.uint8)
+        alive[removed[:n_removed]] = 0
+        G._materialise(alive)
+        t3 = time.perf_counter()
+        if timing is not None:
+            timing.update(csr=t1 - t0, replay=t2 - t1, remove=t3 - t2, removed=int(n_removed), lazy=True)
+        return G
     nodes = list(G)
     adj = G._adj
-    mod = _digraph() if native_edges is not False else None
     if native_edges and mod is None:
         raise RuntimeError("ovlgraph._digraph is not built (make -C genome-assembly-using-overlap-graphs_amd/csrc)")
     # the C passes need networkx's own DiGraph (plain dicts; remove_edge not overridden)
@@ -444,16 +579,11 @@ def remove_cycles_from_graph(overlap_graph, native_edges: Optional[bool] = None,
         off, heads, weights = _csr_python(nodes, adj)
         n_edges = int(off[-1])
     t1 = time.perf_counter()
-    removed = np.zeros(max(n_edges, 1), dtype=np.int64)
-    n_removed = ctypes.c_int64(0)
-    L = _lib.load()
-    _lib.check(L.ovl_remove_cycles(off.ctypes.data_as(ctypes.c_void_p), heads.ctypes.data_as(ctypes.c_void_p),
-                                   weights.ctypes.data_as(ctypes.c_void_p), len(nodes),
-                                   removed.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n_removed)))
+    removed, n_rem = _replay(off, heads, weights)
     t2 = time.perf_counter()
-    if n_removed.value:
+    if n_rem:
         # CSR index -> (u, v): the tail is the node whose adjacency range holds the index
-        idx = removed[: n_removed.value]
+        idx = removed[:n_rem]
         tails = np.searchsorted(off, idx, side="right") - 1
         if mod is not None:
             try:
@@ -466,8 +596,24 @@ def remove_cycles_from_graph(overlap_graph, native_edges: Optional[bool] = None,
                 G.remove_edge(nodes[t], nodes[heads[e]])
     t3 = time.perf_counter()
     if timing is not None:
-        timing.update(csr=t1 - t0, replay=t2 - t1, remove=t3 - t2, removed=int(n_removed.value))
+        timing.update(csr=t1 - t0, replay=t2 - t1, remove=t3 - t2, removed=int(n_rem), lazy=False)
     return G
+
+
+def _replay(off: np.ndarray, heads: np.ndarray, weights: np.ndarray) -> Tuple[np.ndarray, int]:
+    """ovl_remove_cycles over a CSR graph: (removed CSR indices in removal order, their count)."""
+    import ctypes
+    from . import _lib
+    n_nodes = off.shape[0] - 1
+    removed = np.zeros(max(heads.shape[0], 1), dtype=np.int64)
+    n_removed = ctypes.c_int64(0)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    heads = np.ascontiguousarray(heads, dtype=np.int32)
+    weights = np.ascontiguousarray(weights, dtype=np.int64)
+    _lib.check(_lib.load().ovl_remove_cycles(off.ctypes.data_as(ctypes.c_void_p), heads.ctypes.data_as(ctypes.c_void_p),
+                                             weights.ctypes.data_as(ctypes.c_void_p), n_nodes,
+                                             removed.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n_removed)))
+    return removed, int(n_removed.value)
 
 
 def topological_sort(dag):

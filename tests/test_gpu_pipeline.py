@@ -110,12 +110,13 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, pct, c
     slot reuse (many chunks, 1000-pair chunks that are not a multiple of the 64-pair rounding), bad pairs
     expanded to (-1, -1); non-temporal or ordinary host stores; pinned arrays with 0-100 % of the pairs in
     direct int32 chunks after the packed ones; OVL_PACK=0 is the int32 transport.  (OVL_PACK_MIN=0: packed
-    below the default 1 M-pair threshold.)"""
+    below the default 1 M-pair threshold; OVL_PAIRS_COMPACT=0: the pair list crosses as int32, 8 B/pair --
+    the compact encoding has its own tests, test_gpu_compact_pairs.py.)"""
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
     eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_NT": nt, "OVL_PACK_DIRECT_PCT": pct,
-                       "OVL_PIPE_CHUNK": chunk})
+                       "OVL_PIPE_CHUNK": chunk, "OVL_PAIRS_COMPACT": "0"})
     try:
         eng.set_reads(reads)
         n = a.shape[0] - 3

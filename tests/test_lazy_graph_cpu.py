@@ -1,0 +1,140 @@
+"""The lazy overlap DiGraph (no GPU): ``OverlapEdges.to_digraph()`` returns a
+``LazyOverlapDiGraph`` whose dicts are built from the columns on first use.  Every networkx view of it
+(nodes, successor / predecessor order, edge data, shared attribute dicts, degrees), mutation, copy and
+algorithm equals the eager graph's -- networkx's own add_edges_from construction (overlapGraphs.py:22-60) --,
+and ``remove_cycles_from_graph`` on a graph that is still lazy (CSR from the columns, survivors only) leaves
+exactly what it leaves on the eager graph, which the golden cycle records pin (test_cycles.py)."""
+import copy
+import pickle
+import random
+
+import networkx as nx
+import numpy as np
+import pytest
+
+from ovlgraph import overlapGraphs as og
+
+
+def _case(seed, n_reads=300, alphabet="ACG", k=2):
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    rng = random.Random(seed)
+    reads = ["".join(rng.choice(alphabet) for _ in range(rng.randint(1, 6))) for _ in range(n_reads)]
+    d, c = dedup_reads(reads)
+    a, b = enumerate_candidates(d, k)
+    sc = np.array([rng.randint(-3, 9) for _ in range(len(a))], np.int32)
+    en = np.arange(len(a), dtype=np.int32)
+    return d, c, a, b, sc, en
+
+
+def _same_views(L, G):
+    assert list(L.nodes()) == list(G.nodes())
+    assert list(L.nodes(data=True)) == list(G.nodes(data=True))
+    assert list(L.edges(data=True)) == list(G.edges(data=True))
+    assert list(L.in_edges(data=True)) == list(G.in_edges(data=True))
+    assert list(L.degree()) == list(G.degree())
+    assert list(L.in_degree()) == list(G.in_degree())
+    for n in G:
+        assert list(L.successors(n)) == list(G.successors(n))
+        assert list(L.predecessors(n)) == list(G.predecessors(n))
+        for v in L.successors(n):
+            assert L[n][v] is L.pred[v][n]  # one attribute dict per edge, shared as add_edge shares it
+            assert type(L[n][v]["weight"]) is int and type(L[n][v]["end_position"]) is int
+            assert L[n][v] == G[n][v]
+
+
+@pytest.mark.parametrize("ms", [None, 0, 5])
+def test_lazy_equals_networkx_construction(ms):
+    for seed in (1, 2, 3):
+        d, c, a, b, sc, en = _case(seed)
+        assert max(c) > 1
+        E = og.OverlapEdges(d, c, a, b, sc, en, min_score=ms)
+        L = E.to_digraph()
+        assert type(L) is og.LazyOverlapDiGraph and isinstance(L, nx.DiGraph) and not L.is_materialised
+        G = og.assemble_graph(d, c, a, b, sc, en, ms)
+        # counts come from the columns without building anything
+        assert len(L) == L.number_of_nodes() == G.number_of_nodes()
+        assert L.number_of_edges() == G.number_of_edges()
+        assert not L.is_materialised
+        _same_views(L, G)
+        assert type(L) is nx.DiGraph  # materialised: a plain networkx DiGraph from here on
+
+
+def test_each_dict_attribute_materialises():
+    d, c, a, b, sc, en = _case(4)
+    G = og.assemble_graph(d, c, a, b, sc, en)
+    for attr in ("_node", "_adj", "_succ", "_pred", "adj", "succ", "pred", "nodes", "edges"):
+        L = og.OverlapEdges(d, c, a, b, sc, en).to_digraph()
+        getattr(L, attr)
+        assert type(L) is nx.DiGraph, attr
+        assert L._adj is L._succ
+        _same_views(L, G)
+
+
+def test_mutation_copy_pickle_and_algorithms():
+    d, c, a, b, sc, en = _case(5)
+    E = og.OverlapEdges(d, c, a, b, sc, en)
+    G = og.assemble_graph(d, c, a, b, sc, en)
+    # mutation straight on a lazy graph
+    L = E.to_digraph()
+    u, v = next(iter(G.edges()))
+    for H in (L, G):
+        H.add_edge(u, v, weight=-7)
+        H.remove_edge(*list(G.edges())[3])
+        H.add_node("extra", tag=1)
+        H.add_edge("extra", u, weight=2, end_position=0)
+        H[u][v]["color"] = "red"
+    _same_views(L, G)
+    # copies, pickles and derived graphs of a graph that is still lazy
+    for make in (lambda H: H.copy(), lambda H: copy.deepcopy(H), lambda H: pickle.loads(pickle.dumps(H)),
+                 lambda H: H.reverse(copy=True), lambda H: nx.DiGraph(H)):
+        L = E.to_digraph()
+        G = og.assemble_graph(d, c, a, b, sc, en)
+        _same_views(make(L), make(G))
+    L = E.to_digraph()
+    sub = list(G.nodes())[::3]
+    assert list(L.subgraph(sub).edges(data=True)) == list(G.subgraph(sub).edges(data=True))
+    # a networkx algorithm on a lazy graph
+    L = E.to_digraph()
+    assert nx.find_cycle(L, orientation="original") == nx.find_cycle(G, orientation="original")
+    # an empty lazy graph
+    z = np.zeros(0, np.int32)
+    _same_views(og.OverlapEdges(["A"], [2], z, z, z, z).to_digraph(), og.assemble_graph(["A"], [2], z, z, z, z))
+
+
+def test_remove_cycles_on_lazy_graph():
+    for seed in (6, 7, 8):
+        d, c, a, b, sc, en = _case(seed, n_reads=400)
+        E = og.OverlapEdges(d, c, a, b, sc, en)
+        st_l, st_e = {}, {}
+        L = og.remove_cycles_from_graph(E.to_digraph(), timing=st_l)
+        G = og.remove_cycles_from_graph(og.assemble_graph(d, c, a, b, sc, en), timing=st_e)
+        assert st_l["lazy"] and not st_e["lazy"] and st_l["removed"] == st_e["removed"] > 0
+        assert type(L) is nx.DiGraph
+        _same_views(L, G)
+        assert nx.is_directed_acyclic_graph(L)
+
+
+def test_remove_cycles_lazy_overlap_graph(oracle_mod):
+    """A PhiX overlap graph (1,200 reads, l = 100, p = 0.01, k = 5) with its copies: lazy cycle removal
+    keeps what the oracle's loop (the reference's find_cycle loop) keeps."""
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import read_genome_from_fasta, simulate_reads
+    reads, copies = dedup_reads(simulate_reads(read_genome_from_fasta(), 100, 1200, 0.01, seed=9))
+    a, b = enumerate_candidates(reads, 5)
+    sc, en = oracle_mod.batch_ungapped(reads, a, b, 10, -1)
+    L = og.remove_cycles_from_graph(og.OverlapEdges(reads, copies, a, b, sc, en).to_digraph())
+    ref = oracle_mod.remove_cycles(og.assemble_graph(reads, copies, a, b, sc, en))
+    _same_views(L, ref)
+
+
+def test_csr_from_columns_matches_graph_csr():
+    import ctypes  # noqa: F401
+    for ms in (None, 0):
+        d, c, a, b, sc, en = _case(9)
+        E = og.OverlapEdges(d, c, a, b, sc, en, min_score=ms)
+        off, heads, w = E.csr()
+        G = og.assemble_graph(d, c, a, b, sc, en, ms)
+        ref_off, ref_heads, ref_w = og._csr_python(list(G), G._adj)
+        np.testing.assert_array_equal(off, ref_off)
+        np.testing.assert_array_equal(heads, ref_heads)
+        np.testing.assert_array_equal(w, ref_w)
