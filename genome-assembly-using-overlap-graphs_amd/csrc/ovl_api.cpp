@@ -1200,6 +1200,34 @@ int setup_job(const Call& C, Job& J) {
     return OVL_OK;
 }
 
+// OVL_TRACE_PIPE=1 (diagnostics): one stderr line per host-array call with the microsecond offsets of its
+// pipeline events (s setup, i<k> chunk k issued, w<k> its results ready on the host side, d<k> drained,
+// y final synchronisation).
+struct PipeTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    std::string line;
+    PipeTrace() : on(enabled()), t0(std::chrono::steady_clock::now()) {}
+    static bool enabled() {
+        static const bool e = [] {
+            const char* v = getenv("OVL_TRACE_PIPE");
+            return v && atoi(v) != 0;
+        }();
+        return e;
+    }
+    void mark(char what, int64_t k) {
+        if (!on) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        char buf[48];
+        snprintf(buf, sizeof(buf), " %c%lld=%.1f", what, (long long)k, us);
+        line += buf;
+    }
+    ~PipeTrace() {
+        if (on) fprintf(stderr, "ovl_pipe:%s\n", line.c_str());
+    }
+};
+thread_local PipeTrace* g_trace = nullptr;
+
 // Compact host pair list, chunk k (C.compact): the host pool encodes the caller's int32 pairs into the pinned
 // encoding buffer and kernels on the device's second stream decode them into HBM (ovl_pairs.hip), reading the
 // encoding through the host mapping; the chunk's scoring launch waits for dec_ev[k].  Encoding of chunk k:
@@ -1278,6 +1306,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
         }
     });
     if (runs) starts[R] = (int32_t)n;
+    if (g_trace) g_trace->mark('e', k);
     // decode on the second stream (host-mapped reads) into this chunk's slice of the HBM list
     char* db = d->cp_dev + base;
     char* da = db + b_bytes;
@@ -1399,33 +1428,6 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     return OVL_OK;
 }
 
-// OVL_TRACE_PIPE=1 (diagnostics): one stderr line per host-array call with the microsecond offsets of its
-// pipeline events (s setup, i<k> chunk k issued, w<k> its results ready on the host side, d<k> drained,
-// y final synchronisation).
-struct PipeTrace {
-    bool on;
-    std::chrono::steady_clock::time_point t0;
-    std::string line;
-    PipeTrace() : on(enabled()), t0(std::chrono::steady_clock::now()) {}
-    static bool enabled() {
-        static const bool e = [] {
-            const char* v = getenv("OVL_TRACE_PIPE");
-            return v && atoi(v) != 0;
-        }();
-        return e;
-    }
-    void mark(char what, int64_t k) {
-        if (!on) return;
-        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-        char buf[48];
-        snprintf(buf, sizeof(buf), " %c%lld=%.1f", what, (long long)k, us);
-        line += buf;
-    }
-    ~PipeTrace() {
-        if (on) fprintf(stderr, "ovl_pipe:%s\n", line.c_str());
-    }
-};
-thread_local PipeTrace* g_trace = nullptr;
 
 // Pageable outputs: copy chunk k out of its staging slot once its results are there (the D2H copy, or in
 // direct mode the kernel that stored them).
@@ -1933,10 +1935,13 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
     if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
     DeviceGuard guard;
+    PipeTrace trace;  // OVL_TRACE_PIPE: r recount, p prepared, s staged, u uploads issued, y synchronised
     CpuShare::get().refresh();
+    trace.mark('r', 0);
     HostReads h;
     int rc = prep_reads(c, seqs, offsets, n_reads, h);
     if (rc != OVL_OK) return rc;
+    trace.mark('p', 0);
     c->h_len.clear();
     hipError_t e = hipSuccess;
     for (Dev* d : c->devs) {
@@ -1948,13 +1953,16 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     // to every device, then wait for all (the uploads and packs overlap across devices)
     rc = stage_reads(c, c->stage, h);
     if (rc != OVL_OK) return rc;
+    trace.mark('s', 0);
     for (Dev* d : c->devs)
         if ((e = upload_reads(d, h, c->stage)) != hipSuccess) break;
+    trace.mark('u', 0);
     for (Dev* d : c->devs) {
         (void)hipSetDevice(d->device);
         hipError_t e2 = hipStreamSynchronize(d->stream);
         if (e == hipSuccess) e = e2;
     }
+    trace.mark('y', 0);
     if (e != hipSuccess)
         return fail(c, e == hipErrorOutOfMemory ? OVL_E_OOM : OVL_E_HIP, "ovl_set_reads: %s", hipGetErrorString(e));
     for (Dev* d : c->devs) {

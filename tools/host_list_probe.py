@@ -1,0 +1,55 @@
+"""Where a host-pair-list call and a read upload spend their time (OVL_TRACE_PIPE=1 lines on stderr):
+ovl_score_host with the target list in pageable and pinned host memory (compact encoding on / off) and
+ovl_set_reads, at the target point.
+
+    OVL_TRACE_PIPE=1 python tools/host_list_probe.py [config] 2> trace.txt
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
+import numpy as np  # noqa: E402
+
+
+def main():
+    from ovlgraph import OverlapEngine
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.engine import encode_reads
+    from ovlgraph.hostmem import pinned_empty
+    from ovlgraph.reads import config_reads
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "target"
+    reads, _ = dedup_reads(config_reads(cfg, seed=0))
+    enc = encode_reads(reads)
+    res = {}
+    for label, env in (("compact", {}), ("plain", {"OVL_PAIRS_COMPACT": "0"})):
+        os.environ.update(env)
+        eng = OverlapEngine(0)
+        for k in env:
+            os.environ.pop(k)
+        eng.set_reads(reads, enc)
+        a, b = eng.candidates(5)
+        a, b = np.array(a), np.array(b)
+        pa, pb = pinned_empty(a.shape[0]), pinned_empty(a.shape[0])
+        pa[:], pb[:] = a, b
+        out = (pinned_empty(a.shape[0]), pinned_empty(a.shape[0]))
+        for lst, (x, y) in (("pageable", (a, b)), ("pinned", (pa, pb))):
+            for _ in range(3):
+                eng.score(x, y, out=out)
+            t0 = time.perf_counter()
+            for _ in range(20):
+                eng.score(x, y, out=out)
+            res[f"{label}_{lst}_ms"] = (time.perf_counter() - t0) / 20 * 1e3
+            sys.stderr.write(f"== {label} {lst} above\n")
+        t0 = time.perf_counter()
+        for _ in range(10):
+            eng.set_reads(reads, enc)
+        res[f"{label}_set_reads_ms"] = (time.perf_counter() - t0) / 10 * 1e3
+        sys.stderr.write("== set_reads above\n")
+        eng.close()
+    print(res)
+
+
+if __name__ == "__main__":
+    main()
