@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <emmintrin.h>
+#include <immintrin.h>
 #include <pthread.h>
 #include <sched.h>
 #include <sys/socket.h>
@@ -667,9 +668,13 @@ class CpuShare {
     // CPUs this process may run on: its affinity set, capped by the cgroup quota (cpu.max)
     int cpus() const { return cpus_; }
     int sharers() const { return sharers_.load(std::memory_order_relaxed); }
-    // join (once per process) and recount: max(bound slots, LOCAL_WORLD_SIZE), at least 1
-    int refresh() {
+    // join (once per process) and recount: max(bound slots, LOCAL_WORLD_SIZE), at least 1.  A recount probes
+    // 64 slots (~90 us on the box), so setup calls reuse a count younger than 50 ms unless `force`
+    int refresh(bool force = false) {
         std::lock_guard<std::mutex> lk(mu_);
+        const auto now = std::chrono::steady_clock::now();
+        if (!force && fd_ >= 0 && now - last_ < std::chrono::milliseconds(50)) return sharers_.load();
+        last_ = now;
         if (fd_ < 0) fd_ = bind_slot(-1);
         int bound = 0;
         for (int i = 0; i < kSlots; ++i) {
@@ -735,6 +740,7 @@ class CpuShare {
     int fd_ = -1, slot_ = -1;
     char key_[64];
     std::atomic<int> sharers_{1};
+    std::chrono::steady_clock::time_point last_{};
     std::mutex mu_;
 };
 
@@ -998,7 +1004,7 @@ int create_on(const int32_t* ids, int32_t n, ovl_ctx** out) {
             if (ids[j] == ids[i]) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "device %d listed twice", ids[i]);
     }
     DeviceGuard guard;
-    CpuShare::get().refresh();
+    CpuShare::get().refresh(true);
     ovl_ctx* c = new ovl_ctx();
     const Knobs knobs = read_knobs();
     for (int32_t i = 0; i < n; ++i) {
@@ -1251,8 +1257,10 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
     char* ha = hb + b_bytes;                       // a area: runs, or a like b
     CopyPool& pool = CopyPool::get();
     const std::vector<size_t> parts = pool.cut((size_t)n, size_t(1) << 15);
-    std::vector<int64_t> starts_in(parts.size(), 0);
-    // pass 1: b, and the run starts of a in each part (a[i] != a[i - 1], and i == 0)
+    // one pass: b, and the runs of a (a[i] != a[i - 1], and i == 0) into part-local lists, given up (kept
+    // short) once a part has more than 1 run per 16 pairs -- then a crosses like b
+    std::vector<std::vector<int32_t>> pv(parts.size()), ps(parts.size());
+    std::vector<uint8_t> many(parts.size(), 0);
     pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
         if (wd == 2) {
             uint16_t* o = reinterpret_cast<uint16_t*>(hb);
@@ -1263,48 +1271,55 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
         } else {
             memcpy(reinterpret_cast<int32_t*>(hb) + lo, B + lo, sizeof(int32_t) * (hi - lo));
         }
-        int64_t c = 0;
+        const size_t cap = (hi - lo) / 16 + 1;
+        std::vector<int32_t>& vv = pv[i];
+        std::vector<int32_t>& ss = ps[i];
+        vv.reserve(cap);
+        ss.reserve(cap);
         int32_t prev = lo ? A[lo - 1] : (int32_t)~A[0];
         for (size_t p = lo; p < hi; ++p) {
             const int32_t v = A[p];
-            c += v != prev;
+            if (v != prev) {
+                if (vv.size() == cap) {
+                    many[i] = 1;
+                    break;
+                }
+                vv.push_back(v);
+                ss.push_back((int32_t)p);
+            }
             prev = v;
         }
-        starts_in[i] = c;
     });
     int64_t R = 0;
-    std::vector<int64_t> first(parts.size(), 0);
+    bool runs = n < (int64_t(1) << 31);
     for (size_t i = 0; i + 1 < parts.size(); ++i) {
-        first[i] = R;
-        R += starts_in[i];
+        runs = runs && !many[i];
+        R += (int64_t)pv[i].size();
     }
-    const bool runs = 8 * R + 4 < n * wd && n < (int64_t(1) << 31);
+    runs = runs && 8 * R + 4 < n * wd;
     int32_t* vals = reinterpret_cast<int32_t*>(ha);
     int32_t* starts = vals + ((R + 3) & ~int64_t(3));  // 16-byte aligned
-    // pass 2: the runs, or a like b
-    pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
-        if (runs) {
-            int64_t r = first[i];
-            int32_t prev = lo ? A[lo - 1] : (int32_t)~A[0];
-            for (size_t p = lo; p < hi; ++p) {
-                const int32_t v = A[p];
-                if (v != prev) {
-                    vals[r] = v;
-                    starts[r] = (int32_t)p;
-                    ++r;
-                }
-                prev = v;
-            }
-        } else if (wd == 2) {
-            uint16_t* o = reinterpret_cast<uint16_t*>(ha);
-            for (size_t p = lo; p < hi; ++p) {
-                const int32_t v = A[p];
-                o[p] = (v >= 0 && v < nr) ? (uint16_t)v : (uint16_t)0xFFFF;
-            }
-        } else {
-            memcpy(reinterpret_cast<int32_t*>(ha) + lo, A + lo, sizeof(int32_t) * (hi - lo));
+    if (runs) {
+        int64_t r = 0;
+        for (size_t i = 0; i + 1 < parts.size(); ++i) {
+            memcpy(vals + r, pv[i].data(), sizeof(int32_t) * pv[i].size());
+            memcpy(starts + r, ps[i].data(), sizeof(int32_t) * ps[i].size());
+            r += (int64_t)pv[i].size();
         }
-    });
+    } else {
+        // a like b (a second pass, for lists that are not a-major)
+        pool.parallel_parts(parts, [&](size_t, size_t lo, size_t hi) {
+            if (wd == 2) {
+                uint16_t* o = reinterpret_cast<uint16_t*>(ha);
+                for (size_t p = lo; p < hi; ++p) {
+                    const int32_t v = A[p];
+                    o[p] = (v >= 0 && v < nr) ? (uint16_t)v : (uint16_t)0xFFFF;
+                }
+            } else {
+                memcpy(reinterpret_cast<int32_t*>(ha) + lo, A + lo, sizeof(int32_t) * (hi - lo));
+            }
+        });
+    }
     if (runs) starts[R] = (int32_t)n;
     if (g_trace) g_trace->mark('e', k);
     // decode on the second stream (host-mapped reads) into this chunk's slice of the HBM list
@@ -1744,7 +1759,7 @@ OVL_API int ovl_host_unregister(void* ptr) {
 
 OVL_API int ovl_host_pool(int32_t* threads, int32_t* sharers, int32_t* cpus, int32_t* packed) {
     CpuShare& cs = CpuShare::get();
-    const int n = cs.refresh();
+    const int n = cs.refresh(true);
     const int t = CopyPool::threads();
     if (threads) *threads = t;
     if (sharers) *sharers = n;
@@ -1807,6 +1822,80 @@ struct HostReads {
     int32_t n_reads = 0, lmax = 0, planes = 2, wmax = 0, srow = 0, trow = 0;
 };
 
+// seen[v] = 1 for every byte value v in p[0 .. n).  Reads are DNA: 64-byte blocks made of A, C, G and T only
+// are settled with four compares (AVX-512BW; AVX2 on 32-byte blocks), other blocks byte by byte.
+void scan_bytes(const uint8_t* p, size_t n, uint8_t* seen) {
+    uint8_t t[4][256] = {};  // four tables: independent stores
+    size_t q = 0;
+    for (; q + 4 <= n; q += 4) {
+        t[0][p[q]] = 1;
+        t[1][p[q + 1]] = 1;
+        t[2][p[q + 2]] = 1;
+        t[3][p[q + 3]] = 1;
+    }
+    for (; q < n; ++q) t[0][p[q]] = 1;
+    for (int v = 0; v < 256; ++v) seen[v] |= t[0][v] | t[1][v] | t[2][v] | t[3][v];
+}
+
+__attribute__((target("avx512f,avx512bw"))) void scan_symbols_avx512(const uint8_t* p, size_t n, uint8_t* seen) {
+    const __m512i A = _mm512_set1_epi8('A'), C = _mm512_set1_epi8('C'), G = _mm512_set1_epi8('G'),
+                  T = _mm512_set1_epi8('T');
+    __mmask64 ma = 0, mc = 0, mg = 0, mt = 0;
+    size_t q = 0;
+    for (; q + 64 <= n; q += 64) {
+        const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(p + q));
+        const __mmask64 a = _mm512_cmpeq_epi8_mask(v, A), c = _mm512_cmpeq_epi8_mask(v, C),
+                        g = _mm512_cmpeq_epi8_mask(v, G), t = _mm512_cmpeq_epi8_mask(v, T);
+        if ((a | c | g | t) != ~__mmask64(0)) {
+            scan_bytes(p + q, 64, seen);
+            continue;
+        }
+        ma |= a;
+        mc |= c;
+        mg |= g;
+        mt |= t;
+    }
+    scan_bytes(p + q, n - q, seen);
+    seen['A'] |= ma != 0;
+    seen['C'] |= mc != 0;
+    seen['G'] |= mg != 0;
+    seen['T'] |= mt != 0;
+}
+
+__attribute__((target("avx2"))) void scan_symbols_avx2(const uint8_t* p, size_t n, uint8_t* seen) {
+    const __m256i A = _mm256_set1_epi8('A'), C = _mm256_set1_epi8('C'), G = _mm256_set1_epi8('G'),
+                  T = _mm256_set1_epi8('T');
+    uint32_t ma = 0, mc = 0, mg = 0, mt = 0;
+    size_t q = 0;
+    for (; q + 32 <= n; q += 32) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + q));
+        const uint32_t a = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, A));
+        const uint32_t c = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, C));
+        const uint32_t g = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, G));
+        const uint32_t t = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, T));
+        if ((a | c | g | t) != 0xFFFFFFFFu) {
+            scan_bytes(p + q, 32, seen);
+            continue;
+        }
+        ma |= a;
+        mc |= c;
+        mg |= g;
+        mt |= t;
+    }
+    scan_bytes(p + q, n - q, seen);
+    seen['A'] |= ma != 0;
+    seen['C'] |= mc != 0;
+    seen['G'] |= mg != 0;
+    seen['T'] |= mt != 0;
+}
+
+void scan_symbols(const uint8_t* p, size_t n, uint8_t* seen) {
+    static const int isa = __builtin_cpu_supports("avx512bw") ? 2 : (__builtin_cpu_supports("avx2") ? 1 : 0);
+    if (isa == 2) scan_symbols_avx512(p, n, seen);
+    else if (isa == 1) scan_symbols_avx2(p, n, seen);
+    else scan_bytes(p, n, seen);
+}
+
 int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads, HostReads& h) {
     const int64_t base = n_reads > 0 ? offsets[0] : 0;
     if (base < 0) return fail(c, OVL_E_ARG, "offsets[0] < 0");
@@ -1832,20 +1921,9 @@ int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t 
     if (h.total > 0) {
         CopyPool& pool = CopyPool::get();
         const std::vector<size_t> parts = pool.cut((size_t)h.total, size_t(1) << 18);
-        std::vector<std::array<uint8_t, 256>> seen(parts.size());
+        std::vector<std::array<uint8_t, 256>> seen(parts.size(), std::array<uint8_t, 256>{});
         const uint8_t* src = h.src;
-        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
-            uint8_t t[4][256] = {};  // four tables: independent stores
-            size_t q = lo;
-            for (; q + 4 <= hi; q += 4) {
-                t[0][src[q]] = 1;
-                t[1][src[q + 1]] = 1;
-                t[2][src[q + 2]] = 1;
-                t[3][src[q + 3]] = 1;
-            }
-            for (; q < hi; ++q) t[0][src[q]] = 1;
-            for (int v = 0; v < 256; ++v) seen[i][(size_t)v] = t[0][v] | t[1][v] | t[2][v] | t[3][v];
-        });
+        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) { scan_symbols(src + lo, hi - lo, seen[i].data()); });
         for (const auto& t : seen)
             for (int v = 0; v < 256; ++v) present[v] = present[v] || t[(size_t)v];
     }
