@@ -192,9 +192,22 @@ struct ReadStage {
     size_t o_off = 0, o_len = 0, o_full = 0, o_lut = 0, o_raw = 0;
 };
 
+// The host-side facts of a read set (prep_reads); kept by the context so that its arrays are reused, without
+// fresh pages to fault in, by the next ovl_set_reads.
+struct HostReads {
+    std::vector<int64_t> off;
+    std::vector<int32_t> len;
+    std::vector<uint32_t> full;
+    uint8_t lut[256];
+    const uint8_t* src = nullptr;  // the caller's bytes, then (stage_reads) their pinned copy
+    int64_t total = 0;
+    int32_t n_reads = 0, lmax = 0, planes = 2, wmax = 0, srow = 0, trow = 0;
+};
+
 struct ovl_ctx {
     std::vector<Dev*> devs;
     ReadStage stage;             // pinned upload stage of ovl_set_reads
+    HostReads hreads;            // ovl_set_reads' host arrays (reused)
     std::string err;
     std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
     int32_t timing = 0;          // ovl_set_timing
@@ -1271,24 +1284,30 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
         } else {
             memcpy(reinterpret_cast<int32_t*>(hb) + lo, B + lo, sizeof(int32_t) * (hi - lo));
         }
+        // (thread-local lists, handed over at the end: the parts' vector objects share cache lines)
         const size_t cap = (hi - lo) / 16 + 1;
-        std::vector<int32_t>& vv = pv[i];
-        std::vector<int32_t>& ss = ps[i];
-        vv.reserve(cap);
-        ss.reserve(cap);
+        std::vector<int32_t> vv(cap), ss(cap);
+        int32_t* pvv = vv.data();
+        int32_t* pss = ss.data();
+        size_t r = 0;
         int32_t prev = lo ? A[lo - 1] : (int32_t)~A[0];
         for (size_t p = lo; p < hi; ++p) {
             const int32_t v = A[p];
             if (v != prev) {
-                if (vv.size() == cap) {
+                if (r == cap) {
                     many[i] = 1;
                     break;
                 }
-                vv.push_back(v);
-                ss.push_back((int32_t)p);
+                pvv[r] = v;
+                pss[r] = (int32_t)p;
+                ++r;
             }
             prev = v;
         }
+        vv.resize(r);
+        ss.resize(r);
+        pv[i] = std::move(vv);
+        ps[i] = std::move(ss);
     });
     int64_t R = 0;
     bool runs = n < (int64_t(1) << 31);
@@ -1812,16 +1831,6 @@ OVL_API int ovl_last_timing(const ovl_ctx* c, double* kernel_ms, double* call_ms
 
 namespace {
 
-struct HostReads {
-    std::vector<int64_t> off;
-    std::vector<int32_t> len;
-    std::vector<uint32_t> full;
-    uint8_t lut[256];
-    const uint8_t* src = nullptr;  // the caller's bytes, then (stage_reads) their pinned copy
-    int64_t total = 0;
-    int32_t n_reads = 0, lmax = 0, planes = 2, wmax = 0, srow = 0, trow = 0;
-};
-
 // seen[v] = 1 for every byte value v in p[0 .. n).  Reads are DNA: 64-byte blocks made of A, C, G and T only
 // are settled with four compares (AVX-512BW; AVX2 on 32-byte blocks), other blocks byte by byte.
 void scan_bytes(const uint8_t* p, size_t n, uint8_t* seen) {
@@ -2016,7 +2025,8 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     PipeTrace trace;  // OVL_TRACE_PIPE: r recount, p prepared, s staged, u uploads issued, y synchronised
     CpuShare::get().refresh();
     trace.mark('r', 0);
-    HostReads h;
+    HostReads& h = c->hreads;
+    h.lmax = 0;
     int rc = prep_reads(c, seqs, offsets, n_reads, h);
     if (rc != OVL_OK) return rc;
     trace.mark('p', 0);
