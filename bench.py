@@ -838,6 +838,9 @@ def parse_args(argv=None):
     # launcher checks without a GPU (tests/test_bench_launch.py): ranks join a gloo group, rank 0 prints the
     # identity line, and --dry-run-fail-rank R makes rank R exit with status 3
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    # the N > 1 code path at world size 1 (torch.distributed over RCCL with one rank): a one-GPU box runs the
+    # multi-process line's collectives, gathers and sharded step for real (tests/test_gpu_bench_dist.py)
+    ap.add_argument("--dist-path", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
     if args.gpus < 1:
@@ -905,7 +908,16 @@ def main() -> int:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     backend = os.environ.get("OVL_BENCH_BACKEND") or ("gloo" if shared else "nccl")  # nccl = RCCL on ROCm
-    if world > 1:
+    if world > 1 or args.dist_path:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                with socket.socket() as sk:
+                    sk.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

@@ -143,6 +143,8 @@ struct Dev {
     hipEvent_t scratch_evt = nullptr;     // last launch that used lane_col / seed_* ...
     hipEvent_t ev_last = nullptr;         // packed calls into pinned arrays: after the last (direct) chunk
     double pack_pct = -1.0;               // live direct share of packed calls into pinned arrays (pack_share)
+    double pack_pct_h = -1.0;             // the same for calls with a compact host pair list (the host also
+                                          // encodes the list, so its balance point differs)
     hipStream_t scratch_stream = nullptr; // ... and its stream (launches on other streams wait for it)
     bool scratch_used = false;
     int64_t codes_bytes = 0;
@@ -1132,8 +1134,9 @@ int setup_job(const Call& C, Job& J) {
     // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
     if (C.pack) {
-        if (d->pack_pct < 0.0) d->pack_pct = d->k.pack_direct_pct;
-        const int64_t pct = d->k.pack_adapt ? (int64_t)(d->pack_pct + 0.5) : d->k.pack_direct_pct;
+        double& share = C.compact ? d->pack_pct_h : d->pack_pct;
+        if (share < 0.0) share = C.compact ? 2.0 * d->k.pack_direct_pct : d->k.pack_direct_pct;
+        const int64_t pct = d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct;
         packed = C.out_pinned ? (n - n * pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
         const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
@@ -1562,11 +1565,13 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         const auto tw = std::chrono::steady_clock::now();
         const hipError_t q = hipEventQuery(d->ev_last);
         if (q == hipSuccess) {
-            d->pack_pct = std::min(50.0, d->pack_pct + 1.0);
+            double& share = C.compact ? d->pack_pct_h : d->pack_pct;
+            share = std::min(C.compact ? 80.0 : 50.0, share + 1.0);
         } else if (q == hipErrorNotReady) {
             HIPCHK(c, wait_event(d, d->ev_last));
             const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
-            if (us > 8.0) d->pack_pct = std::max(2.0, d->pack_pct - 1.0);
+            double& share = C.compact ? d->pack_pct_h : d->pack_pct;
+            if (us > 8.0) share = std::max(2.0, share - 1.0);
         }
     }
     for (Job& J : jobs) {

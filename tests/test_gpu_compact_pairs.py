@@ -141,3 +141,24 @@ def test_one_shot_abi_call(oracle_mod, target):
         rs, re_ = oracle_mod.batch_closed_form(small, a[keep], b[keep])
         np.testing.assert_array_equal(s, rs)
         np.testing.assert_array_equal(e, re_)
+
+
+def test_compact_adaptive_share(oracle_mod, target):
+    """Host-list calls into pinned arrays keep their own adaptive direct share (the host also encodes the
+    list): exact results call after call, the packed part within 20-98 % of the pairs."""
+    from ovlgraph import OverlapEngine
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = target
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+    n = a.shape[0]
+    with OverlapEngine(0) as eng:
+        eng.set_reads(reads)
+        out = (pinned_empty(n), pinned_empty(n))
+        shares = []
+        for _ in range(12):
+            out[0][:] = -9
+            eng.score(a, b, out=out)
+            np.testing.assert_array_equal(out[0], ref_s)
+            np.testing.assert_array_equal(out[1], ref_e)
+            shares.append(eng.last_transfer()["packed_pairs"] / n)
+        assert all(0.19 <= x <= 0.99 for x in shares), shares
