@@ -739,7 +739,8 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
     import torch.distributed as dist
     name = args.config or "target"
     ident = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
-             "devices_visible": torch.cuda.device_count(), "devices_shared": shared}
+             "devices_visible": torch.cuda.device_count(), "devices_shared": shared,
+             "rank0_numa_node": int(os.environ["OVL_BENCH_NUMA_NODE"]) if os.environ.get("OVL_BENCH_NUMA_NODE") else None}
     if shared:
         ident["note"] = ("more ranks than visible GPUs: ranks share devices (flow rehearsal, gloo barriers) -- "
                          "not a scaling number")
@@ -803,6 +804,42 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
     return line
 
 
+def gpu_numa_node(dev) -> int:
+    """The NUMA node the GPU's PCIe link hangs off (sysfs), or -1."""
+    import torch
+    pr = torch.cuda.get_device_properties(dev)
+    path = "/sys/bus/pci/devices/%04x:%02x:%02x.0/numa_node" % (pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+    try:
+        with open(path) as fh:
+            return int(fh.read().strip())
+    except (OSError, ValueError):
+        return -1
+
+
+def bind_to_gpu_node(dev):
+    """One process per GPU on a 2-socket host (4 GPUs per socket on the MI355X nodes): run this rank's threads
+    on its GPU's NUMA node, so its pinned result arrays, staging and host-pool threads are socket-local -- N
+    ranks each write ~16 MB of results per step into host memory, and remote-socket traffic would cross the
+    inter-socket link.  Returns the node, or None when unknown or not allowed."""
+    node = gpu_numa_node(dev)
+    if node < 0:
+        return None
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as fh:
+            spec = fh.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            lo, _, hi = part.partition("-")
+            cpus.update(range(int(lo), int(hi or lo) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return None
+        os.sched_setaffinity(0, cpus)
+        return node
+    except (OSError, ValueError):
+        return None
+
+
 def spawn_ranks(n: int) -> int:
     """--gpus N > 1 without a launcher: run torch.distributed.run with N ranks of this script as a child
     process (never an exec: nothing here has touched the GPU) and return its exit status."""
@@ -828,6 +865,8 @@ def parse_args(argv=None):
     ap.add_argument("--seed", type=int, default=0, help="read-set seed (weak scaling: rank r uses seed + r)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra configs and stages")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="N > 1: leave the ranks' CPU affinity alone (default: each rank on its GPU's NUMA node)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of all-core CPU-baseline work")
     ap.add_argument("--indel", type=int, default=None, help="indel score (default: the reference's -2**31)")
     ap.add_argument("--band", type=int, default=-1, help="band half-width (-1 = full DP, the reference)")
@@ -908,6 +947,10 @@ def main() -> int:
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     backend = os.environ.get("OVL_BENCH_BACKEND") or ("gloo" if shared else "nccl")  # nccl = RCCL on ROCm
+    numa = None
+    if world > 1 and not shared and not args.no_numa_bind:
+        numa = bind_to_gpu_node(dev)  # before the engine, its host pool and any pinned allocation
+    os.environ["OVL_BENCH_NUMA_NODE"] = "" if numa is None else str(numa)
     if world > 1 or args.dist_path:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -423,6 +423,21 @@ done:
     return out;
 }
 
+/* Python ints for edge attributes: one object per distinct value in [kIntLo, kIntHi) (scores <= 10 * l and end
+ * positions <= l for the reads of the benchmark configs), shared by every edge that carries it, instead of two
+ * allocations per pair; values outside the range are created per pair. */
+enum { kIntLo = -4096, kIntHi = 8192 };
+
+static PyObject* int_of(PyObject** cache, long v) {
+    if (v >= kIntLo && v < kIntHi) {
+        PyObject** slot = &cache[v - kIntLo];
+        if (!*slot) *slot = PyLong_FromLong(v);
+        Py_XINCREF(*slot);
+        return *slot;
+    }
+    return PyLong_FromLong(v);
+}
+
 static PyObject* build_overlap(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *names, *oc, *oa, *ob, *os, *oe, *ok = NULL, *oalive = NULL, *shared = NULL;
@@ -430,6 +445,7 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
                           &PyDict_Type, &shared))
         return NULL;
     Cols C;
+    memset(&C, 0, sizeof(C));
     Py_buffer bs, be, bal;
     memset(&bs, 0, sizeof(bs));
     memset(&be, 0, sizeof(be));
@@ -438,7 +454,9 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
     memset(&L, 0, sizeof(L));
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
     PyObject **sin = NULL, **pin = NULL, **dptr = NULL;
+    PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t *dout = NULL, *din = NULL;
+    if (!ints) { PyErr_NoMemory(); goto done; }
     if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end")) goto done;
     if (bs.len != C.a.len || be.len != C.a.len) {
         PyErr_SetString(PyExc_ValueError, "score and end must have one entry per pair");
@@ -520,8 +538,8 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
                     for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
                         if (alive && !alive[e0 + cb]) continue;
                         if (!wv) {
-                            wv = PyLong_FromLong(sc[p]);
-                            ev = PyLong_FromLong(en[p]);
+                            wv = int_of(ints, sc[p]);
+                            ev = int_of(ints, en[p]);
                             if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
                         }
                         PyObject* d = PyDict_Copy(tmpl);
@@ -556,6 +574,10 @@ done:
     if (bs.obj) PyBuffer_Release(&bs);
     if (be.obj) PyBuffer_Release(&be);
     if (bal.obj) PyBuffer_Release(&bal);
+    if (ints) {
+        for (int i = 0; i < kIntHi - kIntLo; ++i) Py_XDECREF(ints[i]);
+        PyMem_Free(ints);
+    }
     PyMem_Free(dout);
     PyMem_Free(din);
     PyMem_Free(dptr);

@@ -187,37 +187,53 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
         if (head[e] < 0 || head[e] >= n_nodes) return OVL_E_ARG;
     if (n_edges > 0 && !removed) return OVL_E_ARG;
 
+    if (n_edges >= (int64_t(1) << 31) - 1) return OVL_E_UNSUPPORTED;  // int32 skip deltas
+
+    // Per edge, what one yield touches, in one 16-byte record: the head, the skip delta to the next edge
+    // that may still be yielded (0: this one; edges removed or into explored / settled nodes are spliced
+    // out), the weight.  A sentinel record ends the array.
+    struct Edge {
+        int32_t head;
+        int32_t skip;
+        int64_t w;
+    };
+    std::vector<Edge> ed((size_t)n_edges + 1);
+    for (int64_t e = 0; e < n_edges; ++e) ed[(size_t)e] = {head[e], 0, weight[e]};
+    ed[(size_t)n_edges] = {0, 0, 0};
     std::vector<uint8_t> alive(n_edges, 1), explored(n_nodes, 0), visited(n_nodes, 0), active(n_nodes, 0),
-        seen(n_nodes, 0);
+        seen(n_nodes, 0), done(n_nodes, 0);  // done = explored | settled (both only grow)
     std::vector<int64_t> pos(n_nodes, 0);  // out-edge iterator position (CSR index) of visited nodes
-    std::vector<int64_t> skip(n_edges + 1);   // skip[e] == e for live edges (and the end), else > e
-    for (int64_t e = 0; e <= n_edges; ++e) skip[e] = e;
-    std::vector<int64_t> path;             // find_cycle's `edges`: the active path, as CSR indices
-    std::vector<int64_t> ckpt;             // per path edge: undo-log size just before it was yielded
+    // find_cycle's `edges`: the active path, one record per path edge: its CSR index, the undo-log size just
+    // before it was yielded, its weight, its tail (the node whose iterator yielded it) and head
+    struct PathEdge {
+        int64_t q;
+        int64_t ckpt;
+        int64_t w;
+        int32_t tail;
+        int32_t head;
+    };
+    std::vector<PathEdge> path;
     std::vector<int32_t> stack;            // edge_dfs stack: the start node, then the path heads
     std::vector<int32_t> seen_list;
     std::vector<Event> log;
-    std::vector<int32_t> tail_of;          // path edge -> its tail (the node whose iterator yielded it)
-    std::vector<int64_t> path_w;           // path edge -> its weight (the cycle's minimum scans this, contiguous)
     std::vector<int64_t> tail_pos(n_nodes, 0);  // node -> index of the path edge leaving it (valid while active)
     int64_t nrem = 0;
 
     Settler settler(off, head, n_nodes);
     std::vector<uint8_t> settled;
     settler.run(alive.data(), explored, settled);
+    for (int32_t v = 0; v < n_nodes; ++v) done[v] = settled[v];
     // yields between recomputations (OVL_CYCLES_SETTLE_EVERY: a test knob, e.g. 1 = after every yield)
     int64_t every = n_edges / 2;
     if (const char* env = getenv("OVL_CYCLES_SETTLE_EVERY")) every = atoll(env);
     if (every <= 0) every = INT64_MAX;  // only the initial computation
     int64_t budget = every;
 
+    Edge* E = ed.data();
     for (int32_t s = 0; s < n_nodes; ++s) {
-        if (explored[s] || settled[s]) continue;
+        if (done[s]) continue;
         log.clear();
         path.clear();
-        ckpt.clear();
-        tail_of.clear();
-        path_w.clear();
         seen_list.clear();
         stack.assign(1, s);
         int32_t root = s;  // find_cycle's path root (the start node; a reset re-roots at the tail)
@@ -225,13 +241,14 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
         seen[s] = 1;
         seen_list.push_back(s);
         int32_t prev_head = -1;
-        bool done = false;
-        while (!done) {
+        for (;;) {
             if (stack.empty()) {
                 // no cycle reachable from s: everything seen is explored for the later starts
-                for (int32_t v : seen_list) explored[v] = 1;
+                for (int32_t v : seen_list) {
+                    explored[v] = 1;
+                    done[v] = 1;
+                }
                 active[root] = 0;
-                done = true;
                 break;
             }
             const int32_t cur = stack.back();
@@ -242,22 +259,23 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
             }
             // next yield of cur's iterator.  Edges into explored or settled nodes are walked by edge_dfs
             // without any effect on find_cycle, and both sets only grow, so such an edge is spliced out
-            // of every later iteration (skip pointers, shared with the removed edges) instead of being
+            // of every later iteration (skip deltas, shared with the removed edges) instead of being
             // yielded; the iterator advance over a run of them is logged once with the yield after it.
             const int64_t end = off[cur + 1];
             int64_t q = pos[cur];
             for (;;) {
-                while (skip[q] != q) {  // first live edge at or after q (path halving)
-                    skip[q] = skip[skip[q]];
-                    q = skip[q];
+                while (E[q].skip) {  // first live edge at or after q (path halving)
+                    const int64_t p1 = q + E[q].skip;
+                    const int64_t p2 = p1 + E[p1].skip;
+                    E[q].skip = (int32_t)(p2 - q);
+                    q = p2;
                 }
                 if (q >= end) {
                     q = end;
                     break;
                 }
-                const int32_t hq = head[q];
-                if (!explored[hq] && !settled[hq]) break;
-                skip[q] = q + 1;
+                if (!done[E[q].head]) break;
+                E[q].skip = 1;
             }
             if (q == end) {  // iterator exhausted: pop
                 if (pos[cur] != q) {
@@ -271,9 +289,10 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
             const int64_t mark = (int64_t)log.size();
             log.push_back({1, cur, pos[cur]});
             pos[cur] = q + 1;
-            const int32_t h = head[q];
+            const int32_t h = E[q].head;
             if (--budget < 0) {
                 settler.run(alive.data(), explored, settled);
+                for (int32_t v = 0; v < n_nodes; ++v) done[v] = explored[v] | settled[v];
                 budget = every;
                 if (settled[h]) continue;
             }
@@ -287,39 +306,32 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                         active[root] = 1;
                         break;
                     }
-                    const int64_t pe = path.back();
+                    active[path.back().head] = 0;
                     path.pop_back();
-                    ckpt.pop_back();
-                    tail_of.pop_back();
-                    path_w.pop_back();
-                    active[head[pe]] = 0;
-                    if (!path.empty() && head[path.back()] == cur) break;
+                    if (!path.empty() && path.back().head == cur) break;
                 }
             }
             tail_pos[cur] = (int64_t)path.size();
-            path.push_back(q);
-            ckpt.push_back(mark);
-            tail_of.push_back(cur);
-            path_w.push_back(weight[q]);
+            path.push_back({q, mark, E[q].w, cur, h});
             if (active[h]) {
                 // cycle: the path suffix from the first edge leaving h (the path is simple, so that edge is
                 // tail_pos[h]); remove its weakest edge, the first minimum in cycle order
                 const size_t i0 = (size_t)tail_pos[h];
+                const PathEdge* pp = path.data();
                 size_t kmin = i0;
-                int64_t wmin = path_w[i0];
-                const int64_t* pw = path_w.data();
+                int64_t wmin = pp[i0].w;
                 for (size_t k = i0 + 1; k < path.size(); ++k)
-                    if (pw[k] < wmin) {
-                        wmin = pw[k];
+                    if (pp[k].w < wmin) {
+                        wmin = pp[k].w;
                         kmin = k;
                     }
-                const int64_t dead = path[kmin];
-                const int32_t tail_of_dead = tail_of[kmin];
+                const int64_t dead = pp[kmin].q;
+                const int32_t tail_of_dead = pp[kmin].tail;
                 removed[nrem++] = dead;
                 alive[dead] = 0;
-                skip[dead] = dead + 1;
+                E[dead].skip = 1;
                 // rewind the DFS to the moment `dead` was about to be yielded
-                const int64_t target = ckpt[kmin];
+                const int64_t target = pp[kmin].ckpt;
                 while ((int64_t)log.size() > target) {
                     const Event ev = log.back();
                     log.pop_back();
@@ -333,12 +345,9 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                     }
                 }
                 // heads leaving the path (not the closing edge's: that node is on the surviving path)
-                for (size_t k = kmin; k + 1 < path.size(); ++k) active[head[path[k]]] = 0;
+                for (size_t k = kmin; k + 1 < path.size(); ++k) active[pp[k].head] = 0;
                 active[root] = 1;  // (the root is unchanged since path[kmin] was yielded)
                 path.resize(kmin);
-                ckpt.resize(kmin);
-                tail_of.resize(kmin);
-                path_w.resize(kmin);
                 // the edge_dfs stack at that moment: the root (= the start node: only it can be on the
                 // stack without being a path head) and the surviving path heads
                 stack.resize(kmin + 1);
@@ -348,7 +357,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                     root = tail_of_dead;
                     active[root] = 1;
                 }
-                prev_head = kmin > 0 ? head[path[kmin - 1]] : -1;
+                prev_head = kmin > 0 ? path[kmin - 1].head : -1;
                 continue;
             }
             if (!seen[h]) {
