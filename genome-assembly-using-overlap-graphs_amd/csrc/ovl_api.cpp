@@ -1218,7 +1218,9 @@ int setup_job(const Call& C, Job& J) {
     }
     if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
     if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
-    if (C.pack && d->k.pack_stage) HIPCHK(d, ensure(d->pk_hbm, (size_t)kSlots * 2 * (size_t)d->st_cap + 64));
+    // kSlots slots of st_cap uint16 (+ slack: a copy moves whole 16-byte pieces)
+    if (C.pack && d->k.pack_stage)
+        HIPCHK(d, ensure(d->pk_hbm, (size_t)kSlots * sizeof(uint16_t) * (size_t)d->st_cap + 64));
     if (C.timing && (int64_t)d->t_ev.size() < 2 * J.nchunks) {
         while ((int64_t)d->t_ev.size() < 2 * J.nchunks) {
             hipEvent_t ev;
@@ -1410,7 +1412,7 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     // stream moves the 2 B/pair to the host staging slot while the next chunk scores (the escaped scores of
     // the few pairs that need them still go straight to the host slot); the slot's previous copy is done
     const bool via_hbm = C.pack && k < J.n_packed && d->k.pack_stage;
-    uint16_t* pk = as<uint16_t>(d->pk_hbm) + (size_t)slot * 2 * (size_t)d->st_cap;
+    uint16_t* pk = as<uint16_t>(d->pk_hbm) + (size_t)slot * (size_t)d->st_cap;  // slots of st_cap uint16
     if (via_hbm) {
         os = reinterpret_cast<int32_t*>(pk);
         if (k >= kSlots) HIPCHK(d, hipStreamWaitEvent(d->stream, d->ev_k[slot], 0));
