@@ -93,9 +93,10 @@ struct Knobs {
     int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
-    int32_t pack_stage = 1;       // OVL_PACK_STAGE=0: packed chunks store over the link from the scoring kernel
-                                  // itself instead of into HBM, with a copy kernel on the second stream moving
-                                  // them to the host staging slot while the next chunk scores (A/B knob)
+    int32_t pack_stage = 0;       // OVL_PACK_STAGE: packed chunks score into HBM and move to the host staging slot
+                                  // while the next chunk scores -- 1 a copy kernel on the second stream, 2 a
+                                  // copy-engine transfer, 3 a copy kernel on a high-priority stream -- instead
+                                  // of storing over the link from the scoring kernel itself (0; A/B knob)
     int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
                                   // instead of the compact encoding (encode_chunk; A/B knob)
     int64_t compact_min = 1 << 16;  // OVL_PAIRS_COMPACT_MIN: compact encoding from this many pairs per call
@@ -116,6 +117,7 @@ struct Dev {
     hipStream_t stream = nullptr;  // kernels
     hipStream_t s_in = nullptr;    // H2D copies of host-array calls
     hipStream_t s_out = nullptr;   // D2H copies of host-array calls
+    hipStream_t s_hi = nullptr;    // OVL_PACK_STAGE=3: packed-chunk copies at high priority
     int32_t cu_count = 256;
     Knobs k;
     // knob aliases used by the launch code
@@ -659,7 +661,7 @@ Knobs read_knobs() {
         k.pack_adapt = 0;  // a fixed share
     }
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PACK_STAGE")) k.pack_stage = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PACK_STAGE")) k.pack_stage = std::max(0, std::min(3, atoi(e)));
     if (const char* e = getenv("OVL_PAIRS_COMPACT_MIN")) k.compact_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
@@ -951,7 +953,7 @@ void free_staging(int32_t*& p) {
 void destroy_dev(Dev* d) {
     if (!d) return;
     (void)hipSetDevice(d->device);
-    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
+    for (hipStream_t s : {d->stream, d->s_in, d->s_out, d->s_hi})
         if (s) (void)hipStreamSynchronize(s);
     for (DevBuf* b : {&d->codes, &d->off, &d->len, &d->sfx, &d->pfx, &d->lut, &d->full, &d->raw, &d->a, &d->b,
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
@@ -973,7 +975,7 @@ void destroy_dev(Dev* d) {
         if (e) (void)hipEventDestroy(e);
     if (d->scratch_evt) (void)hipEventDestroy(d->scratch_evt);
     if (d->ev_last) (void)hipEventDestroy(d->ev_last);
-    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
+    for (hipStream_t s : {d->stream, d->s_in, d->s_out, d->s_hi})
         if (s) (void)hipStreamDestroy(s);
     delete d;
 }
@@ -1423,9 +1425,21 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
     if (via_hbm) {
         HIPCHK(d, hipEventRecord(d->ev_sc[slot], d->stream));
-        HIPCHK(d, hipStreamWaitEvent(d->s_out, d->ev_sc[slot], 0));
-        HIPCHK(d, ovl_launch_to_host(pk, d->st_out_dev + so, 2 * n, d->s_out));
-        HIPCHK(d, hipEventRecord(d->ev_k[slot], d->s_out));
+        hipStream_t cs = d->s_out;
+        if (d->k.pack_stage == 3) {
+            if (!d->s_hi) {
+                int lo = 0, hi = 0;
+                HIPCHK(d, hipDeviceGetStreamPriorityRange(&lo, &hi));
+                HIPCHK(d, hipStreamCreateWithPriority(&d->s_hi, hipStreamNonBlocking, hi));
+            }
+            cs = d->s_hi;
+        }
+        HIPCHK(d, hipStreamWaitEvent(cs, d->ev_sc[slot], 0));
+        if (d->k.pack_stage == 2)
+            HIPCHK(d, hipMemcpyAsync(d->st_out + so, pk, 2 * (size_t)n, hipMemcpyDeviceToHost, cs));
+        else
+            HIPCHK(d, ovl_launch_to_host(pk, d->st_out_dev + so, 2 * n, cs));
+        HIPCHK(d, hipEventRecord(d->ev_k[slot], cs));
     } else if (staged_in || staged_out) {
         HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
     }
@@ -1521,7 +1535,8 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
 void quiesce(std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         (void)hipSetDevice(J.d->device);
-        for (hipStream_t s : {J.d->stream, J.d->s_in, J.d->s_out}) (void)hipStreamSynchronize(s);
+        for (hipStream_t s : {J.d->stream, J.d->s_in, J.d->s_out, J.d->s_hi})
+            if (s) (void)hipStreamSynchronize(s);
     }
 }
 
@@ -1603,7 +1618,10 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         if (J.nchunks == 0) continue;
         HIPCHK(c, hipSetDevice(J.d->device));
         HIPCHK(c, hipStreamSynchronize(C.direct ? J.d->stream : J.d->s_out));
-        if (C.direct && C.pack) HIPCHK(c, hipStreamSynchronize(J.d->s_out));  // (the packed chunks' copies)
+        if (C.direct && C.pack) {  // (the packed chunks' copies)
+            HIPCHK(c, hipStreamSynchronize(J.d->s_out));
+            if (J.d->s_hi) HIPCHK(c, hipStreamSynchronize(J.d->s_hi));
+        }
     }
     trace.mark('y', 0);
     double kms = 0.0;
