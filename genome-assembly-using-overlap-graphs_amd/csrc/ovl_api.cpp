@@ -93,10 +93,6 @@ struct Knobs {
     int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
-    int32_t pack_stage = 0;       // OVL_PACK_STAGE: packed chunks score into HBM and move to the host staging slot
-                                  // while the next chunk scores -- 1 a copy kernel on the second stream, 2 a
-                                  // copy-engine transfer, 3 a copy kernel on a high-priority stream -- instead
-                                  // of storing over the link from the scoring kernel itself (0; A/B knob)
     int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
                                   // instead of the compact encoding (encode_chunk; A/B knob)
     int64_t compact_min = 1 << 16;  // OVL_PAIRS_COMPACT_MIN: compact encoding from this many pairs per call
@@ -117,7 +113,6 @@ struct Dev {
     hipStream_t stream = nullptr;  // kernels
     hipStream_t s_in = nullptr;    // H2D copies of host-array calls
     hipStream_t s_out = nullptr;   // D2H copies of host-array calls
-    hipStream_t s_hi = nullptr;    // OVL_PACK_STAGE=3: packed-chunk copies at high priority
     int32_t cu_count = 256;
     Knobs k;
     // knob aliases used by the launch code
@@ -171,8 +166,6 @@ struct Dev {
     size_t l_tb_host_bytes = 0;
     // host-array pipeline: events per slot and pinned staging (slots x cap pairs x {a, b} / {score, end})
     hipEvent_t ev_h2d[kSlots] = {}, ev_in[kSlots] = {}, ev_k[kSlots] = {}, ev_out[kSlots] = {};
-    hipEvent_t ev_sc[kSlots] = {};  // packed chunk scored into its HBM slot (pk_hbm), before the copy to the host
-    DevBuf pk_hbm;                  // packed results of kSlots chunks in HBM (OVL_PACK_STAGE)
     int32_t* st_in = nullptr;
     int32_t* st_out = nullptr;
     int32_t* st_in_dev = nullptr;   // device addresses of the staging rings (kernels read / store them)
@@ -661,7 +654,6 @@ Knobs read_knobs() {
         k.pack_adapt = 0;  // a fixed share
     }
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PACK_STAGE")) k.pack_stage = std::max(0, std::min(3, atoi(e)));
     if (const char* e = getenv("OVL_PAIRS_COMPACT_MIN")) k.compact_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
@@ -953,13 +945,13 @@ void free_staging(int32_t*& p) {
 void destroy_dev(Dev* d) {
     if (!d) return;
     (void)hipSetDevice(d->device);
-    for (hipStream_t s : {d->stream, d->s_in, d->s_out, d->s_hi})
+    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
         if (s) (void)hipStreamSynchronize(s);
     for (DevBuf* b : {&d->codes, &d->off, &d->len, &d->sfx, &d->pfx, &d->lut, &d->full, &d->raw, &d->a, &d->b,
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
                       &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
                       &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
-                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids, &d->pk_hbm})
+                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids})
         release(*b);
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
@@ -969,13 +961,13 @@ void destroy_dev(Dev* d) {
     for (hipEvent_t e : d->dec_ev)
         if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < kSlots; ++i)
-        for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i], d->ev_sc[i]})
+        for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i]})
             if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : d->t_ev)
         if (e) (void)hipEventDestroy(e);
     if (d->scratch_evt) (void)hipEventDestroy(d->scratch_evt);
     if (d->ev_last) (void)hipEventDestroy(d->ev_last);
-    for (hipStream_t s : {d->stream, d->s_in, d->s_out, d->s_hi})
+    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
         if (s) (void)hipStreamDestroy(s);
     delete d;
 }
@@ -991,7 +983,7 @@ hipError_t init_dev(Dev* d) {
         if (e != hipSuccess) return e;
     }
     for (int i = 0; i < kSlots; ++i)
-        for (hipEvent_t* ev : {&d->ev_h2d[i], &d->ev_in[i], &d->ev_k[i], &d->ev_out[i], &d->ev_sc[i]}) {
+        for (hipEvent_t* ev : {&d->ev_h2d[i], &d->ev_in[i], &d->ev_k[i], &d->ev_out[i]}) {
             e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
             if (e != hipSuccess) return e;
         }
@@ -1216,13 +1208,10 @@ int setup_job(const Call& C, Job& J) {
     if ((need_in || need_out) && J.chunk > d->st_cap) {
         free_staging(d->st_in);
         free_staging(d->st_out);
-        d->st_cap = (J.chunk + 7) & ~int64_t(7);  // slots 16-byte aligned (the packed copies move 16-byte pieces)
+        d->st_cap = J.chunk;
     }
     if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
     if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
-    // kSlots slots of st_cap uint16 (+ slack: a copy moves whole 16-byte pieces)
-    if (C.pack && d->k.pack_stage)
-        HIPCHK(d, ensure(d->pk_hbm, (size_t)kSlots * sizeof(uint16_t) * (size_t)d->st_cap + 64));
     if (C.timing && (int64_t)d->t_ev.size() < 2 * J.nchunks) {
         while ((int64_t)d->t_ev.size() < 2 * J.nchunks) {
             hipEvent_t ev;
@@ -1410,39 +1399,11 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     int32_t* os = staged_out ? d->st_out_dev + so : J.d_score + off;
     int32_t* oe = staged_out ? d->st_out_dev + so + d->st_cap : J.d_end + off;
     d->out_mode = C.pack && k < J.n_packed ? 2 : 1;
-    // a packed chunk scores into its HBM slot, at the kernel's own speed, and a copy kernel on the second
-    // stream moves the 2 B/pair to the host staging slot while the next chunk scores (the escaped scores of
-    // the few pairs that need them still go straight to the host slot); the slot's previous copy is done
-    const bool via_hbm = C.pack && k < J.n_packed && d->k.pack_stage;
-    uint16_t* pk = as<uint16_t>(d->pk_hbm) + (size_t)slot * (size_t)d->st_cap;  // slots of st_cap uint16
-    if (via_hbm) {
-        os = reinterpret_cast<int32_t*>(pk);
-        if (k >= kSlots) HIPCHK(d, hipStreamWaitEvent(d->stream, d->ev_k[slot], 0));
-    }
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
     int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
     if (rc != OVL_OK) return rc;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
-    if (via_hbm) {
-        HIPCHK(d, hipEventRecord(d->ev_sc[slot], d->stream));
-        hipStream_t cs = d->s_out;
-        if (d->k.pack_stage == 3) {
-            if (!d->s_hi) {
-                int lo = 0, hi = 0;
-                HIPCHK(d, hipDeviceGetStreamPriorityRange(&lo, &hi));
-                HIPCHK(d, hipStreamCreateWithPriority(&d->s_hi, hipStreamNonBlocking, hi));
-            }
-            cs = d->s_hi;
-        }
-        HIPCHK(d, hipStreamWaitEvent(cs, d->ev_sc[slot], 0));
-        if (d->k.pack_stage == 2)
-            HIPCHK(d, hipMemcpyAsync(d->st_out + so, pk, 2 * (size_t)n, hipMemcpyDeviceToHost, cs));
-        else
-            HIPCHK(d, ovl_launch_to_host(pk, d->st_out_dev + so, 2 * n, cs));
-        HIPCHK(d, hipEventRecord(d->ev_k[slot], cs));
-    } else if (staged_in || staged_out) {
-        HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
-    }
+    if (staged_in || staged_out) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
     if (C.pack && C.out_pinned && J.n_packed < J.nchunks && k == J.nchunks - 1)
         HIPCHK(d, hipEventRecord(d->ev_last, d->stream));
     return OVL_OK;
@@ -1535,8 +1496,7 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
 void quiesce(std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         (void)hipSetDevice(J.d->device);
-        for (hipStream_t s : {J.d->stream, J.d->s_in, J.d->s_out, J.d->s_hi})
-            if (s) (void)hipStreamSynchronize(s);
+        for (hipStream_t s : {J.d->stream, J.d->s_in, J.d->s_out}) (void)hipStreamSynchronize(s);
     }
 }
 
@@ -1618,10 +1578,6 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         if (J.nchunks == 0) continue;
         HIPCHK(c, hipSetDevice(J.d->device));
         HIPCHK(c, hipStreamSynchronize(C.direct ? J.d->stream : J.d->s_out));
-        if (C.direct && C.pack) {  // (the packed chunks' copies)
-            HIPCHK(c, hipStreamSynchronize(J.d->s_out));
-            if (J.d->s_hi) HIPCHK(c, hipStreamSynchronize(J.d->s_hi));
-        }
     }
     trace.mark('y', 0);
     double kms = 0.0;

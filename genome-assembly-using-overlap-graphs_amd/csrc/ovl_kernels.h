@@ -85,9 +85,6 @@ extern "C" hipError_t ovl_launch_dp(const OvlDpArgs* args, hipStream_t stream);
 // compact host pair lists (ovl_pairs.hip): dst[i] = src[i] from 2- or 4-byte elements (uint16 0xFFFF -> -1; src and
 // dst 16-byte aligned), and runs: dst[starts[r] .. starts[r + 1]) = vals[r]
 extern "C" hipError_t ovl_launch_widen(const void* src, int32_t width, int64_t n, int32_t* dst, hipStream_t stream);
-// ceil(bytes / 16) 16-byte pieces from device memory to host-mapped memory (both 16-byte aligned; the tail
-// piece is copied whole, so both buffers must extend to the next 16 bytes)
-extern "C" hipError_t ovl_launch_to_host(const void* src, void* dst, int64_t bytes, hipStream_t stream);
 extern "C" hipError_t ovl_launch_runs(const int32_t* vals, const int32_t* starts, int64_t n_runs, int32_t* dst,
                                       hipStream_t stream);
 extern "C" int ovl_band_diag_slots(int32_t band, int32_t lcap, int32_t* nseg_out);

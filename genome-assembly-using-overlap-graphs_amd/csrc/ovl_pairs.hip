@@ -71,28 +71,9 @@ __global__ __launch_bounds__(256) void runs_kernel(const int32_t* __restrict__ v
     }
 }
 
-// bytes [0, n16 * 16) from HBM to host-mapped memory, 16 bytes per lane-iteration, non-temporal both ways
-__global__ __launch_bounds__(256) void to_host_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + i);
-        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst) + i);
-    }
-}
-
 }  // namespace ovl
 
 using namespace ovl;
-
-extern "C" hipError_t ovl_launch_to_host(const void* src, void* dst, int64_t bytes, hipStream_t stream) {
-    if (bytes <= 0) return hipSuccess;
-    if ((reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(dst) & 15)) return hipErrorInvalidValue;
-    const int64_t n16 = (bytes + 15) / 16;
-    const unsigned blocks = (unsigned)std::min<int64_t>((n16 + 255) / 256, 256);
-    to_host_kernel<<<blocks, 256, 0, stream>>>(static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16);
-    return hipGetLastError();
-}
 
 extern "C" hipError_t ovl_launch_widen(const void* src, int32_t width, int64_t n, int32_t* dst, hipStream_t stream) {
     if (n <= 0) return hipSuccess;

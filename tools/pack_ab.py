@@ -14,10 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
 import numpy as np  # noqa: E402
 
-KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN", "OVL_PACK_STAGE")
+KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PACK_NT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
 SETTINGS = (("int32", {"OVL_PACK": "0"}),
-            ("packed_stage", {}),
-            ("packed_link", {"OVL_PACK_STAGE": "0"}))
+            ("packed_adaptive", {}),
+            ("packed_pct18", {"OVL_PACK_DIRECT_PCT": "18"}))
 if os.environ.get("PACK_AB_SETTINGS"):  # name=KNOB:value,KNOB:value;name=...
     SETTINGS = tuple((nm, dict(kv.split(":") for kv in spec.split(",") if kv))
                      for nm, spec in (x.split("=", 1) for x in os.environ["PACK_AB_SETTINGS"].split(";")))
