@@ -582,6 +582,12 @@ def kernel_name(w, sink: int, pairs: int) -> str:
     return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}>"
 
 
+# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed)
+LINK_BYTES_PER_PAIR = {0: 0, 1: 8, 2: 2}
+# a kernel's stores into pinned host memory, measured on the box (profiles/r02_pcie_write.txt)
+LINK_PEAK_GBS = 55.3
+
+
 def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
     """The kernels that run INSIDE the timed step, each launch timed with HIP events on its stream
     (ovl_set_timing / ovl_last_launches) over `reps` steps: per result sink, the median launch duration,
@@ -617,7 +623,10 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
         byts = int(np.median(d["bytes"]))
         launches = len(d["ms"]) / reps
         ach = byts / (ms * 1e-3) / 1e9
+        link = pairs * LINK_BYTES_PER_PAIR.get(sink, 0)
         table.append({"sink": sink, "what": SINKS.get(sink, "?"), "kernel": kernel_name(w, sink, pairs),
+                      "link_bytes_per_launch": link, "link_gbs": link / (ms * 1e-3) / 1e9,
+                      "link_frac": link / (ms * 1e-3) / 1e9 / LINK_PEAK_GBS,
                       "launches_per_step": launches, "launch_ms": ms, "launch_ms_all": ms_all,
                       "first_launch_ms": float(np.median(d["first"])) if d["first"] else None,
                       "pairs_per_launch": pairs, "algorithmic_bytes_per_launch": byts, "achieved_gbs": ach,
@@ -631,6 +640,11 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
             "pairs_per_launch": dom["pairs_per_launch"],
             "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
             "launches_per_step": dom["launches_per_step"],
+            "link": {"bound": "host link", "achieved": dom["link_gbs"], "peak": LINK_PEAK_GBS, "unit": "GB/s",
+                     "frac": dom["link_frac"], "bytes_per_launch": dom["link_bytes_per_launch"],
+                     "what": "result bytes the launch stores over the PCIe link into host memory / its duration; "
+                             "peak: a kernel storing two int32 arrays into pinned host memory "
+                             "(profiles/r02_pcie_write.txt)"},
             "what": "the step's dominant kernel (the one scoring most of the step's pairs, inside ms_per_step): "
                     "SURVEY §8d bytes of the pairs one launch scores / its median duration, HIP events on its "
                     "launch stream inside the timed step's own call (ovl_last_launches; launches queued behind "

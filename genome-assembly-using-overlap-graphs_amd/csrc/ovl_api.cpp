@@ -44,6 +44,7 @@
 #include <vector>
 
 #include "ovl.h"
+#include "ovl_encode.h"
 #include "ovl_expand.h"
 #include "ovl_kernels.h"
 
@@ -96,6 +97,8 @@ struct Knobs {
     int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
                                   // instead of the compact encoding (encode_chunk; A/B knob)
     int64_t compact_min = 1 << 16;  // OVL_PAIRS_COMPACT_MIN: compact encoding from this many pairs per call
+    int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
+                                  // instead of uniform_kernel reading b16 + tile deltas in place (A/B knob)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -182,8 +185,13 @@ struct Dev {
     char* cp_host = nullptr;
     char* cp_dev = nullptr;
     size_t cp_bytes = 0;
+    DevBuf cp_hbm;  // the in-place encoding's chunks copied into HBM (same layout as cp_host)
     std::vector<hipEvent_t> dec_ev;
     int64_t cp_link = 0;
+    // the next ungapped launch reads its pair list in the host encoding (OvlUngappedArgs::ix_*), or null
+    const uint16_t* ix_b16 = nullptr;
+    const uint8_t* ix_d8 = nullptr;
+    const int32_t* ix_base = nullptr;
 };
 
 // The host side of a read-set upload in one pinned block (grown on demand, kept by the context): offsets,
@@ -436,6 +444,23 @@ int ensure_heavy(Dev* c) {
     return OVL_OK;
 }
 
+// rs_log2 of an ungapped launch over n pairs: bit shifts split over 1 << rs_log2 lanes (the general kernel),
+// or (uniform kernel, 2 planes) latency mode when rs_log2 > 0
+int32_t ungapped_rs_log2(const Dev* c, int64_t n_pairs) {
+    int32_t rs_log2 = 0;
+    const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
+    while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
+    if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * 8) ? 1 : 0;
+    if (c->split_override >= 0) rs_log2 = c->split_override;  // OVL_SPLIT tuning knob
+    return rs_log2;
+}
+
+// An ungapped launch over n pairs runs uniform_kernel in throughput mode, the one that can read a
+// host-encoded pair list in place (uniform_kernel IX)
+bool ix_launch(const Dev* c, int64_t n_pairs) {
+    return c->planes == 2 && c->lmax > 0 && c->wmax >= 1 && c->wmax <= 8 && ungapped_rs_log2(c, n_pairs) == 0;
+}
+
 int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
                        int32_t match, int32_t mismatch, int64_t indel, int32_t* d_score, int32_t* d_end,
                        hipStream_t s) {
@@ -457,6 +482,8 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         if (rc != OVL_OK) return rc;
         seed_end = as<int32_t>(c->seed_e);
     }
+    if (c->ix_b16 && (pl.kernel != OVL_KERNEL_UNGAPPED || pl.key64 || !ix_launch(c, n_pairs)))
+        return fail(c, OVL_E_UNSUPPORTED, "host-encoded pair list on a launch that cannot read it");
     if (pl.kernel == OVL_KERNEL_UNGAPPED) {
         OvlUngappedArgs g{};
         g.sfx = as<uint32_t>(c->sfx);
@@ -471,12 +498,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         // general kernel: split a pair's bit shifts over 1, 2 or 4 lanes until the grid
         // has enough wavefronts.  Uniform kernel: latency mode (two wavefronts per tile,
         // side pairs beside the sweep) when there is about one tile per wavefront slot.
-        int32_t rs_log2 = 0;
-        const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
-        while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
-        if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * 8) ? 1 : 0;
-        if (c->split_override >= 0) rs_log2 = c->split_override;  // OVL_SPLIT tuning knob
-        g.rs_log2 = rs_log2;
+        g.rs_log2 = ungapped_rs_log2(c, n_pairs);
         // uniform-length fast path (2 bit planes): pairs of two reads of length lmax;
         // uniform_kernel scores the other pairs through its LDS side ring
         g.lw = c->planes == 2 ? c->lmax : 0;
@@ -491,9 +513,12 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
         g.host_out = c->out_mode;
+        g.ix_b16 = c->ix_b16;
+        g.ix_d8 = c->ix_d8;
+        g.ix_base = c->ix_base;
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
-        if (c->k.heavy_first && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
+        if (c->k.heavy_first && !g.ix_b16 && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
             d_a < ca + c->cand_n && d_b == as<int32_t>(c->cand_b) + (d_a - ca) && (d_a - ca) % 64 == 0) {
             int rc = ensure_heavy(c);
             if (rc != OVL_OK) return rc;
@@ -655,6 +680,7 @@ Knobs read_knobs() {
     }
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PAIRS_COMPACT_MIN")) k.compact_min = std::max(0LL, atoll(e));
+    if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -951,7 +977,7 @@ void destroy_dev(Dev* d) {
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
                       &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
                       &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
-                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids})
+                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids, &d->cp_hbm})
         release(*b);
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
@@ -1117,6 +1143,7 @@ struct Job {
     const int32_t* zb = nullptr;
     int32_t* d_score = nullptr;  // device results (local indexing)
     int32_t* d_end = nullptr;
+    std::vector<uint8_t> ixk;    // C.compact: chunk k's list is read in place by uniform_kernel (encode_chunk)
 };
 
 // Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
@@ -1168,6 +1195,7 @@ int setup_job(const Call& C, Job& J) {
             HIPCHK(d, hipHostGetDevicePointer((void**)&d->cp_dev, d->cp_host, 0));
             d->cp_bytes = need;
         }
+        if (d->k.pairs_ix) HIPCHK(d, ensure(d->cp_hbm, need));
         while ((int64_t)d->dec_ev.size() < J.nchunks) {
             hipEvent_t ev;
             HIPCHK(d, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1270,42 +1298,52 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
     const size_t base = (8 * (size_t)off + 32 * (size_t)k + 15) & ~size_t(15);
     char* hb = d->cp_host + base;                  // b area
     const size_t b_bytes = ((size_t)n * wd + 15) & ~size_t(15);
-    char* ha = hb + b_bytes;                       // a area: runs, or a like b
+    char* ha = hb + b_bytes;                       // a area: tile deltas + bases, runs, or a like b
     CopyPool& pool = CopyPool::get();
     const std::vector<size_t> parts = pool.cut((size_t)n, size_t(1) << 15);
+    static const ovl_encode::Fns enc = ovl_encode::pick(getenv("OVL_ENCODE_ISA"));
+    if (!enc.narrow) return fail(d, OVL_E_ARG, "OVL_ENCODE_ISA names an ISA this CPU does not run");
+    J.ixk.resize((size_t)J.nchunks, 0);
+    J.ixk[(size_t)k] = 0;
+    // In place (uniform_kernel IX): b as uint16 and a as tile deltas (d8[p] = a[p] - a[64t], bases int32),
+    // 3 bytes per pair and 4 per tile, copied into HBM by the copy engine on the second stream (large DMA
+    // reads; the kernel's own 64-byte reads through the host mapping ran at ~25 GB/s) while the previous
+    // chunk scores, and read by the scoring launch as they lie -- no decode launch.  Needs a-major tiles (a
+    // within 255 of its tile's first, every a in range; the parts are cut at multiples of 64) and a
+    // throughput-mode uniform launch; else the decode below.
+    if (wd == 2 && d->k.pairs_ix && C.plan->kernel == OVL_KERNEL_UNGAPPED && !C.plan->key64 && ix_launch(d, n)) {
+        uint8_t* d8 = reinterpret_cast<uint8_t*>(ha);
+        int32_t* tb = reinterpret_cast<int32_t*>(ha + (((size_t)n + 15) & ~size_t(15)));
+        std::vector<uint8_t> bad(parts.size(), 0);
+        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
+            enc.narrow(B, nr, reinterpret_cast<uint16_t*>(hb), lo, hi);
+            bad[i] = !enc.d8(A, nr, d8, tb, lo, hi);
+        });
+        if (std::find(bad.begin(), bad.end(), 1) == bad.end()) {
+            J.ixk[(size_t)k] = 1;
+            if (g_trace) g_trace->mark('e', k);
+            const size_t bytes = b_bytes + (((size_t)n + 15) & ~size_t(15)) + 4 * (size_t)((n + 63) / 64);
+            HIPCHK(d, hipSetDevice(d->device));
+            HIPCHK(d, hipMemcpyAsync(as<char>(d->cp_hbm) + base, hb, bytes, hipMemcpyHostToDevice, d->s_in));
+            HIPCHK(d, hipEventRecord(d->dec_ev[(size_t)k], d->s_in));
+            d->cp_link += 3 * (int64_t)n + 4 * ((n + 63) / 64);
+            return OVL_OK;
+        }
+    }
     // one pass: b, and the runs of a (a[i] != a[i - 1], and i == 0) into part-local lists, given up (kept
     // short) once a part has more than 1 run per 16 pairs -- then a crosses like b
     std::vector<std::vector<int32_t>> pv(parts.size()), ps(parts.size());
     std::vector<uint8_t> many(parts.size(), 0);
     pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
-        if (wd == 2) {
-            uint16_t* o = reinterpret_cast<uint16_t*>(hb);
-            for (size_t p = lo; p < hi; ++p) {
-                const int32_t v = B[p];
-                o[p] = (v >= 0 && v < nr) ? (uint16_t)v : (uint16_t)0xFFFF;
-            }
-        } else {
-            memcpy(reinterpret_cast<int32_t*>(hb) + lo, B + lo, sizeof(int32_t) * (hi - lo));
-        }
+        if (wd == 2) enc.narrow(B, nr, reinterpret_cast<uint16_t*>(hb), lo, hi);
+        else memcpy(reinterpret_cast<int32_t*>(hb) + lo, B + lo, sizeof(int32_t) * (hi - lo));
         // (thread-local lists, handed over at the end: the parts' vector objects share cache lines)
         const size_t cap = (hi - lo) / 16 + 1;
-        std::vector<int32_t> vv(cap), ss(cap);
-        int32_t* pvv = vv.data();
-        int32_t* pss = ss.data();
-        size_t r = 0;
-        int32_t prev = lo ? A[lo - 1] : (int32_t)~A[0];
-        for (size_t p = lo; p < hi; ++p) {
-            const int32_t v = A[p];
-            if (v != prev) {
-                if (r == cap) {
-                    many[i] = 1;
-                    break;
-                }
-                pvv[r] = v;
-                pss[r] = (int32_t)p;
-                ++r;
-            }
-            prev = v;
+        std::vector<int32_t> vv(cap + 1), ss(cap + 1);
+        size_t r = enc.runs(A, lo ? A[lo - 1] : (int32_t)~A[0], lo, hi, vv.data(), ss.data(), cap);
+        if (r > cap) {
+            many[i] = 1;
+            r = 0;
         }
         vv.resize(r);
         ss.resize(r);
@@ -1332,11 +1370,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
         // a like b (a second pass, for lists that are not a-major)
         pool.parallel_parts(parts, [&](size_t, size_t lo, size_t hi) {
             if (wd == 2) {
-                uint16_t* o = reinterpret_cast<uint16_t*>(ha);
-                for (size_t p = lo; p < hi; ++p) {
-                    const int32_t v = A[p];
-                    o[p] = (v >= 0 && v < nr) ? (uint16_t)v : (uint16_t)0xFFFF;
-                }
+                enc.narrow(A, nr, reinterpret_cast<uint16_t*>(ha), lo, hi);
             } else {
                 memcpy(reinterpret_cast<int32_t*>(ha) + lo, A + lo, sizeof(int32_t) * (hi - lo));
             }
@@ -1377,7 +1411,17 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     if (staged_in && k >= kSlots && !chunk_staged(C, J, k - kSlots)) HIPCHK(d, wait_event(d, d->ev_k[slot]));
     const int32_t* ka;
     const int32_t* kb;
-    if (C.compact) {
+    if (C.compact && J.ixk[(size_t)k]) {
+        // read in place by uniform_kernel from its HBM copy (encode_chunk's layout of chunk k)
+        HIPCHK(d, hipStreamWaitEvent(d->stream, d->dec_ev[(size_t)k], 0));
+        const size_t base = (8 * (size_t)off + 32 * (size_t)k + 15) & ~size_t(15);
+        const size_t b_bytes = ((size_t)n * 2 + 15) & ~size_t(15);
+        const char* hbm = as<char>(d->cp_hbm) + base;
+        d->ix_b16 = reinterpret_cast<const uint16_t*>(hbm);
+        d->ix_d8 = reinterpret_cast<const uint8_t*>(hbm + b_bytes);
+        d->ix_base = reinterpret_cast<const int32_t*>(hbm + b_bytes + (((size_t)n + 15) & ~size_t(15)));
+        ka = kb = nullptr;
+    } else if (C.compact) {
         // decoded into HBM by encode_chunk's kernels on the second stream
         HIPCHK(d, hipStreamWaitEvent(d->stream, d->dec_ev[(size_t)k], 0));
         ka = J.ka + off;
@@ -1401,6 +1445,9 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     d->out_mode = C.pack && k < J.n_packed ? 2 : 1;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
     int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
+    d->ix_b16 = nullptr;
+    d->ix_d8 = nullptr;
+    d->ix_base = nullptr;
     if (rc != OVL_OK) return rc;
     if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
     if (staged_in || staged_out) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));

@@ -631,14 +631,18 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
 // most that fits without spilling
 #define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : 4))) \
                                   : ((W) <= 4 ? 7 : ((W) <= 5 ? 6 : ((W) <= 6 ? 5 : 4))))
-template <int W, int KM, bool LAT, int OM>
+// IX: the pair list is read in its host encoding through the host mapping (b = ix_b16[p], 0xFFFF a bad
+// index; a = ix_base[tile] + ix_d8[p]): 3 bytes per pair plus 4 per tile cross the link inside the launch,
+// no decode launch before it (ovl_api.cpp encode_chunk).
+template <int W, int KM, bool LAT, int OM, bool IX = false>
 __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, const int32_t* __restrict__ a_idx, const int32_t* __restrict__ b_idx, int64_t n_pairs,
     int32_t lw, const uint32_t* __restrict__ full, int32_t match, int32_t mismatch,
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag,
     const int32_t* __restrict__ heavy_ids, const uint8_t* __restrict__ tile_flags, int32_t heavy_n,
-    int64_t tile_base) {
+    int64_t tile_base, const uint16_t* __restrict__ ix_b16, const uint8_t* __restrict__ ix_d8,
+    const int32_t* __restrict__ ix_base) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
@@ -704,8 +708,17 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         }
         const int64_t p = tile * 64 + lane;
         const bool mine = item < n_items && tile < n_tiles && p < n_pairs;
-        int32_t a = mine ? a_idx[p] : 0;
-        int32_t b = mine ? b_idx[p] : 0;
+        int32_t a = 0, b = 0;
+        if constexpr (IX) {
+            if (mine) {
+                const uint32_t bv = ix_b16[p];
+                b = bv == 0xFFFFu ? -1 : (int32_t)bv;
+                a = ix_base[tile] + (int32_t)ix_d8[p];
+            }
+        } else {
+            a = mine ? a_idx[p] : 0;
+            b = mine ? b_idx[p] : 0;
+        }
         const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
         if (!ok) { a = 0; b = 0; }
         if (LAT && role == 1) {
@@ -1341,16 +1354,29 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
     return hipGetLastError();
 }
 
-template <int W, int KM, bool LAT, int OM>
+template <int W, int KM, bool LAT, int OM, bool IX = false>
 static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
-    uniform_kernel<W, KM, LAT, OM><<<blocks, 256, 0, stream>>>(g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx,
-                                                                g.n_pairs, g.lw, g.full, g.match, g.mismatch,
-                                                                g.out_score, g.out_end, g.err_flag, g.heavy_ids,
-                                                                g.tile_flags, g.heavy_n, g.tile_base);
+    uniform_kernel<W, KM, LAT, OM, IX><<<blocks, 256, 0, stream>>>(
+        g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full, g.match, g.mismatch, g.out_score,
+        g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
 }
 
 template <int W, int KM, bool LAT>
 static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    if (g.ix_b16) {
+        // host-encoded pair lists: throughput mode, int32 keys, host-mapped results (the compact one-shot path)
+        if constexpr (!LAT && KM == 0) {
+            if (g.host_out == 1) {
+                launch_uniform_4<W, KM, LAT, 1, true>(g, blocks, stream);
+                return true;
+            }
+            if (g.host_out == 2) {
+                launch_uniform_4<W, KM, LAT, 2, true>(g, blocks, stream);
+                return true;
+            }
+        }
+        return false;
+    }
     switch (g.host_out) {
         case 0: launch_uniform_4<W, KM, LAT, 0>(g, blocks, stream); return true;
         case 1: launch_uniform_4<W, KM, LAT, 1>(g, blocks, stream); return true;
@@ -1460,6 +1486,8 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->host_out >= 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
+    if (g->ix_b16 && (g->lw <= 0 || g->key64 || g->rs_log2 > 0 || g->heavy_ids || !g->ix_d8 || !g->ix_base))
+        return hipErrorInvalidValue;  // host-encoded lists: uniform throughput mode only
     if (g->lw > 0) {
         // rs_log2 > 0 here selects the latency mode
         const unsigned nb = grid_for((g->n_pairs << (g->rs_log2 > 0 ? 1 : 0)) +

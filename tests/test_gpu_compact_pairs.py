@@ -1,10 +1,12 @@
 """GPU: host pair lists in compact form (ovl_pairs.hip, ovl_api.cpp encode_chunk).
 
 ovl_score_host / ovl_score_pairs encode the caller's int32 pairs per pipeline chunk -- b as uint16 when
-n_reads <= 65,535, a as runs when the list is a-major (overlapGraphs.py:43-52) -- and kernels decode them into
-HBM.  Every result is compared with the oracle and with the uncompressed path (OVL_PAIRS_COMPACT=0): a-major
-and shuffled lists (runs / no runs), uint16 and int32 widths, pinned and pageable lists, odd chunk sizes, and
-bad indices (OVL_E_INDEX, -1 results, the rest exact).
+n_reads <= 65,535; a, when the list is a-major (overlapGraphs.py:43-52), as tile deltas that uniform_kernel
+reads in place (IX: a = base[p / 64] + d8[p]) or as runs that kernels decode into HBM.  Every result is
+compared with the oracle and with the uncompressed path (OVL_PAIRS_COMPACT=0): a-major and shuffled lists
+(in place / runs / no runs), uint16 and int32 widths, pinned and pageable lists, odd chunk sizes, tiles whose
+a jumps past the delta range, calls small enough for the latency-mode launch, and bad indices (OVL_E_INDEX,
+-1 results, the rest exact).
 """
 import os
 
@@ -162,3 +164,108 @@ def test_compact_adaptive_share(oracle_mod, target):
             np.testing.assert_array_equal(out[1], ref_e)
             shares.append(eng.last_transfer()["packed_pairs"] / n)
         assert all(0.19 <= x <= 0.99 for x in shares), shares
+
+
+def _pair_link_bytes(eng, n):
+    """Bytes of the pair list that crossed the link in the last call (results subtracted: 2 B per packed
+    pair, 8 B per int32 pair)."""
+    t = eng.last_transfer()
+    return t["link_bytes"] - 2 * t["packed_pairs"] - 8 * (n - t["packed_pairs"])
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_ix_in_place_vs_decode(oracle_mod, target, pinned):
+    """The a-major target list is read in place (3 B per pair + 4 B per tile); OVL_PAIRS_IX=0 decodes the
+    same encoding's runs into HBM first.  Same results, each path visible in its link bytes."""
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = target
+    n = a.shape[0]
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+    if pinned:
+        pa, pb = pinned_empty(n), pinned_empty(n)
+        pa[:], pb[:] = a, b
+        a, b = pa, pb
+    ix = _engine_env({})
+    dec = _engine_env({"OVL_PAIRS_IX": "0"})
+    try:
+        for e in (ix, dec):
+            e.set_reads(reads)
+        for _ in range(3):
+            s, en = ix.score(a, b)
+            np.testing.assert_array_equal(s, ref_s)
+            np.testing.assert_array_equal(en, ref_e)
+            lb = _pair_link_bytes(ix, n)
+            assert 3 * n + 4 * (n // 64) <= lb <= 3 * n + 4 * (n // 64 + 64), lb
+        s, en = dec.score(a, b)
+        np.testing.assert_array_equal(s, ref_s)
+        np.testing.assert_array_equal(en, ref_e)
+        assert _pair_link_bytes(dec, n) < 3 * n  # b16 + runs
+    finally:
+        ix.close()
+        dec.close()
+
+
+def test_ix_tile_jumps_fall_back(oracle_mod, target):
+    """An a-major list whose a jumps by more than 255 inside some tiles: those chunks take the runs decode,
+    the others stay in place; exact either way."""
+    reads, _, _ = target
+    nr = len(reads)
+    rng = np.random.default_rng(5)
+    n = 1_200_000
+    # a non-decreasing over [0, nr) with runs of ~40, plus a few jumps of 300-2000 inside tiles
+    steps = (rng.random(n) < 1 / 40).astype(np.int64)
+    jump_at = rng.choice(n, 6, replace=False)
+    steps[jump_at] = rng.integers(300, 2000, 6)
+    a = np.cumsum(steps)
+    a = (a * (nr - 1) // max(int(a[-1]), 1)).astype(np.int32)
+    b = rng.integers(0, nr, n, dtype=np.int32)
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+    eng = _engine_env({})
+    try:
+        eng.set_reads(reads)
+        s, e = eng.score(a, b)
+        np.testing.assert_array_equal(s, ref_s)
+        np.testing.assert_array_equal(e, ref_e)
+        assert _pair_link_bytes(eng, n) < 3 * n + 4 * (n // 64)  # some chunks took the runs
+    finally:
+        eng.close()
+
+
+def test_ix_small_call_latency_mode(oracle_mod, target):
+    """100 K pairs (compact, but few enough for the latency-mode launch, which takes the decoded list)."""
+    reads, a, b = target
+    a, b = a[:100_000], b[:100_000]
+    ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
+    eng = _engine_env({})
+    try:
+        eng.set_reads(reads)
+        s, e = eng.score(a, b)
+        np.testing.assert_array_equal(s, ref_s)
+        np.testing.assert_array_equal(e, ref_e)
+        assert _pair_link_bytes(eng, a.shape[0]) < 3 * a.shape[0]
+    finally:
+        eng.close()
+
+
+def test_ix_cfg3_width5(oracle_mod):
+    """cfg3 (l = 150, W = 5 words per row) through the in-place list: equal to the resident-list scoring and
+    to the oracle on a sample."""
+    from ovlgraph import OverlapEngine
+    from ovlgraph.candidates import dedup_reads
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("cfg3", seed=0))
+    with OverlapEngine(0) as eng:
+        eng.set_reads(reads)
+        a, b = eng.candidates(5)
+        a, b = np.array(a), np.array(b)
+        n = a.shape[0]
+        s, e = eng.score(a, b)
+        lb = _pair_link_bytes(eng, n)
+        assert 3 * n + 4 * (n // 64) <= lb <= 3 * n + 4 * (n // 64 + 64), lb
+        cs, ce = eng.score_candidates()
+        np.testing.assert_array_equal(s, cs)
+        np.testing.assert_array_equal(e, ce)
+        idx = np.linspace(0, n - 1, 150_000).astype(np.int64)
+        rs, re_ = oracle_mod.batch_closed_form(reads, a[idx], b[idx])
+        np.testing.assert_array_equal(s[idx], rs)
+        np.testing.assert_array_equal(e[idx], re_)
