@@ -832,11 +832,14 @@ class CopyPool {
         b.push_back(n);
         return b;
     }
-    // f(i, lo, hi) for every part i of `b` (from cut), on the workers and the calling thread (part 0)
-    void parallel_parts(const std::vector<size_t>& b, const std::function<void(size_t, size_t, size_t)>& f) {
+    // f(i, lo, hi) for every part i of `b` (from cut), on the workers and the calling thread (part 0); `pre`,
+    // when given, runs on the calling thread once the workers have their parts, before its own
+    void parallel_parts(const std::vector<size_t>& b, const std::function<void(size_t, size_t, size_t)>& f,
+                        const std::function<void()>& pre = nullptr) {
         spin_us_.store(CpuShare::get().sharers() > 1 ? 0 : spin_cfg_, std::memory_order_relaxed);
         const size_t parts = b.size() - 1;
         if (parts <= 1) {
+            if (pre) pre();
             f(0, b[0], b[parts]);
             return;
         }
@@ -851,6 +854,7 @@ class CopyPool {
             queued_.store(tasks_.size(), std::memory_order_release);
         }
         cv_.notify_all();
+        if (pre) pre();
         f(0, b[0], b[1]);
         // the batch's end: polled for a while (the workers finish within microseconds of the caller), then
         // a blocking wait
@@ -1286,8 +1290,19 @@ thread_local PipeTrace* g_trace = nullptr;
 //   a: runs (value, chunk-relative start; starts[R] = n) when 8 R + 4 < n * width -- the candidate lists of
 //      overlapGraphs.py:43-52 are a-major, ~55 pairs per run at the target point --, else like b.
 // At the target point 4.3 MB cross the link instead of 16 MB.
-int encode_chunk(const Call& C, Job& J, int64_t k) {
+int issue_chunk(const Call& C, Job& J, int64_t k);
+
+// `pre` (the previous chunk's issue, when given) runs on the calling thread while the pool encodes
+int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& pre = nullptr) {
     Dev* d = J.d;
+    int pre_rc = OVL_OK;
+    bool pre_done = !pre;
+    const std::function<void()> run_pre = [&] {
+        if (!pre_done) {
+            pre_done = true;
+            pre_rc = pre();
+        }
+    };
     const int64_t off = J.cb[(size_t)k];
     const int64_t n = J.cb[(size_t)k + 1] - off;
     const int64_t g = J.lo + off;
@@ -1315,17 +1330,17 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
         uint8_t* d8 = reinterpret_cast<uint8_t*>(ha);
         int32_t* tb = reinterpret_cast<int32_t*>(ha + (((size_t)n + 15) & ~size_t(15)));
         std::vector<uint8_t> bad(parts.size(), 0);
-        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
-            enc.narrow(B, nr, reinterpret_cast<uint16_t*>(hb), lo, hi);
-            bad[i] = !enc.d8(A, nr, d8, tb, lo, hi);
-        });
+        pool.parallel_parts(
+            parts,
+            [&](size_t i, size_t lo, size_t hi) {
+                enc.narrow(B, nr, reinterpret_cast<uint16_t*>(hb), lo, hi);
+                bad[i] = !enc.d8(A, nr, d8, tb, lo, hi);
+            },
+            run_pre);
+        if (pre_rc != OVL_OK) return pre_rc;
         if (std::find(bad.begin(), bad.end(), 1) == bad.end()) {
-            J.ixk[(size_t)k] = 1;
+            J.ixk[(size_t)k] = 1;  // (issue_chunk_direct copies the chunk into HBM and launches on it)
             if (g_trace) g_trace->mark('e', k);
-            const size_t bytes = b_bytes + (((size_t)n + 15) & ~size_t(15)) + 4 * (size_t)((n + 63) / 64);
-            HIPCHK(d, hipSetDevice(d->device));
-            HIPCHK(d, hipMemcpyAsync(as<char>(d->cp_hbm) + base, hb, bytes, hipMemcpyHostToDevice, d->s_in));
-            HIPCHK(d, hipEventRecord(d->dec_ev[(size_t)k], d->s_in));
             d->cp_link += 3 * (int64_t)n + 4 * ((n + 63) / 64);
             return OVL_OK;
         }
@@ -1349,7 +1364,8 @@ int encode_chunk(const Call& C, Job& J, int64_t k) {
         ss.resize(r);
         pv[i] = std::move(vv);
         ps[i] = std::move(ss);
-    });
+    }, run_pre);
+    if (pre_rc != OVL_OK) return pre_rc;
     int64_t R = 0;
     bool runs = n < (int64_t(1) << 31);
     for (size_t i = 0; i + 1 < parts.size(); ++i) {
@@ -1412,10 +1428,15 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     const int32_t* ka;
     const int32_t* kb;
     if (C.compact && J.ixk[(size_t)k]) {
-        // read in place by uniform_kernel from its HBM copy (encode_chunk's layout of chunk k)
-        HIPCHK(d, hipStreamWaitEvent(d->stream, d->dec_ev[(size_t)k], 0));
+        // read in place by uniform_kernel from its HBM copy (encode_chunk's layout of chunk k), copied by the
+        // copy engine on the second stream
         const size_t base = (8 * (size_t)off + 32 * (size_t)k + 15) & ~size_t(15);
         const size_t b_bytes = ((size_t)n * 2 + 15) & ~size_t(15);
+        const size_t bytes = b_bytes + (((size_t)n + 15) & ~size_t(15)) + 4 * (size_t)((n + 63) / 64);
+        HIPCHK(d, hipMemcpyAsync(as<char>(d->cp_hbm) + base, d->cp_host + base, bytes, hipMemcpyHostToDevice,
+                                 d->s_in));
+        HIPCHK(d, hipEventRecord(d->dec_ev[(size_t)k], d->s_in));
+        HIPCHK(d, hipStreamWaitEvent(d->stream, d->dec_ev[(size_t)k], 0));
         const char* hbm = as<char>(d->cp_hbm) + base;
         d->ix_b16 = reinterpret_cast<const uint16_t*>(hbm);
         d->ix_d8 = reinterpret_cast<const uint8_t*>(hbm + b_bytes);
@@ -1586,10 +1607,16 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
-            if ((rc = issue_chunk(C, J, k)) != OVL_OK) break;
-            trace.mark('i', k);
-            // the next chunk's encoding (host) while this one decodes and scores
-            if (C.compact && k + 1 < J.nchunks && (rc = encode_chunk(C, J, k + 1)) != OVL_OK) break;
+            const auto issue = [&]() -> int {
+                const int r = issue_chunk(C, J, k);
+                trace.mark('i', k);
+                return r;
+            };
+            // compact lists: this chunk is issued (copy, launch) by the calling thread while the pool encodes
+            // the next one, then the next chunk decodes / copies and scores while the one after is encoded
+            if (C.compact && k + 1 < J.nchunks) rc = encode_chunk(C, J, k + 1, issue);
+            else rc = issue();
+            if (rc != OVL_OK) break;
             const int64_t j = k - (kSlots - 1);
             if (j >= 0 && chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
         }

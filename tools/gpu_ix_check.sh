@@ -8,7 +8,7 @@ mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_compact_pairs.py -x -v --timeout 200 --timeout-method thread \
   > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -40 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
-OVL_TRACE_PIPE=1 timeout -k 10 240 rocprofv3 --kernel-trace -d $OUT/prof -o tl -- python3 tools/host_list_timeline.py target 10 \
+OVL_TRACE_PIPE=1 timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace -d $OUT/prof -o tl -- python3 tools/host_list_timeline.py target 10 \
   > $OUT/tl_out.txt 2> $OUT/tl_trace.txt || { echo "timeline failed"; tail -20 $OUT/tl_trace.txt; exit 1; }
 cat $OUT/tl_out.txt
 for r in 1 2; do

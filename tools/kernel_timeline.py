@@ -12,6 +12,15 @@ def main():
     last = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, start, end, stream_id from kernels order by start"))
+    try:  # memory copies too, when traced (--memory-copy-trace)
+        cols = [r[1] for r in c.execute("pragma table_info(memory_copies)")]
+        if cols:
+            nm = "name" if "name" in cols else cols[0]
+            rows += [("copy " + str(r[0]) + " " + str(r[3]) + " B", r[1], r[2], -1)
+                     for r in c.execute(f"select {nm}, start, end, size from memory_copies")]
+            rows.sort(key=lambda r: r[1])
+    except sqlite3.Error:
+        pass
     groups, cur, end = [], [], None
     for r in rows:
         if end is not None and r[1] - end > 1_000_000:
