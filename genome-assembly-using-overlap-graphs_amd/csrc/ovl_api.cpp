@@ -45,6 +45,7 @@
 
 #include "ovl.h"
 #include "ovl_encode.h"
+#include "ovl_scan.h"
 #include "ovl_expand.h"
 #include "ovl_kernels.h"
 
@@ -199,7 +200,7 @@ struct Dev {
 struct ReadStage {
     char* p = nullptr;
     size_t bytes = 0;
-    size_t o_off = 0, o_len = 0, o_full = 0, o_lut = 0, o_raw = 0;
+    size_t o_off = 0, o_len = 0, o_full = 0, o_lut = 0, o_raw = 0, o_pk = 0;
 };
 
 // The host-side facts of a read set (prep_reads); kept by the context so that its arrays are reused, without
@@ -211,6 +212,7 @@ struct HostReads {
     uint8_t lut[256];
     const uint8_t* src = nullptr;  // the caller's bytes, then (stage_reads) their pinned copy
     int64_t total = 0;
+    bool packed2 = false;          // every byte is A, C, G or T: the stage holds them 2-bit packed (o_pk)
     int32_t n_reads = 0, lmax = 0, planes = 2, wmax = 0, srow = 0, trow = 0;
 };
 
@@ -1910,110 +1912,92 @@ OVL_API int ovl_last_timing(const ovl_ctx* c, double* kernel_ms, double* call_ms
 
 namespace {
 
-// seen[v] = 1 for every byte value v in p[0 .. n).  Reads are DNA: 64-byte blocks made of A, C, G and T only
-// are settled with four compares (AVX-512BW; AVX2 on 32-byte blocks), other blocks byte by byte.
-void scan_bytes(const uint8_t* p, size_t n, uint8_t* seen) {
-    uint8_t t[4][256] = {};  // four tables: independent stores
-    size_t q = 0;
-    for (; q + 4 <= n; q += 4) {
-        t[0][p[q]] = 1;
-        t[1][p[q + 1]] = 1;
-        t[2][p[q + 2]] = 1;
-        t[3][p[q + 3]] = 1;
-    }
-    for (; q < n; ++q) t[0][p[q]] = 1;
-    for (int v = 0; v < 256; ++v) seen[v] |= t[0][v] | t[1][v] | t[2][v] | t[3][v];
-}
-
-__attribute__((target("avx512f,avx512bw"))) void scan_symbols_avx512(const uint8_t* p, size_t n, uint8_t* seen) {
-    const __m512i A = _mm512_set1_epi8('A'), C = _mm512_set1_epi8('C'), G = _mm512_set1_epi8('G'),
-                  T = _mm512_set1_epi8('T');
-    __mmask64 ma = 0, mc = 0, mg = 0, mt = 0;
-    size_t q = 0;
-    for (; q + 64 <= n; q += 64) {
-        const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(p + q));
-        const __mmask64 a = _mm512_cmpeq_epi8_mask(v, A), c = _mm512_cmpeq_epi8_mask(v, C),
-                        g = _mm512_cmpeq_epi8_mask(v, G), t = _mm512_cmpeq_epi8_mask(v, T);
-        if ((a | c | g | t) != ~__mmask64(0)) {
-            scan_bytes(p + q, 64, seen);
-            continue;
-        }
-        ma |= a;
-        mc |= c;
-        mg |= g;
-        mt |= t;
-    }
-    scan_bytes(p + q, n - q, seen);
-    seen['A'] |= ma != 0;
-    seen['C'] |= mc != 0;
-    seen['G'] |= mg != 0;
-    seen['T'] |= mt != 0;
-}
-
-__attribute__((target("avx2"))) void scan_symbols_avx2(const uint8_t* p, size_t n, uint8_t* seen) {
-    const __m256i A = _mm256_set1_epi8('A'), C = _mm256_set1_epi8('C'), G = _mm256_set1_epi8('G'),
-                  T = _mm256_set1_epi8('T');
-    uint32_t ma = 0, mc = 0, mg = 0, mt = 0;
-    size_t q = 0;
-    for (; q + 32 <= n; q += 32) {
-        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + q));
-        const uint32_t a = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, A));
-        const uint32_t c = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, C));
-        const uint32_t g = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, G));
-        const uint32_t t = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, T));
-        if ((a | c | g | t) != 0xFFFFFFFFu) {
-            scan_bytes(p + q, 32, seen);
-            continue;
-        }
-        ma |= a;
-        mc |= c;
-        mg |= g;
-        mt |= t;
-    }
-    scan_bytes(p + q, n - q, seen);
-    seen['A'] |= ma != 0;
-    seen['C'] |= mc != 0;
-    seen['G'] |= mg != 0;
-    seen['T'] |= mt != 0;
-}
-
-void scan_symbols(const uint8_t* p, size_t n, uint8_t* seen) {
-    static const int isa = __builtin_cpu_supports("avx512bw") ? 2 : (__builtin_cpu_supports("avx2") ? 1 : 0);
-    if (isa == 2) scan_symbols_avx512(p, n, seen);
-    else if (isa == 1) scan_symbols_avx2(p, n, seen);
-    else scan_bytes(p, n, seen);
-}
-
+// Offsets, lengths, the length bitmap and the longest read (split over the host pool for large read sets).
 int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads, HostReads& h) {
     const int64_t base = n_reads > 0 ? offsets[0] : 0;
     if (base < 0) return fail(c, OVL_E_ARG, "offsets[0] < 0");
     h.n_reads = n_reads;
-    h.off.assign((size_t)n_reads + 1, 0);
-    h.len.assign((size_t)std::max(n_reads, 1), 0);
-    for (int32_t r = 0; r < n_reads; ++r) {
-        const int64_t l = offsets[r + 1] - offsets[r];
-        if (l < 0) return fail(c, OVL_E_ARG, "offsets not non-decreasing at read %d", r);
-        if (l > INT32_MAX / 2) return fail(c, OVL_E_UNSUPPORTED, "read %d is too long", r);
-        h.off[(size_t)r + 1] = offsets[r + 1] - base;
-        h.len[(size_t)r] = (int32_t)l;
-        h.lmax = std::max(h.lmax, (int32_t)l);
+    h.off.resize((size_t)n_reads + 1);
+    h.len.resize((size_t)std::max(n_reads, 1));
+    h.off[0] = 0;
+    h.len[0] = 0;
+    CopyPool& pool = CopyPool::get();
+    // parts of whole 32-read words (the bitmap), each with its longest read and first bad read
+    const std::vector<size_t> parts = pool.cut((size_t)n_reads, size_t(1) << 14);
+    std::vector<int32_t> pmax(parts.size(), 0), pbad(parts.size(), -1), ptoo(parts.size(), -1);
+    pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
+        int32_t m = 0;
+        for (size_t r = lo; r < hi; ++r) {
+            const int64_t l = offsets[r + 1] - offsets[r];
+            if (l < 0 || l > INT32_MAX / 2) {
+                (l < 0 ? pbad[i] : ptoo[i]) = (int32_t)r;
+                return;
+            }
+            h.off[r + 1] = offsets[r + 1] - base;
+            h.len[r] = (int32_t)l;
+            m = std::max(m, (int32_t)l);
+        }
+        pmax[i] = m;
+    });
+    h.lmax = 0;
+    for (size_t i = 0; i < parts.size(); ++i) {
+        if (pbad[i] >= 0) return fail(c, OVL_E_ARG, "offsets not non-decreasing at read %d", pbad[i]);
+        if (ptoo[i] >= 0) return fail(c, OVL_E_UNSUPPORTED, "read %d is too long", ptoo[i]);
+        h.lmax = std::max(h.lmax, pmax[i]);
     }
     h.total = n_reads > 0 ? h.off[(size_t)n_reads] : 0;
     h.full.assign(((size_t)std::max(n_reads, 1) + 31) / 32, 0u);
-    for (int32_t r = 0; r < n_reads; ++r)
-        if (h.len[(size_t)r] == h.lmax) h.full[(size_t)r >> 5] |= 1u << (r & 31);
+    pool.parallel_parts(parts, [&](size_t, size_t lo, size_t hi) {
+        for (size_t r = lo; r < hi; ++r)
+            if (h.len[r] == h.lmax) h.full[r >> 5] |= 1u << (r & 31);  // (parts cut at multiples of 64 reads)
+    });
     if (h.total > 0 && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
-    // alphabet: dense codes in byte order (equality-preserving); the bytes seen, split over the host pool
-    bool present[256] = {false};
     h.src = seqs ? seqs + base : nullptr;
+    return OVL_OK;
+}
+
+// The pinned upload stage: offsets, lengths, bitmap and code table, and the read bytes -- 2-bit packed by the
+// host pool in the same pass that scans them for the alphabet when every byte is A, C, G or T (a quarter of
+// the bytes to upload, expanded by unpack2_kernel), else copied as they are.  Sets the code table and the
+// bit-plane layout (dense codes in byte order, equality-preserving).
+int stage_reads(ovl_ctx* c, ReadStage& st, HostReads& h) {
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    st.o_off = 0;
+    st.o_len = al(st.o_off + sizeof(int64_t) * h.off.size());
+    st.o_full = al(st.o_len + sizeof(int32_t) * h.len.size());
+    st.o_lut = al(st.o_full + sizeof(uint32_t) * h.full.size());
+    st.o_pk = al(st.o_lut + 256);
+    st.o_raw = al(st.o_pk + (size_t)h.total / 4 + 64);
+    const size_t need = al(st.o_raw + (size_t)h.total + 1);
+    if (st.bytes < need) {
+        if (st.p) (void)hipHostFree(st.p);
+        st.p = nullptr;
+        st.bytes = 0;
+        HIPCHK(c, hipHostMalloc((void**)&st.p, need, hipHostMallocPortable));
+        st.bytes = need;
+    }
+    bool present[256] = {false};
+    h.packed2 = false;
     if (h.total > 0) {
         CopyPool& pool = CopyPool::get();
-        const std::vector<size_t> parts = pool.cut((size_t)h.total, size_t(1) << 18);
+        const std::vector<size_t> parts = pool.cut((size_t)h.total, size_t(1) << 18);  // (multiples of 64)
         std::vector<std::array<uint8_t, 256>> seen(parts.size(), std::array<uint8_t, 256>{});
+        std::vector<uint8_t> ok(parts.size() - 1, 0);  // (cut gives parts + 1 bounds)
         const uint8_t* src = h.src;
-        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) { scan_symbols(src + lo, hi - lo, seen[i].data()); });
+        uint8_t* pk = reinterpret_cast<uint8_t*>(st.p + st.o_pk);
+        // OVL_READS_PACK2=0 (A/B knob): the bytes are uploaded as they are
+        static const bool pack2 = !(getenv("OVL_READS_PACK2") && atoi(getenv("OVL_READS_PACK2")) == 0);
+        pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
+            if (pack2) {
+                ok[i] = ovl_scan::scan_pack(src, lo, hi, seen[i].data(), pk);
+            } else {
+                ovl_scan::scan_bytes(src + lo, hi - lo, seen[i].data());
+            }
+        });
         for (const auto& t : seen)
             for (int v = 0; v < 256; ++v) present[v] = present[v] || t[(size_t)v];
+        h.packed2 = std::find(ok.begin(), ok.end(), 0) == ok.end();
+        if (!h.packed2) host_copy(st.p + st.o_raw, h.src, (size_t)h.total);
     }
     memset(h.lut, 0, sizeof(h.lut));
     int k = 0;
@@ -2025,32 +2009,11 @@ int prep_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t 
     if (h.lmax <= kFastMaxLen) h.wmax = std::max(1, (h.lmax + 31) / 32);
     h.srow = h.wmax ? ((h.wmax * h.planes + 3) & ~3) : 0;
     h.trow = h.srow;
-    return OVL_OK;
-}
-
-// Fill the pinned upload stage (the bytes copied in by the host pool), so the uploads are DMA from pinned
-// memory instead of the runtime's staging of pageable memory.
-int stage_reads(ovl_ctx* c, ReadStage& st, HostReads& h) {
-    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    st.o_off = 0;
-    st.o_len = al(st.o_off + sizeof(int64_t) * h.off.size());
-    st.o_full = al(st.o_len + sizeof(int32_t) * h.len.size());
-    st.o_lut = al(st.o_full + sizeof(uint32_t) * h.full.size());
-    st.o_raw = al(st.o_lut + 256);
-    const size_t need = al(st.o_raw + (size_t)h.total + 1);
-    if (st.bytes < need) {
-        if (st.p) (void)hipHostFree(st.p);
-        st.p = nullptr;
-        st.bytes = 0;
-        HIPCHK(c, hipHostMalloc((void**)&st.p, need, hipHostMallocPortable));
-        st.bytes = need;
-    }
     memcpy(st.p + st.o_off, h.off.data(), sizeof(int64_t) * h.off.size());
     memcpy(st.p + st.o_len, h.len.data(), sizeof(int32_t) * h.len.size());
     memcpy(st.p + st.o_full, h.full.data(), sizeof(uint32_t) * h.full.size());
     memcpy(st.p + st.o_lut, h.lut, 256);
-    if (h.total > 0) host_copy(st.p + st.o_raw, h.src, (size_t)h.total);
-    h.src = reinterpret_cast<const uint8_t*>(st.p + st.o_raw);
+    h.src = reinterpret_cast<const uint8_t*>(st.p + (h.packed2 ? st.o_pk : st.o_raw));
     return OVL_OK;
 }
 
@@ -2066,7 +2029,7 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
     if ((e = ensure(d->len, sizeof(int32_t) * h.len.size())) != hipSuccess) return e;
     if ((e = ensure(d->codes, (size_t)h.total + 64)) != hipSuccess) return e;  // tail pad: clamped reads
     if ((e = ensure(d->lut, 256)) != hipSuccess) return e;
-    if ((e = ensure(d->raw, (size_t)h.total)) != hipSuccess) return e;
+    if ((e = ensure(d->raw, (size_t)h.total + 64)) != hipSuccess) return e;
     if ((e = ensure(d->full, sizeof(uint32_t) * h.full.size())) != hipSuccess) return e;
     hipStream_t s = d->stream;
     if ((e = hipMemcpyAsync(d->off.p, st.p + st.o_off, sizeof(int64_t) * h.off.size(), hipMemcpyHostToDevice, s)))
@@ -2076,7 +2039,13 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
     if ((e = hipMemcpyAsync(d->lut.p, st.p + st.o_lut, 256, hipMemcpyHostToDevice, s))) return e;
     if ((e = hipMemcpyAsync(d->full.p, st.p + st.o_full, sizeof(uint32_t) * h.full.size(), hipMemcpyHostToDevice, s)))
         return e;
-    if (h.total > 0) {
+    if (h.total > 0 && h.packed2) {
+        // 2-bit packed bytes (stage_reads), read by unpack2_kernel in 16-byte groups
+        const size_t pk_bytes = (((size_t)h.total + 63) / 64) * 16;
+        if ((e = hipMemcpyAsync(d->raw.p, h.src, pk_bytes, hipMemcpyHostToDevice, s))) return e;
+        if ((e = ovl_launch_unpack2(as<uint8_t>(d->raw), as<uint8_t>(d->lut), as<uint8_t>(d->codes), h.total, s)))
+            return e;
+    } else if (h.total > 0) {
         if ((e = hipMemcpyAsync(d->raw.p, h.src, (size_t)h.total, hipMemcpyHostToDevice, s))) return e;
         if ((e = ovl_launch_map_codes(as<uint8_t>(d->raw), as<uint8_t>(d->lut), as<uint8_t>(d->codes), h.total, s)))
             return e;

@@ -74,6 +74,10 @@ struct OvlDpArgs {
     int32_t classic;     // full DP without traceback: use dp_kernel instead of dp_fast_kernel (tests)
 };
 
+// 2-bit packed ACGT bytes (base i at bits 2(i % 4) of byte i / 4; pk 16-byte aligned, readable up to the next
+// 16-byte boundary) -> codes[i] = lut["ACGT"[code]]
+extern "C" hipError_t ovl_launch_unpack2(const uint8_t* pk, const uint8_t* lut, uint8_t* codes, int64_t n,
+                                         hipStream_t stream);
 extern "C" hipError_t ovl_launch_map_codes(const uint8_t* raw, const uint8_t* lut, uint8_t* codes, int64_t n,
                                            hipStream_t stream);
 extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const int64_t* off, const int32_t* len,

@@ -113,6 +113,41 @@ __global__ void map_codes_kernel(const uint8_t* __restrict__ raw, const uint8_t*
     for (; i < n; i += stride) codes[i] = lut[raw[i]];
 }
 
+// 2-bit packed ACGT bytes (host-packed by ovl_set_reads: base i at bits 2(i % 4) of byte i / 4, A C G T =
+// 0 1 2 3) -> dense symbol codes through the read set's LUT (codes[i] = lut["ACGT"[code]]); one lane per 16
+// packed bytes (64 bases: one 16-byte load, four 16-byte stores), a 4-entry table in registers.
+__global__ void unpack2_kernel(const uint8_t* __restrict__ pk, const uint8_t* __restrict__ lut,
+                               uint8_t* __restrict__ codes, int64_t n) {
+    const uint32_t c0 = lut['A'], c1 = lut['C'], c2 = lut['G'], c3 = lut['T'];
+    const int64_t groups = (n + 63) / 64;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += stride) {
+        const uint4 v = reinterpret_cast<const uint4*>(pk)[g];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t out[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t x = w[k >> 2] >> (8 * (k & 3));  // packed byte k: bases 4k .. 4k + 3
+            uint32_t o = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t c = (x >> (2 * b)) & 3u;
+                const uint32_t m = c == 0 ? c0 : (c == 1 ? c1 : (c == 2 ? c2 : c3));
+                o |= m << (8 * b);
+            }
+            out[k] = o;
+        }
+        const int64_t base = g * 64;
+        if (base + 64 <= n) {
+            uint4* d = reinterpret_cast<uint4*>(codes + base);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = make_uint4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
+        } else {
+            for (int64_t i = base; i < n; ++i) codes[i] = (uint8_t)(out[(i - base) >> 2] >> (8 * ((i - base) & 3)));
+        }
+    }
+}
+
 // One lane per (read, word).  Both rows were zeroed beforehand (row padding and the
 // zero word W of the prefix layout stay zero).
 template <int P>
@@ -1335,6 +1370,16 @@ extern "C" hipError_t ovl_launch_map_codes(const uint8_t* raw, const uint8_t* lu
     int64_t blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     map_codes_kernel<<<(unsigned)blocks, 256, 0, stream>>>(raw, lut, codes, n);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t ovl_launch_unpack2(const uint8_t* pk, const uint8_t* lut, uint8_t* codes, int64_t n,
+                                         hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if (reinterpret_cast<uintptr_t>(pk) & 15) return hipErrorInvalidValue;
+    int64_t blocks = ((n + 63) / 64 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    unpack2_kernel<<<(unsigned)blocks, 256, 0, stream>>>(pk, lut, codes, n);
     return hipGetLastError();
 }
 

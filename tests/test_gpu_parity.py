@@ -452,3 +452,34 @@ def test_dp_fast_and_classic_agree_with_oracle(oracle_mod, params):
             del os.environ["OVL_DP_CLASSIC"]
         np.testing.assert_array_equal(sc, rs)
         np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("case", ["acgt_odd_total", "subset_AT", "subset_CG_T", "n_at_end", "n_at_start",
+                                  "lowercase", "tiny"])
+def test_read_upload_forms(engine, oracle_mod, case):
+    """ovl_set_reads uploads ACGT-only read sets 2-bit packed (stage_reads, unpack2_kernel) and any other
+    byte set as it is: odd totals (not a multiple of 4 or 64 bytes), alphabets that are strict subsets of ACGT
+    (their dense codes differ from A C G T = 0 1 2 3), a single other byte at either end of the bytes (the
+    packing abandoned in the last or the first part), lowercase, a few bases -- all equal to the oracle."""
+    rng = random.Random(sum(map(ord, case)))
+    alpha = {"subset_AT": "AT", "subset_CG_T": "CGT", "lowercase": "acgt"}.get(case, "ACGT")
+    n = 3 if case == "tiny" else 3001
+    reads = [_rand(rng, rng.randint(1, 7) if case == "tiny" else rng.choice([97, 100, 101, 100, 33]), alpha)
+             for _ in range(n)]
+    if case == "n_at_end":
+        reads[-1] = reads[-1][:-1] + "N"
+    if case == "n_at_start":
+        reads[0] = "N" + reads[0][1:]
+    m = 40_000 if n > 3 else 9
+    a = np.array([rng.randrange(n) for _ in range(m)], np.int32)
+    b = np.array([rng.randrange(n) for _ in range(m)], np.int32)
+    engine.set_reads(reads)
+    s, e = engine.score(a, b)
+    rs, re_ = oracle_mod.batch_ungapped(reads, a, b, 10, -1)
+    np.testing.assert_array_equal(s, rs)
+    np.testing.assert_array_equal(e, re_)
+    # the gapped kernels read the same codes
+    s2, e2 = engine.score(a[:2000], b[:2000], indel=-2)
+    rs2, re2 = oracle_mod.batch_dp(reads, a[:2000], b[:2000], 10, -1, -2)
+    np.testing.assert_array_equal(s2, rs2)
+    np.testing.assert_array_equal(e2, re2)
