@@ -66,6 +66,7 @@ constexpr unsigned kHostShared = hipHostMallocPortable | hipHostMallocCoherent;
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool view = false;  // a part of another buffer (set_view): not freed, not grown
 };
 
 thread_local std::string g_err;
@@ -139,7 +140,8 @@ struct Dev {
     int32_t srow = 0;  // sfx row stride (words)
     int32_t trow = 0;  // pfx row stride (words)
     DevBuf codes, off, len, sfx, pfx, lut, full;  // full: bit r set iff len[r] == lmax
-    DevBuf raw;                                   // upload staging of ovl_set_reads (freed after the upload)
+    DevBuf raw;                                   // the uploaded read bytes (raw or 2-bit packed)
+    DevBuf rd;  // ovl_set_reads' upload block, the stage's layout; off, len, full, lut and raw are views into it
     // scratch
     DevBuf a, b, score, end, tb, err_flag;
     DevBuf lane_col;      // lane-per-pair DP: per-wavefront strip hand-off columns
@@ -269,6 +271,7 @@ int fail(const Dev* d, int code, const char* fmt, ...) {
 
 hipError_t ensure(DevBuf& b, size_t bytes) {
     if (bytes < 16) bytes = 16;
+    if (b.view) return hipErrorInvalidValue;
     if (b.bytes >= bytes) return hipSuccess;
     if (b.p) {
         hipError_t e = hipFree(b.p);
@@ -282,9 +285,16 @@ hipError_t ensure(DevBuf& b, size_t bytes) {
 }
 
 void release(DevBuf& b) {
-    if (b.p) (void)hipFree(b.p);
+    if (b.p && !b.view) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
+    b.view = false;
+}
+
+void set_view(DevBuf& v, DevBuf& whole, size_t offset, size_t bytes) {
+    v.p = static_cast<char*>(whole.p) + offset;
+    v.bytes = bytes;
+    v.view = true;
 }
 
 template <typename T>
@@ -979,7 +989,7 @@ void destroy_dev(Dev* d) {
     (void)hipSetDevice(d->device);
     for (hipStream_t s : {d->stream, d->s_in, d->s_out})
         if (s) (void)hipStreamSynchronize(s);
-    for (DevBuf* b : {&d->codes, &d->off, &d->len, &d->sfx, &d->pfx, &d->lut, &d->full, &d->raw, &d->a, &d->b,
+    for (DevBuf* b : {&d->codes, &d->off, &d->len, &d->sfx, &d->pfx, &d->lut, &d->full, &d->raw, &d->rd, &d->a, &d->b,
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
                       &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
                       &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
@@ -2025,28 +2035,24 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
     d->cand_n = -1;
     d->heavy_for = -1;
     const int32_t n_reads = h.n_reads;
-    if ((e = ensure(d->off, sizeof(int64_t) * h.off.size())) != hipSuccess) return e;
-    if ((e = ensure(d->len, sizeof(int32_t) * h.len.size())) != hipSuccess) return e;
+    // one copy of the stage's block (offsets, lengths, bitmap, code table, then the packed or raw bytes), the
+    // arrays used in place as views into it
+    const size_t pk_bytes = (((size_t)h.total + 63) / 64) * 16;
+    const size_t blk = h.packed2 ? st.o_pk + pk_bytes : st.o_raw + (size_t)h.total;
+    for (DevBuf* v : {&d->off, &d->len, &d->full, &d->lut, &d->raw}) release(*v);
+    if ((e = ensure(d->rd, blk + 64)) != hipSuccess) return e;
+    set_view(d->off, d->rd, st.o_off, sizeof(int64_t) * h.off.size());
+    set_view(d->len, d->rd, st.o_len, sizeof(int32_t) * h.len.size());
+    set_view(d->full, d->rd, st.o_full, sizeof(uint32_t) * h.full.size());
+    set_view(d->lut, d->rd, st.o_lut, 256);
+    set_view(d->raw, d->rd, h.packed2 ? st.o_pk : st.o_raw, h.packed2 ? pk_bytes : (size_t)h.total);
     if ((e = ensure(d->codes, (size_t)h.total + 64)) != hipSuccess) return e;  // tail pad: clamped reads
-    if ((e = ensure(d->lut, 256)) != hipSuccess) return e;
-    if ((e = ensure(d->raw, (size_t)h.total + 64)) != hipSuccess) return e;
-    if ((e = ensure(d->full, sizeof(uint32_t) * h.full.size())) != hipSuccess) return e;
     hipStream_t s = d->stream;
-    if ((e = hipMemcpyAsync(d->off.p, st.p + st.o_off, sizeof(int64_t) * h.off.size(), hipMemcpyHostToDevice, s)))
-        return e;
-    if ((e = hipMemcpyAsync(d->len.p, st.p + st.o_len, sizeof(int32_t) * h.len.size(), hipMemcpyHostToDevice, s)))
-        return e;
-    if ((e = hipMemcpyAsync(d->lut.p, st.p + st.o_lut, 256, hipMemcpyHostToDevice, s))) return e;
-    if ((e = hipMemcpyAsync(d->full.p, st.p + st.o_full, sizeof(uint32_t) * h.full.size(), hipMemcpyHostToDevice, s)))
-        return e;
+    if ((e = hipMemcpyAsync(d->rd.p, st.p, blk, hipMemcpyHostToDevice, s))) return e;
     if (h.total > 0 && h.packed2) {
-        // 2-bit packed bytes (stage_reads), read by unpack2_kernel in 16-byte groups
-        const size_t pk_bytes = (((size_t)h.total + 63) / 64) * 16;
-        if ((e = hipMemcpyAsync(d->raw.p, h.src, pk_bytes, hipMemcpyHostToDevice, s))) return e;
         if ((e = ovl_launch_unpack2(as<uint8_t>(d->raw), as<uint8_t>(d->lut), as<uint8_t>(d->codes), h.total, s)))
             return e;
     } else if (h.total > 0) {
-        if ((e = hipMemcpyAsync(d->raw.p, h.src, (size_t)h.total, hipMemcpyHostToDevice, s))) return e;
         if ((e = ovl_launch_map_codes(as<uint8_t>(d->raw), as<uint8_t>(d->lut), as<uint8_t>(d->codes), h.total, s)))
             return e;
     }
@@ -2054,8 +2060,6 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
         const size_t rows = (size_t)std::max(n_reads, 1);
         if ((e = ensure(d->sfx, rows * h.srow * sizeof(uint32_t)))) return e;
         if ((e = ensure(d->pfx, rows * h.trow * sizeof(uint32_t)))) return e;
-        if ((e = hipMemsetAsync(d->sfx.p, 0, rows * h.srow * sizeof(uint32_t), s))) return e;
-        if ((e = hipMemsetAsync(d->pfx.p, 0, rows * h.trow * sizeof(uint32_t), s))) return e;
         if ((e = ovl_launch_pack(h.planes, as<uint8_t>(d->codes), as<int64_t>(d->off), as<int32_t>(d->len), n_reads,
                                  h.wmax, h.srow, h.trow, as<uint32_t>(d->sfx), as<uint32_t>(d->pfx), s)))
             return e;

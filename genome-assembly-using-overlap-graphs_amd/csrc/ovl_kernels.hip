@@ -148,8 +148,8 @@ __global__ void unpack2_kernel(const uint8_t* __restrict__ pk, const uint8_t* __
     }
 }
 
-// One lane per (read, word).  Both rows were zeroed beforehand (row padding and the
-// zero word W of the prefix layout stay zero).
+// One lane per (read, word); the lane of a row's last word also zeroes the row padding (words W*P ..
+// row stride), so the rows need no clearing beforehand.
 template <int P>
 __global__ void pack_planes_kernel(const uint8_t* __restrict__ codes, const int64_t* __restrict__ off,
                                    const int32_t* __restrict__ len, int32_t n_reads, int32_t w,
@@ -185,6 +185,10 @@ __global__ void pack_planes_kernel(const uint8_t* __restrict__ codes, const int6
         for (int p = 0; p < P; ++p) {
             pfx[(int64_t)r * trow + k * P + p] = pl[p];
             sfx[(int64_t)r * srow + k * P + p] = sl[p];
+        }
+        if (k == w - 1) {
+            for (int32_t q = w * P; q < trow; ++q) pfx[(int64_t)r * trow + q] = 0u;
+            for (int32_t q = w * P; q < srow; ++q) sfx[(int64_t)r * srow + q] = 0u;
         }
     }
 }
@@ -601,6 +605,65 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     return out;
 }
 
+// Read a inside b's window (a lane of uniform_kernel's sweep whose read a is shorter than b, n < m): the end
+// positions j in (n, m] compare all n bases of a with t[j - n, j) (L = n), which the sweep's shifts do not
+// see.  j is wave-uniform -- the loop runs it from jhi down to jlo, the bounds over the wave's such lanes --
+// and each lane keeps the keys of its own range.  In the rows, s base i sits at position 32W - n + i (suffix
+// layout) and t base i at position i (prefix layout), so t shifted up by 32W - j puts t[j - n + i] on s base
+// i; the shifted t moves up one bit per step (one v_alignbit per word and plane), and the s-padding
+// positions below 32W - n are masked out.  Returns the best key of the lane's range (INT32_MIN if empty).
+template <int W>
+__device__ __forceinline__ int32_t window_keys(const uint32_t* Sw, const uint32_t* Tw, int32_t n, int32_t m,
+                                            int32_t jlo, int32_t jhi, int32_t match, int32_t dms) {
+    constexpr int P = 2;
+    uint32_t SV[W];  // valid s bits: positions >= 32W - n
+    const int32_t s0 = 32 * W - n;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const int32_t lo = 32 * k;
+        SV[k] = s0 <= lo ? ~0u : (s0 >= lo + 32 ? 0u : (~0u << (uint32_t)(s0 - lo)));
+    }
+    // t shifted up by sh0 = 32W - jhi (wave-uniform: word shift ws, bit shift bs)
+    const int32_t sh0 = 32 * W - jhi;
+    const int ws = sh0 >> 5, bs = sh0 & 31;
+    uint32_t U[W][P];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+#pragma unroll
+        for (int c = 0; c < P; ++c) {
+            uint32_t hi = 0u, lo = 0u;
+#pragma unroll
+            for (int q = 0; q < W; ++q) {  // (scalar select on ws: no dynamic register indexing)
+                if (q == ws) {
+                    hi = k - q >= 0 ? Tw[(k - q) * P + c] : 0u;
+                    lo = k - q - 1 >= 0 ? Tw[(k - q - 1) * P + c] : 0u;
+                }
+            }
+            U[k][c] = bs ? alignbit(hi, lo, 32u - (uint32_t)bs) : hi;
+        }
+    }
+    const int32_t d16 = (int32_t)((uint32_t)dms << 16);
+    const int32_t kn = (int32_t)((uint32_t)(match * n) << 16);
+    int32_t best = INT32_MIN;
+    for (int32_t j = jhi; j >= jlo; --j) {
+        uint32_t X = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            const uint32_t mm = __builtin_amdgcn_bitop3_b32(Sw[k * P + 1], U[k][1], Sw[k * P] ^ U[k][0], 0xBE) & SV[k];
+            X = bcnt_acc(mm, X);
+        }
+        const int32_t key = (int32_t)X * d16 + (kn - j);
+        if (j > n && j <= m && key > best) best = key;
+        // j - 1: t one bit further up
+#pragma unroll
+        for (int k = W - 1; k >= 0; --k) {
+#pragma unroll
+            for (int c = 0; c < P; ++c) U[k][c] = alignbit(U[k][c], k ? U[k - 1][c] : 0u, 31u);
+        }
+    }
+    return best;
+}
+
 // One general-path unit: up to 64/RS pairs, RS = 2^rs_log2 lanes per pair (lanes
 // slot, slot + 64/RS, ...; lane group g sweeps r = g, g + RS, ...), any lengths
 // <= 32W, per-lane masks.  Writes (score, end), or (-1, -1) for a bad index.
@@ -825,16 +888,20 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         uint32_t Sw[SROW], Tw[TROW];
         load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
         load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
-        // read a of length lw? one bit per read (L1-resident bitmap); b's length decides uniform (m = lw)
-        // or t-truncated (m < lw, scored by this sweep with a snapshot); a shorter read a is a side pair
+        // read a of length lw? one bit per read (L1-resident bitmap); b's length decides uniform (m = lw).
+        // TT: every other pair is scored by this sweep too -- its keys for j <= min(n, m) are the uniform
+        // keys (a snapshot of the block maxima after shift min(n, m) % 32), and a shorter read a (n < m) adds
+        // its windows j in (n, m] after the sweep (window_keys); else a shorter read a is a side pair
         const bool fa = ok && ((full[a >> 5] >> (a & 31)) & 1u);
         const int32_t mb = len[b];
+        int32_t na = lw;
+        if (TT && ok && !fa) na = len[a];
         const bool uni = fa && mb == lw;
-        const bool tt = TT && fa && mb < lw;
-        const int32_t tm = tt ? mb : -1;
+        const bool tt = TT && ok && !uni;
+        const int32_t tm = tt ? (na < mb ? na : mb) : -1;
         uint32_t tmask = 0;
-        for (uint64_t bm = __ballot(tt); bm; bm &= bm - 1)  // scalar loop over the t-truncated lanes
-            tmask |= 1u << (__builtin_amdgcn_readlane(mb, (int)__builtin_ctzll(bm)) & 31);
+        for (uint64_t bm = __ballot(tt); bm; bm &= bm - 1)  // scalar loop over the truncated lanes
+            tmask |= 1u << (__builtin_amdgcn_readlane(tm, (int)__builtin_ctzll(bm)) & 31);
         OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
         if constexpr (!LAT) {
             if (mine && !ok) ovl_flag_error(err_flag);
@@ -850,11 +917,25 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
 #else
         T best = sweep_uniform<W, KM>(Sw, Tw, lw, match, mismatch - match, 0u, 32u, tmask, tm);
 #endif
+        if constexpr (TT) {
+            const bool win = tt && na < mb;
+            uint64_t wm = __ballot(win);
+            if (wm) {  // wave-uniform: j from the largest m down to the smallest n + 1 over the window lanes
+                int32_t jlo = 1 << 30, jhi = 0;
+                for (; wm; wm &= wm - 1) {
+                    const int l = (int)__builtin_ctzll(wm);
+                    jlo = min(jlo, __builtin_amdgcn_readlane(na, l) + 1);
+                    jhi = max(jhi, __builtin_amdgcn_readlane(mb, l));
+                }
+                const int32_t wk = window_keys<W>(Sw, Tw, na, mb, jlo, jhi, match, mismatch - match);
+                if (win && (T)wk > best) best = (T)wk;
+            }
+        }
         OVL_TR_CLOCK(3, (uint32_t)best);
         if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
-            put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, lw, match, pack_inv(match, mismatch));
+            put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, na, match, pack_inv(match, mismatch));
         }
         OVL_TR_CLOCK(4, (uint32_t)best);
 #ifndef OVL_ABLATE_DRAIN
