@@ -886,8 +886,15 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             continue;
         }
         uint32_t Sw[SROW], Tw[TROW];
+#ifdef OVL_ABLATE_LOADS  // diagnostic build only: rows made up from the indices (no row loads)
+#pragma unroll
+        for (int i = 0; i < SROW; ++i) Sw[i] = (uint32_t)a * 0x9E3779B9u + (uint32_t)i * 0x85EBCA6Bu;
+#pragma unroll
+        for (int i = 0; i < TROW; ++i) Tw[i] = (uint32_t)b * 0xC2B2AE35u + (uint32_t)i * 0x27D4EB2Fu;
+#else
         load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
         load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+#endif
         // read a of length lw? one bit per read (L1-resident bitmap); b's length decides uniform (m = lw).
         // TT: every other pair is scored by this sweep too -- its keys for j <= min(n, m) are the uniform
         // keys (a snapshot of the block maxima after shift min(n, m) % 32), and a shorter read a (n < m) adds
