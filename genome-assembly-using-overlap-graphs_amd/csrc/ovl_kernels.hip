@@ -759,7 +759,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     // latency mode: 0 = sweep, 1 = side pairs; the side wave is the first of each pair in the block
     // (A/B with its drain at priority 1: cfg2 8.40 -> 8.33 us; without the priority 8.85 us)
     const int role = LAT ? ((wib & 1) ^ 1) : 0;
-    const int G = LAT ? 2 : (int)(blockDim.x >> 6);  // tiles per block per iteration (throughput: one per wave)
+    constexpr int G = LAT ? 2 : 4;                 // tiles per block per iteration
     const int grp = LAT ? (wib >> 1) : wib;
     int4* ring = ring_all[LAT ? 0 : wib];
     const int64_t n_tiles = (n_pairs + 63) >> 6;
