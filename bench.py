@@ -72,7 +72,7 @@ def algorithmic_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> int:
 
 
 def _short_kernel(name: str) -> str:
-    """'void ovl::uniform_kernel<4, 0, false, 2>(...)' -> 'uniform_kernel<4, 0, false, 2>'."""
+    """'void ovl::uniform_kernel<4, 0, false, 2, false>(...)' -> 'uniform_kernel<4, 0, false, 2, false>'."""
     name = name.split("(")[0].strip()
     for pre in ("void ", "ovl::"):
         name = name.replace(pre, "")
@@ -579,7 +579,8 @@ def kernel_name(w, sink: int, pairs: int) -> str:
         return f"{w.kernel} kernel"
     lmax = w.eng.info()["lmax"]
     lat = (pairs + 63) // 64 <= 256 * 8
-    return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}>"
+    # (the fifth parameter, IX, is true only for host pair lists read in their encoding)
+    return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}, false>"
 
 
 # result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed)
