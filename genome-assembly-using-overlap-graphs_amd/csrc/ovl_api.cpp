@@ -2069,7 +2069,12 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
 
 }  // namespace
 
-OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
+namespace {
+
+// ovl_set_reads; sync = false (ovl_score_pairs) leaves the uploads running on each device's kernel stream --
+// the scoring launches queue behind them there -- and the caller synchronises those streams before it returns
+// (the pinned stage must outlive the copy)
+int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads, bool sync) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
     if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
@@ -2089,8 +2094,8 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
         d->cand_n = -1;
         d->heavy_for = -1;
     }
-    // the pinned stage (the previous upload from it is complete: ovl_set_reads synchronises), then the upload
-    // to every device, then wait for all (the uploads and packs overlap across devices)
+    // the pinned stage (the previous upload from it is complete: every caller synchronised it), then the
+    // upload to every device, then wait for all (the uploads and packs overlap across devices)
     rc = stage_reads(c, c->stage, h);
     if (rc != OVL_OK) return rc;
     trace.mark('s', 0);
@@ -2098,6 +2103,7 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
         if ((e = upload_reads(d, h, c->stage)) != hipSuccess) break;
     trace.mark('u', 0);
     for (Dev* d : c->devs) {
+        if (!sync && e == hipSuccess) break;
         (void)hipSetDevice(d->device);
         hipError_t e2 = hipStreamSynchronize(d->stream);
         if (e == hipSuccess) e = e2;
@@ -2116,6 +2122,12 @@ OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offset
     }
     c->h_len.assign(h.len.begin(), h.len.begin() + n_reads);
     return OVL_OK;
+}
+
+}  // namespace
+
+OVL_API int ovl_set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
+    return set_reads(c, seqs, offsets, n_reads, true);
 }
 
 OVL_API int ovl_reads_info(const ovl_ctx* c, int32_t* n_reads, int32_t* lmax, int32_t* planes, int64_t* device_bytes) {
@@ -2218,9 +2230,19 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
 OVL_API int ovl_score_pairs(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads,
                             const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs, int32_t match,
                             int32_t mismatch, int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end) {
-    int rc = ovl_set_reads(c, seqs, offsets, n_reads);
+    // the read upload runs on the devices while the host encodes the pair list's first chunk; the scoring
+    // launches queue behind it on the same streams
+    int rc = set_reads(c, seqs, offsets, n_reads, false);
     if (rc != OVL_OK) return rc;
-    return ovl_score_host(c, a_idx, b_idx, n_pairs, match, mismatch, indel, band, out_score, out_end);
+    rc = ovl_score_host(c, a_idx, b_idx, n_pairs, match, mismatch, indel, band, out_score, out_end);
+    DeviceGuard guard;
+    for (Dev* d : c->devs) {  // (the stage outlives the copy; an upload error surfaces here if nothing else did)
+        (void)hipSetDevice(d->device);
+        const hipError_t e = hipStreamSynchronize(d->stream);
+        if (rc == OVL_OK && e != hipSuccess)
+            rc = fail(c, OVL_E_HIP, "ovl_score_pairs: read upload: %s", hipGetErrorString(e));
+    }
+    return rc;
 }
 
 OVL_API int ovl_align_one(ovl_ctx* ctx, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
