@@ -46,6 +46,16 @@ __global__ void wide16_two(int4* a, int4* b, int64_t n4) {  // four pairs per la
     }
 }
 
+__global__ void packed16(uint16_t* p, int64_t n) {  // one uint16 per lane (the packed result sink)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store((uint16_t)(i * 7), p + i);
+}
+
+__global__ void packed16x2(uint32_t* p, int64_t n2) {  // two uint16 per lane as one 4-byte store
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store((uint32_t)(i * 7), p + i);
+}
+
 int main() {
     const int64_t n = 2000000;
     const size_t bytes = (size_t)n * 8;
@@ -59,6 +69,7 @@ int main() {
     int dev = 0, cus = 0;
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int reps = 50;
+    size_t nbytes = bytes;  // bytes a timed operation moves (the GB/s column)
     auto time_it = [&](const char* name, auto fn) -> int {
         for (int w = 0; w < 3; ++w) fn();
         CHK(hipDeviceSynchronize());
@@ -69,7 +80,7 @@ int main() {
         float ms = 0;
         CHK(hipEventElapsedTime(&ms, e0, e1));
         ms /= reps;
-        printf("%-34s %8.4f ms  %6.2f GB/s\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+        printf("%-34s %8.4f ms  %6.2f GB/s\n", name, ms, nbytes / (ms * 1e-3) / 1e9);
         return 0;
     };
     int32_t* ha = (int32_t*)h;
@@ -82,6 +93,18 @@ int main() {
         time_it("int4, two pairs per lane", [&] { wide16<<<blocks, 256>>>((int4*)h, n / 2); });
         time_it("int4 x two arrays, 4 pairs/lane", [&] { wide16_two<<<blocks, 256>>>((int4*)ha, (int4*)hb, n / 4); });
     }
+    // the packed sink: 2 bytes per pair, into default and into fine-grained (coherent) pinned memory
+    void* hc = nullptr;
+    CHK(hipHostMalloc(&hc, bytes, hipHostMallocCoherent));
+    nbytes = (size_t)n * 2;
+    for (int blocks : {cus * 16, cus * 64}) {
+        printf("-- packed, grid %d x 256\n", blocks);
+        time_it("uint16 per lane", [&] { packed16<<<blocks, 256>>>((uint16_t*)h, n); });
+        time_it("uint16 per lane, coherent", [&] { packed16<<<blocks, 256>>>((uint16_t*)hc, n); });
+        time_it("2 x uint16 per lane, coherent", [&] { packed16x2<<<blocks, 256>>>((uint32_t*)hc, n / 2); });
+    }
+    nbytes = bytes;
+    CHK(hipHostFree(hc));
     time_it("hipMemcpyAsync D2H", [&] { (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, 0); });
     time_it("hipMemcpyAsync D2H (2 halves)", [&] {
         (void)hipMemcpyAsync(h, d, bytes / 2, hipMemcpyDeviceToHost, 0);
