@@ -31,6 +31,11 @@
 
 #include "ovl_kernels.h"
 
+// uniform sweep: two shifts from one shifted s (sweep_uniform, keys_s2); 0 shifts s for each shift
+#ifndef OVL_SHIFT_PAIR
+#define OVL_SHIFT_PAIR 1
+#endif
+
 namespace ovl {
 
 #ifdef OVL_TRACE  // diagnostic build only (make trace): per-wavefront timestamps of the uniform kernel
@@ -480,6 +485,99 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     // r = 0 (t unshifted, block W when lw = 32W) through keys; r >= 1 through keys_s for W <= 4 (A/B on
     // one box: cfg2 -0.7 %, target -0.4 %; at W = 5, cfg3, +1.3 %, so W >= 5 keeps the t shift)
     constexpr bool SHIFT_S = W <= 4;
+    // Two shifts from one shifted s (keys_s2): s shifted down by 31 - r serves shift r + 1 against t as it
+    // is and shift r against t moved up one bit (Tup, built once per pair), so a step of two shifts shifts
+    // s once.  In Tup, bit 0 of word 0 is t position -1 (no base): that bit of a block's bottom word is
+    // masked out (one v_and for blocks q >= 1; folded into the top-word mask for q = 0).
+    constexpr bool PAIR = SHIFT_S && KM == 0 && OVL_SHIFT_PAIR;
+    uint32_t Tup[PAIR ? W : 1][P];
+    if constexpr (PAIR) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+#pragma unroll
+            for (int c = 0; c < P; ++c) Tup[i][c] = alignbit(Tw[i * P + c], i ? Tw[(i - 1) * P + c] : 0u, 31u);
+        }
+    }
+    // The same for the t shift (W >= 5, keys_t2): t shifted up by r + 1 serves shift r + 1 against s as it
+    // is and shift r against s moved down one bit (Sdn); bit 31 of Sdn's word W-1 is position 32W (no base):
+    // that bit of a block's top word is masked out.
+    constexpr bool PAIR_T = !SHIFT_S && KM == 0 && OVL_SHIFT_PAIR;
+    uint32_t Sdn[PAIR_T ? W : 1][P];
+    if constexpr (PAIR_T) {
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+#pragma unroll
+            for (int c = 0; c < P; ++c)
+                Sdn[k][c] = k < W - 1 ? alignbit(Sw[(k + 1) * P + c], Sw[k * P + c], 1u) : Sw[k * P + c] >> 1;
+        }
+    }
+    auto keys_t2 = [&](uint32_t r, T rm, auto nq_tag, T (&k0)[W + 1], T (&k1)[W + 1]) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        static_assert(NQ <= W, "keys_t2: r >= 1 has at most W blocks");
+        const uint32_t r1 = r + 1;                                // 2..31
+        const uint32_t vt = (uint32_t)((int32_t)0x80000000 >> r);  // U[0]: its top r + 1 bits hold bases
+        uint32_t U[W][P];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+#pragma unroll
+            for (int c = 0; c < P; ++c) U[i][c] = alignbit(Tw[i * P + c], i ? Tw[(i - 1) * P + c] : 0u, r1);
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            uint32_t X0 = 0, X1 = 0;
+#pragma unroll
+            for (int k = W - 1 - q; k < W; ++k) {
+                const int i = k + q - (W - 1);
+                uint32_t m1 = __builtin_amdgcn_bitop3_b32(Sw[k * P + 1], U[i][1], Sw[k * P] ^ U[i][0], 0xBE);
+                uint32_t m0 = __builtin_amdgcn_bitop3_b32(Sdn[k][1], U[i][1], Sdn[k][0] ^ U[i][0], 0xBE);
+                if (i == 0) {
+                    m1 &= vt;
+                    m0 &= k == W - 1 ? (vt & 0x7FFFFFFFu) : vt;
+                } else if (k == W - 1) {
+                    m0 &= 0x7FFFFFFFu;
+                }
+                const bool first = k == W - 1 - q;
+                X1 = first ? (uint32_t)__builtin_popcount(m1) : bcnt_acc(m1, X1);
+                X0 = first ? (uint32_t)__builtin_popcount(m0) : bcnt_acc(m0, X0);
+            }
+            k0[q] = ((((int32_t)X0 << 8) >> 8) * ((dv << 8) >> 8)) + rm;
+            k1[q] = ((((int32_t)X1 << 8) >> 8) * ((dv << 8) >> 8)) + (rm + mq);
+        }
+    };
+    auto keys_s2 = [&](uint32_t r, T rm, auto nq_tag, T (&k0)[W + 1], T (&k1)[W + 1]) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        static_assert(NQ <= W, "keys_s2: r >= 1 has at most W blocks");
+        const uint32_t sg = 31u - r;                  // 1..30 (r + 1 <= 31)
+        const uint32_t vt = 0xFFFFFFFFu >> sg;        // s word W-1: its low r + 1 bits hold bases
+        uint32_t V[W][P];
+#pragma unroll
+        for (int k = W - NQ; k < W; ++k) {
+#pragma unroll
+            for (int c = 0; c < P; ++c)
+                V[k][c] = k < W - 1 ? alignbit(Sw[(k + 1) * P + c], Sw[k * P + c], sg) : Sw[k * P + c] >> sg;
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            uint32_t X0 = 0, X1 = 0;
+#pragma unroll
+            for (int k = W - 1 - q; k < W; ++k) {
+                const int i = k - (W - 1 - q);
+                uint32_t m1 = __builtin_amdgcn_bitop3_b32(V[k][1], Tw[i * P + 1], V[k][0] ^ Tw[i * P], 0xBE);
+                uint32_t m0 = __builtin_amdgcn_bitop3_b32(V[k][1], Tup[i][1], V[k][0] ^ Tup[i][0], 0xBE);
+                if (k == W - 1) {
+                    m1 &= vt;
+                    m0 &= i == 0 ? (vt & ~1u) : vt;
+                } else if (i == 0) {
+                    m0 &= ~1u;
+                }
+                const bool first = k == W - 1 - q;
+                X1 = first ? (uint32_t)__builtin_popcount(m1) : bcnt_acc(m1, X1);
+                X0 = first ? (uint32_t)__builtin_popcount(m0) : bcnt_acc(m0, X0);
+            }
+            k0[q] = ((((int32_t)X0 << 8) >> 8) * ((dv << 8) >> 8)) + rm;
+            k1[q] = ((((int32_t)X1 << 8) >> 8) * ((dv << 8) >> 8)) + (rm + mq);
+        }
+    };
     // t-truncated lanes: the best key of blocks 0..qm as they stand after shift m % 32 (block qm's last
     // valid end position).  A max under "q <= qm" masks, not a select on "q == qm": the compiler turns
     // an equality select chain into an indexed table, and the block maxima into an LDS array.
@@ -513,7 +611,11 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     auto body2 = [&](uint32_t r, T rm, auto nq_tag) {
         constexpr int NQ = decltype(nq_tag)::value;
         T k0[W + 1], k1[W + 1];
-        if constexpr (SHIFT_S) {
+        if constexpr (PAIR) {
+            keys_s2(r, rm, nq_tag, k0, k1);
+        } else if constexpr (PAIR_T) {
+            keys_t2(r, rm, nq_tag, k0, k1);
+        } else if constexpr (SHIFT_S) {
             keys_s(r, 0xFFFFFFFFu >> (32u - r), rm, nq_tag, k0);
             keys_s(r + 1, 0xFFFFFFFFu >> (31u - r), rm + mq, nq_tag, k1);
         } else {

@@ -111,7 +111,7 @@ def load():
     global _lib
     with _lock:
         if _lib is None:
-            path = os.environ.get("OVL_LIB_PATH", LIB_PATH)
+            path = os.environ.get("OVL_LIB_PATH") or LIB_PATH
             if not os.path.exists(path):
                 raise OvlError(-2, f"{path} not built: run __graft_entry__.build() "
                                    "(make -C genome-assembly-using-overlap-graphs_amd/csrc)")
