@@ -57,9 +57,10 @@ WORKLOAD_DESC = {
 
 # VALU issue model (profiles/r01_valu_rates.txt, tools/valu_rates.hip): a wave64 integer VALU instruction
 # occupies its SIMD ~2.6 (xor/or/and/add/sub/bitop3/lshr) or ~4.3 (bcnt/alignbit/mad24/max/min/cndmask...)
-# shader cycles; the uniform sweep's loop mix (tools/isa_mix.py) averages 3.66.  The ISA peak is 2 cycles
+# shader cycles; the uniform sweep's loop mix (59 VALU per two shifts: 34 fast, 25 slow; round 3) averages 3.51.
+# The ISA peak is 2 cycles
 # per wave64 instruction on a SIMD-32 (MI355X_MICROARCH.md, "Wave scheduling").
-VALU_CYCLES_PER_INST = 3.66
+VALU_CYCLES_PER_INST = 3.51
 ISA_CYCLES_PER_INST = 2.0
 SIMD_COUNT = 1024
 SHADER_CLOCK_HZ = 2.4e9
