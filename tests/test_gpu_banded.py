@@ -92,6 +92,27 @@ def test_banded_cfg5_sample(engine, oracle_mod):
         np.testing.assert_array_equal(en, re_)
 
 
+def test_banded_cfg5_full_list(engine, oracle_mod):
+    """Config 5 at full size: every one of the 3.38 M candidate pairs at band 8 (the sweep's lane-kernel
+    form over the whole list, every tile and length mix), and a 500k strided sample at band 64 (one
+    wavefront per SIMD, the widest lane-kernel band), against oracle_overlap_banded."""
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import config_reads
+    reads, _ = dedup_reads(config_reads("cfg5"))
+    a, b = enumerate_candidates(reads, 5)
+    engine.set_reads(reads)
+    sc, en = engine.score(a, b, 10, -1, -2, 8)
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, 8)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+    idx = np.linspace(0, a.shape[0] - 1, 500_000).astype(np.int64)
+    a, b = a[idx], b[idx]
+    sc, en = engine.score(a, b, 10, -1, -2, 64)
+    rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, 64)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
+
+
 def test_banded_unsupported_magnitudes(engine):
     from ovlgraph import OvlError
     engine.set_reads(["ACGTACGT", "CGTACGTA"])
