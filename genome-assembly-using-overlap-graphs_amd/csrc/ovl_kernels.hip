@@ -35,6 +35,10 @@
 #ifndef OVL_SHIFT_PAIR
 #define OVL_SHIFT_PAIR 1
 #endif
+// uniform sweep: rows of at most this many words shift s (W above: t)
+#ifndef OVL_SHIFT_S_MAXW
+#define OVL_SHIFT_S_MAXW 5
+#endif
 
 namespace ovl {
 
@@ -483,8 +487,10 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
         }
     };
     // r = 0 (t unshifted, block W when lw = 32W) through keys; r >= 1 through keys_s for W <= 4 (A/B on
-    // one box: cfg2 -0.7 %, target -0.4 %; at W = 5, cfg3, +1.3 %, so W >= 5 keeps the t shift)
-    constexpr bool SHIFT_S = W <= 4;
+    // one box: cfg2 -0.7 %, target -0.4 %; at W = 5, cfg3, +1.3 %, so W >= 5 kept the t shift) -- and with
+    // two shifts per shifted row for W <= 5 (cfg3: 191 against 194-197 us with the t shift, three
+    // interleaved passes, profiles/r03_shift_s_w5_ab.json)
+    constexpr bool SHIFT_S = W <= OVL_SHIFT_S_MAXW;
     // Two shifts from one shifted s (keys_s2): s shifted down by 31 - r serves shift r + 1 against t as it
     // is and shift r against t moved up one bit (Tup, built once per pair), so a step of two shifts shifts
     // s once.  In Tup, bit 0 of word 0 is t position -1 (no base): that bit of a block's bottom word is
