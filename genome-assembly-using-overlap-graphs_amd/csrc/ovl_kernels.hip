@@ -35,9 +35,9 @@
 #ifndef OVL_SHIFT_PAIR
 #define OVL_SHIFT_PAIR 1
 #endif
-// uniform sweep: rows of at most this many words shift s (W above: t)
+// uniform sweep: rows of at most this many words shift s (W above: t; every W <= 8 by default)
 #ifndef OVL_SHIFT_S_MAXW
-#define OVL_SHIFT_S_MAXW 5
+#define OVL_SHIFT_S_MAXW 8
 #endif
 
 namespace ovl {
@@ -488,8 +488,9 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
     };
     // r = 0 (t unshifted, block W when lw = 32W) through keys; r >= 1 through keys_s for W <= 4 (A/B on
     // one box: cfg2 -0.7 %, target -0.4 %; at W = 5, cfg3, +1.3 %, so W >= 5 kept the t shift) -- and with
-    // two shifts per shifted row for W <= 5 (cfg3: 191 against 194-197 us with the t shift, three
-    // interleaved passes, profiles/r03_shift_s_w5_ab.json)
+    // two shifts per shifted row for every W (cfg3, W = 5: 191 against 194-197 us with the t shift; cfg5's
+    // default scoring, W = 8: 445-449 against 448-452 us, and W = 6 no longer spills; three interleaved passes
+    // each, profiles/r03_shift_s_w5_ab.json, r03_shift_s_w8_ab.json)
     constexpr bool SHIFT_S = W <= OVL_SHIFT_S_MAXW;
     // Two shifts from one shifted s (keys_s2): s shifted down by 31 - r serves shift r + 1 against t as it
     // is and shift r against t moved up one bit (Tup, built once per pair), so a step of two shifts shifts
