@@ -31,7 +31,7 @@
 
 #include "ovl_kernels.h"
 
-// uniform sweep: two shifts from one shifted s (sweep_uniform, keys_s2); 0 shifts s for each shift
+// uniform sweep: two shifts from one shifted row (sweep_uniform, keys_s2 / keys_t2); 0: one shifted row per shift
 #ifndef OVL_SHIFT_PAIR
 #define OVL_SHIFT_PAIR 1
 #endif
@@ -505,9 +505,9 @@ __device__ __forceinline__ typename Key<KM>::T sweep_uniform(const uint32_t* Sw,
             for (int c = 0; c < P; ++c) Tup[i][c] = alignbit(Tw[i * P + c], i ? Tw[(i - 1) * P + c] : 0u, 31u);
         }
     }
-    // The same for the t shift (W >= 5, keys_t2): t shifted up by r + 1 serves shift r + 1 against s as it
-    // is and shift r against s moved down one bit (Sdn); bit 31 of Sdn's word W-1 is position 32W (no base):
-    // that bit of a block's top word is masked out.
+    // The same for the t shift (W > OVL_SHIFT_S_MAXW, keys_t2): t shifted up by r + 1 serves shift r + 1
+    // against s as it is and shift r against s moved down one bit (Sdn); bit 31 of Sdn's word W-1 is position
+    // 32W (no base): that bit of a block's top word is masked out.
     constexpr bool PAIR_T = !SHIFT_S && KM == 0 && OVL_SHIFT_PAIR;
     uint32_t Sdn[PAIR_T ? W : 1][P];
     if constexpr (PAIR_T) {
