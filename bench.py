@@ -10,23 +10,26 @@ mismatch count, 2 B per pair) and host threads expand them into the caller's pin
 int32 arrays: packed chunks expanded while the next chunk scores, and the last ~20 % of
 the pairs stored as int32 straight into the arrays.
 
-    python bench.py [--gpus N --steps K --warmup W --config target --scaling weak|strong]
+    python bench.py [--gpus N --steps K --warmup W --config target]
 
 ``--gpus N`` > 1 without a launcher: this process starts ``python -m torch.distributed.run
 --nproc-per-node N bench.py ...`` as a CHILD before touching the GPU, waits for it and exits
 with its status (the ranks print the line).  Launched by torch.distributed.run (WORLD_SIZE set),
 WORLD_SIZE must equal --gpus.
 
-Every N runs the same workload (--config, default the north_star target point: PhiX N=50k
-l=100 p=0.01 k=5, ~2.0 M pairs).  N = 1: one process, one GPU.  N > 1, one process per GPU:
-  weak (default): every rank scores its own read set of that workload (seed + rank) -- the
-    reference's own parallel shape, independent graph builds side by side (experiments.py:537
-    fans graph builds out over joblib workers); value = all ranks' pairs / max-over-ranks time;
-  strong: ONE read set, its candidate list sharded by sum n*m over the ranks, every rank's
-    (score, end) into rank 0's shared pinned host buffer (ovlgraph.sharded.ShardedStep); the
-    line also carries the same list scored by one GPU in the same run and the speed-up.
-The N > 1 weak line also carries BASELINE configs[3]'s shape (cfg4, 38 M pairs) strong-scaled
-the same way.  Time = max over ranks between barriers.  Rank 0 prints one JSON line.
+Every N scores the same list (--config, default the north_star target point: PhiX N=50k
+l=100 p=0.01 k=5, 1,993,959 candidate pairs), so the N-point curve is strong scaling.
+N = 1: one process, one GPU.  N > 1, one process per GPU (north_star: "candidate pairs shard
+embarrassingly across the GPUs"): every rank holds the same read set and enumerates the same
+list, scores its contiguous shard (balanced by sum n*m) and its kernels store the shard's
+(score, end) into rank 0's shared pinned host buffer (ovlgraph.sharded.ShardedStep, a step
+fence in shared memory, no collective per step); value = the list's pairs / max-over-ranks
+time.  The N > 1 line also carries: the same list scored by rank 0's GPU alone in the same
+run (one_gpu_ms_per_step, speedup_vs_one_gpu, matches_one_gpu), rank 0's in-step roofline,
+the same shards collected by an RCCL gather into rank 0's HBM (rccl_gather), a read set per
+rank (weak_scaling: the reference's joblib shape), BASELINE configs[3] pair-sharded
+(cfg4_strong), configs[4]'s band sweep sharded (cfg5_sharded_band_sweep) and one process over
+the job's GPUs (single_process_all_gpus).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -110,6 +113,21 @@ def load_traffic(workload: str, kernel: str = None):
     """HBM bytes per launch of `kernel` from the committed PMC summary for this workload, or None."""
     d = load_profile(workload, kernel)
     return int(d["hbm_bytes_per_launch"]) if d.get("hbm_bytes_per_launch") else None
+
+
+def shard_traffic(key: str, workload: str, kernel: str, pairs_per_launch: int):
+    """(HBM bytes per launch, source) for `kernel` on a shard: the PMC summary of that shard when one is
+    committed (profiles/*_pmc.json with workload `key`), else the whole list's per-launch bytes scaled per
+    pair (the same kernel over the same reads), else (None, None)."""
+    t = load_traffic(key, kernel)
+    if t is not None:
+        return t, f"pmc ({key})"
+    d = load_profile(workload, kernel)
+    ppl = (d.get("bench_same_run") or {}).get("pairs_per_launch")
+    if d.get("hbm_bytes_per_launch") and ppl:
+        return int(d["hbm_bytes_per_launch"] / ppl * pairs_per_launch), \
+            f"pmc ({workload}, {ppl} pairs per launch) scaled per pair"
+    return None, None
 
 
 def valu_roofline(workload: str, kernel_ms: float, kernel: str = None):
@@ -256,12 +274,35 @@ class Workload:
         self.ds = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
         self.de = torch.empty(self.n_pairs, dtype=torch.int32, device=dev)
         from ovlgraph.hostmem import pinned_empty
-        self.out = (pinned_empty(self.n_pairs), pinned_empty(self.n_pairs))
+        self.out = self.own_out = (pinned_empty(self.n_pairs), pinned_empty(self.n_pairs))
+        self.lo, self.hi = 0, self.n_pairs  # the pairs a step scores (a rank's shard at N > 1)
+        self.shard = None  # (rank, world) when sharded
         t = time.perf_counter()
         self.step()  # the first scoring call (code objects load, staging and heavy tiles built)
         mark("first_call")
         self.t_stages = st
         self.t_setup = sum(st.values())
+
+    def set_shard(self, rank: int, world: int, lo: int, hi: int, out=None) -> None:
+        """Steps score pairs [lo, hi) only (rank `rank`'s shard of `world`), into `out` (full-length arrays,
+        e.g. the shared result buffer) or this workload's pinned arrays."""
+        self.shard = (rank, world)
+        self.lo, self.hi = int(lo), int(hi)
+        if out is not None:
+            self.out = out
+
+    def refresh_device_list(self) -> None:
+        """After something re-enumerated the resident list on this engine (ShardedStep does)."""
+        self.pa, self.pb, n = self.eng.candidates_device()
+        assert n == self.n_pairs
+
+    @property
+    def profile_key(self) -> str:
+        """The workload name the committed PMC summaries use (a shard: "<name>/shard<r>of<N>")."""
+        return self.name if self.shard is None else f"{self.name}/shard{self.shard[0]}of{self.shard[1]}"
+
+    def close(self) -> None:
+        self.eng.close()
 
     def lens(self) -> np.ndarray:
         return np.fromiter((len(r) for r in self.reads), dtype=np.int64, count=len(self.reads))
@@ -272,8 +313,14 @@ class Workload:
         return algorithmic_bytes(self.lens(), self.a, self.b)
 
     def step(self) -> None:
-        """The metric's step: resident list -> kernels -> (score, end) in pinned host memory."""
-        self.eng.score_candidates(10, -1, self.indel, self.band, out=self.out)
+        """The metric's step: resident list -> kernels -> (score, end) in pinned host memory (a shard: its
+        range of the list into its slice of the arrays)."""
+        if self.lo == 0 and self.hi == self.n_pairs:
+            self.eng.score_candidates(10, -1, self.indel, self.band, out=self.out)
+        elif self.hi > self.lo:
+            lo, hi = self.lo, self.hi
+            self.eng.score_candidates_range(lo, hi, 10, -1, self.indel, self.band,
+                                            out=(self.out[0][lo:hi], self.out[1][lo:hi]))
 
     def launch(self, stream) -> None:
         """Kernel only (device outputs), on `stream`: the dominant kernel's timing for the roofline."""
@@ -517,7 +564,7 @@ def sharded_band_sweep(world: int, rank: int, dev, eng, bands, indel: int, steps
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
         ok = None
-        if rank == 0 and band == bands[0]:
+        if rank == 0:
             got = st.results()
             ref = eng.score_candidates(10, -1, indel, band)
             ok = bool(np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]))
@@ -526,22 +573,36 @@ def sharded_band_sweep(world: int, rank: int, dev, eng, bands, indel: int, steps
                               "pairs_per_s": st.n_pairs * steps / el,
                               **({"matches_single_gpu": ok} if ok is not None else {})})
         st.close()
+    out["what"] = (f"BASELINE configs[4] over {world} ranks: cfg5's one list sharded by sum n*m, each rank's "
+                   f"(score, end) into rank 0's shared pinned host buffer; band -1 = the reference's full DP, "
+                   f"band >= 0 the seed-and-extend knob (no reference mode); every point checked against rank 0 "
+                   f"alone scoring the whole list")
     return out
 
 
-def single_process_all_gpus(rank: int, reads, k: int, steps: int, eng):
-    """The reference's own shape on the whole node: ONE process, one context over every visible GPU
-    (ovl_create over the device list), the same list scored with each GPU storing its
+def single_process_all_gpus(rank: int, world: int, shared: bool, reads, k: int, steps: int, eng):
+    """The reference's own shape on the job's GPUs: ONE process, one context over the `world` GPUs of the
+    ranks (ovl_create over the device list), the same list scored with each GPU storing its
     shard of (score, end) straight into the caller's pinned arrays.  Rank 0 runs it alone while the other
-    ranks wait; checked against rank 0's one-GPU engine."""
-    import torch
+    ranks wait; checked against rank 0's one-GPU engine.  When ranks share GPUs (a one-GPU rehearsal) the
+    context lists GPU 0 `world` times (OVL_SHARE_DEVICES=1: one shard slot each)."""
     from ovlgraph import OverlapEngine
     from ovlgraph.hostmem import pinned_empty
     if rank != 0:
         return None
-    ids = list(range(torch.cuda.device_count()))
+    ids = [0] * world if shared else list(range(world))
+    saved = os.environ.get("OVL_SHARE_DEVICES")
+    if shared:
+        os.environ["OVL_SHARE_DEVICES"] = "1"
     t0 = time.perf_counter()
-    multi = OverlapEngine(devices=ids)
+    try:
+        multi = OverlapEngine(devices=ids)
+    finally:
+        if shared:
+            if saved is None:
+                os.environ.pop("OVL_SHARE_DEVICES", None)
+            else:
+                os.environ["OVL_SHARE_DEVICES"] = saved
     multi.set_reads(reads)
     n = multi.enumerate_candidates(k)
     setup = time.perf_counter() - t0
@@ -558,8 +619,8 @@ def single_process_all_gpus(rank: int, reads, k: int, steps: int, eng):
     ok = bool(np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1]))
     multi.close()
     return {"devices": ids, "pairs": n, "ms_per_step": el / steps * 1e3, "pairs_per_s": n * steps / el,
-            "setup_s": round(setup, 2), "matches_single_gpu": ok,
-            "what": "one process, OverlapEngine(devices=all visible): shards by sum n*m, each GPU's kernels "
+            "setup_s": round(setup, 2), "matches_single_gpu": ok, "devices_shared": shared,
+            "what": "one process, OverlapEngine(devices=[the job's GPUs]): shards by sum n*m, each GPU's kernels "
                     "store its slice into the caller's pinned arrays (no collective)"}
 
 
@@ -596,8 +657,8 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
     pairs and §8d algorithmic bytes per launch (the launch's own pair range), HBM fraction.  Returns
     (roofline of the dominant in-step kernel, per-sink table, step-level roofline)."""
     lens = w.lens()
-    cum = np.zeros(w.n_pairs + 1, dtype=np.int64)
-    np.cumsum(pair_bytes(lens, w.a, w.b), out=cum[1:])
+    cum = np.zeros(w.hi - w.lo + 1, dtype=np.int64)
+    np.cumsum(pair_bytes(lens, w.a[w.lo:w.hi], w.b[w.lo:w.hi]), out=cum[1:])
     w.eng.set_timing(True)
     runs = []
     for _ in range(reps):
@@ -633,12 +694,18 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
                       "first_launch_ms": float(np.median(d["first"])) if d["first"] else None,
                       "pairs_per_launch": pairs, "algorithmic_bytes_per_launch": byts, "achieved_gbs": ach,
                       "frac": ach / HBM_PEAK_GBS, "ms_per_step": ms_all * launches})
+    if not table:  # an empty shard launches nothing
+        return None, [], None
     # the dominant in-step kernel: the one that scores most of the step's pairs (the packed chunks); the
     # table beside it has every in-step kernel with its own fraction
     dom = max(table, key=lambda t: t["pairs_per_launch"] * t["launches_per_step"])
-    traffic = load_traffic(w.name, dom["kernel"])
+    if w.shard is None:
+        traffic, tsrc = load_traffic(w.name, dom["kernel"]), "pmc"
+    else:
+        traffic, tsrc = shard_traffic(w.profile_key, w.name, dom["kernel"], dom["pairs_per_launch"])
     roof = {"bound": "hbm", "achieved": dom["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": dom["frac"], "traffic": traffic, "kernel": dom["kernel"], "launch_ms": dom["launch_ms"],
+            "frac": dom["frac"], "traffic": traffic, "traffic_source": tsrc, "kernel": dom["kernel"],
+            "launch_ms": dom["launch_ms"],
             "pairs_per_launch": dom["pairs_per_launch"],
             "algorithmic_bytes_per_launch": dom["algorithmic_bytes_per_launch"],
             "launches_per_step": dom["launches_per_step"],
@@ -709,12 +776,15 @@ def gather_floats(vals, world: int, dev, backend: str):
     return [r.cpu().tolist() for r in rows]
 
 
+def max_over_ranks(el: float, world: int, dev, backend: str) -> float:
+    return max(r[0] for r in gather_floats([el], world, dev, backend))
+
+
 def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: int, warmup: int):
     """One read set of `name`, its candidate list sharded by sum n*m over the ranks, every rank's results into
     rank 0's shared pinned host buffer (ShardedStep, dest="host"); then rank 0 alone scores the whole list
     on its GPU (the one-GPU time of the same workload, same run) while the others wait; parity of the
     gathered result against that."""
-    import torch
     import torch.distributed as dist
     from ovlgraph import OverlapEngine
     from ovlgraph.candidates import dedup_reads
@@ -727,7 +797,7 @@ def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: i
     st = ShardedStep(reads, k=CONFIGS[name]["k"], engine=eng, dest="host")
     setup = time.perf_counter() - t0
     el = timed_steps(st.step, steps, warmup, dev, world)
-    el_max = max(r[0] for r in gather_floats([el], world, dev, backend))
+    el_max = max_over_ranks(el, world, dev, backend)
     one = None
     ok = None
     if rank == 0:
@@ -746,11 +816,157 @@ def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: i
             "speedup_vs_one_gpu": one / el_max, "matches_one_gpu": ok, "setup_s": round(setup, 2),
             "scaling": "strong",
             "what": "one shared list sharded by sum n*m, each rank's (score, end) into rank 0's shared pinned host "
-                    "buffer; one_gpu: rank 0 alone scores the whole list in the same run (others idle)"}
+                    "buffer (step fence in shared memory); one_gpu: rank 0 alone scores the whole list in the "
+                    "same run (others idle)"}
+
+
+GATHER_DESC = ("dest=host: every rank's kernels store its shard's (score, end) over its own GPU's PCIe link "
+               "straight into its slice of one pinned host buffer that rank 0 owns (POSIX shared memory, each "
+               "rank pins its pages); a step fence of per-rank counters in the buffer's header page orders the "
+               "steps (rank 0 returns when every slice has landed; no collective per step); SURVEY §8e's "
+               "per-device D2H into pinned host slices")
+
+
+def sharded_list(name: str, world: int, rank: int, dev, backend: str, args):
+    """The N > 1 headline (north_star: candidate pairs sharded across the GPUs): ONE read set of the workload
+    (seed args.seed on every rank, so every rank holds the same reads and enumerates the same list), its
+    candidate list sharded by sum n*m, every rank's (score, end) into rank 0's shared pinned host buffer.
+    Also: rank 0's in-step rooflines on its shard (every rank times its own shard at the same time), the
+    whole list scored by rank 0's GPU alone in the same run, parity of the gathered results against that,
+    and the same shards gathered into rank 0's HBM by dist.gather (RCCL send/recv over xGMI) instead."""
+    import torch.distributed as dist
+    from ovlgraph.hostmem import pinned_empty
+    from ovlgraph.sharded import ShardedStep
+    t0 = time.perf_counter()
+    w = Workload(name, seed=args.seed, dev=dev)
+    st = ShardedStep(w.reads, k=w.cfg["k"], engine=w.eng, dest="host")
+    assert st.n_pairs == w.n_pairs
+    w.refresh_device_list()
+    w.set_shard(rank, world, st.lo, st.hi, out=(st.shared.score, st.shared.end))
+    setup = time.perf_counter() - t0
+    el = timed_steps(st.step, args.steps, args.warmup, dev, world)
+    rows = gather_floats([el, st.hi - st.lo], world, dev, backend)
+    el_max = max(r[0] for r in rows)
+    # every rank's in-step launches at once (each its own shard, as in the step); rank 0 reports its own
+    roof, table, step_roof = in_step_rooflines(w, el / args.steps * 1e3)
+    dist.barrier()
+    st.step()  # one fenced step: rank 0's buffer holds every slice of it
+    one = ok = None
+    if rank == 0:
+        got = st.results()
+        out = (pinned_empty(w.n_pairs), pinned_empty(w.n_pairs))
+        one = timed_steps(lambda: w.eng.score_candidates(out=out), args.steps, args.warmup, dev, 1)
+        ok = bool(np.array_equal(got[0], out[0]) and np.array_equal(got[1], out[1]))
+    dist.barrier()
+    w.out = w.own_out  # drop the views of the shared buffer, so that it can be unmapped and unlinked
+    st.close()
+    # the same shards gathered by a collective into rank 0's HBM (north_star's "RCCL gather"); results end on
+    # rank 0's GPU, not in host memory, so this is not the metric's step
+    g = ShardedStep(w.reads, k=w.cfg["k"], engine=w.eng, dest="rank0")
+    el_g = max_over_ranks(timed_steps(g.step, args.steps, args.warmup, dev, world), world, dev, backend)
+    g_ok = None
+    if rank == 0:
+        got = g.results()
+        g_ok = bool(np.array_equal(got[0], out[0]) and np.array_equal(got[1], out[1]))
+    g.close()
+    w.refresh_device_list()
+    res = {"w": w, "el_max": el_max, "pairs_per_rank": [int(r[1]) for r in rows],
+           "per_rank_ms_per_step": [r[0] / args.steps * 1e3 for r in rows],
+           "roofline": roof, "in_step_kernels": table, "step_roofline": step_roof, "setup_s": round(setup, 2)}
+    if rank == 0:
+        res.update(one_gpu_ms_per_step=one / args.steps * 1e3, one_gpu_pairs_per_s=w.n_pairs * args.steps / one,
+                   speedup_vs_one_gpu=one / el_max, matches_one_gpu=ok,
+                   rccl_gather={"dest": "rank0", "backend": backend, "ms_per_step": el_g / args.steps * 1e3,
+                                "pairs_per_s": w.n_pairs * args.steps / el_g, "matches_one_gpu": g_ok,
+                                "bytes_per_step": g.gather_bytes(),
+                                "what": "the same shards scored into each rank's HBM and collected by one "
+                                        "dist.gather to rank 0 (RCCL send/recv over xGMI on backend nccl; over "
+                                        "gloo when ranks share a GPU); results end in rank 0's HBM, not in host "
+                                        "memory, so not the metric's step"})
+    return res
+
+
+def weak_scaling(name: str, world: int, rank: int, dev, backend: str, args):
+    """Every rank its own read set of the workload (seed + rank): independent graph builds side by side, the
+    reference's joblib shape (experiments.py:537); no data-path collective."""
+    w = Workload(name, seed=args.seed + rank, dev=dev)
+    el = timed_steps(w.step, args.steps, args.warmup, dev, world)
+    rows = gather_floats([el, w.n_pairs, len(w.reads)], world, dev, backend)
+    w.close()
+    if rank != 0:
+        return None
+    el_max = max(r[0] for r in rows)
+    pairs = [int(r[1]) for r in rows]
+    return {"value": sum(pairs) * args.steps / el_max, "unit": "overlap-pairs/s", "scaling": "weak",
+            "ms_per_step": el_max / args.steps * 1e3, "pairs": sum(pairs), "pairs_per_rank": pairs,
+            "reads_per_rank": [int(r[2]) for r in rows], "seeds": [args.seed + r for r in range(world)],
+            "per_rank_ms_per_step": [r[0] / args.steps * 1e3 for r in rows],
+            "what": f"x{world} weak: every rank scores its own read set's device-enumerated list into its own "
+                    f"pinned host arrays (graph builds side by side, as the reference's joblib workers, "
+                    f"experiments.py:537); no data-path collective"}
+
+
+def multi_line(args, world: int, ident: dict, top: dict, extras: dict) -> dict:
+    """Rank 0's N > 1 line: the sharded list at the top, the secondary shapes beside it.  `top` holds the
+    measurements of sharded_list (or None-valued placeholders in a dry run)."""
+    name = args.config or "target"
+    w = top.get("w")
+    pairs = w.n_pairs if w is not None else None
+    el = top.get("el_max")
+    line = {
+        "metric": METRIC, "value": pairs * args.steps / el if el else None, "unit": "overlap-pairs/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3 if el else None,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+        "config": {"workload": f"{name}: {WORKLOAD_DESC[name]}", "reads": len(w.reads) if w is not None else None,
+                   "pairs": pairs, "pairs_per_rank": top.get("pairs_per_rank"), "seed": args.seed,
+                   "read_length": w.cfg["l"] if w is not None else None,
+                   "parallelism": f"pair-sharded x{world}: one process per GPU, one read set and its "
+                                  f"device-enumerated candidate list on every rank, contiguous shards balanced by "
+                                  f"sum n*m, each rank's results into rank 0's shared pinned host buffer",
+                   "kernel": w.kernel if w is not None else None,
+                   "scoring": {"match": 10, "mismatch": -1, "indel": w.indel if w is not None else None, "band": -1}},
+        **ident,
+        "gather": {"dest": "host", "fence": "shm", "bytes_per_step": 8 * pairs if pairs else None,
+                   "what": GATHER_DESC},
+        "one_gpu_ms_per_step": top.get("one_gpu_ms_per_step"),
+        "one_gpu_pairs_per_s": top.get("one_gpu_pairs_per_s"),
+        "speedup_vs_one_gpu": top.get("speedup_vs_one_gpu"),
+        "matches_one_gpu": top.get("matches_one_gpu"),
+        "per_rank_ms_per_step": top.get("per_rank_ms_per_step"),
+        "roofline": top.get("roofline"),
+        "in_step_kernels": top.get("in_step_kernels"),
+        "step_roofline": top.get("step_roofline"),
+        "rccl_gather": top.get("rccl_gather"),
+        "setup_s": top.get("setup_s"),
+        "cpu_baseline": None,
+        "cpu_baseline_note": "the CPU baseline runs on rank 0 at N = 1 only (bench contract); see the N = 1 line",
+    }
+    if line["roofline"] is not None:
+        line["roofline"]["what"] = "rank 0's shard: " + line["roofline"]["what"]
+    line.update(extras)
+    return line
+
+
+def extra_plan(args, world: int):
+    """The secondary N > 1 measurements this run makes, in order (empty with --no-extra)."""
+    if args.no_extra:
+        return []
+    name = args.config or "target"
+    plan = ["weak_scaling"]
+    if name != "cfg4":
+        plan.append("cfg4_strong")  # BASELINE configs[3]: 8x pair-sharded
+    if name != "cfg5":
+        plan.append("cfg5_sharded_band_sweep")  # BASELINE configs[4]: the band sweep across the ranks (4x)
+    plan.append("single_process_all_gpus")  # the reference's own shape: one process over the job's GPUs
+    return plan
+
+
+SHARDED_SWEEP_BANDS = [4, 8, 16, 32, 64, -1]
 
 
 def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
-    """N > 1: every rank runs the same workload (weak: its own read set; strong: a shard of one list)."""
+    """N > 1: the workload's one list sharded over the ranks (the line's value), then the secondary shapes."""
     import torch
     import torch.distributed as dist
     name = args.config or "target"
@@ -760,63 +976,22 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
     if shared:
         ident["note"] = ("more ranks than visible GPUs: ranks share devices (flow rehearsal, gloo barriers) -- "
                          "not a scaling number")
-    if args.scaling == "strong":
-        res = strong_scaling(name, world, rank, dev, backend, args.steps, args.warmup)
-        if rank != 0:
-            return None
-        return {"metric": METRIC, "value": res["pairs_per_s"], "unit": "overlap-pairs/s", "n_gpus": world,
-                "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
-                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "int32",
-                "data": "synthetic",
-                "config": {"workload": res["workload"], "reads": res["reads"], "pairs": res["pairs"],
-                           "parallelism": f"pair-sharded x{world}: one process per GPU, one shared device-enumerated "
-                                          f"list, shards balanced by sum n*m, results into rank 0's shared pinned "
-                                          f"host buffer"},
-                **ident, "one_gpu_ms_per_step": res["one_gpu_ms_per_step"],
-                "speedup_vs_one_gpu": res["speedup_vs_one_gpu"], "matches_one_gpu": res["matches_one_gpu"],
-                "roofline": None, "cpu_baseline": None,
-                "cpu_baseline_note": "the CPU baseline runs on rank 0 at N = 1 only (bench contract)"}
-    # weak: every rank its own read set of the workload
-    w = Workload(name, seed=args.seed + rank, dev=dev)
-    el = timed_steps(w.step, args.steps, args.warmup, dev, world)
-    roof, table, step_roof = in_step_rooflines(w, el / args.steps * 1e3)
-    kms = kernel_timing(w, max(args.steps, 20), dev)
-    rows = gather_floats([el, w.n_pairs, len(w.reads), kms], world, dev, backend)
-    el_max = max(r[0] for r in rows)
-    pairs = [int(r[1]) for r in rows]
-    strong = None
-    if not args.no_extra:
-        strong = strong_scaling("cfg4", world, rank, dev, backend, max(5, args.steps // 2), 2)
-    if rank != 0:
-        return None
-    total = sum(pairs)
-    algo = w.algo_bytes()
-    ach = algo / (kms * 1e-3) / 1e9
-    line = {
-        "metric": METRIC, "value": total * args.steps / el_max, "unit": "overlap-pairs/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el_max / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-        "config": {"workload": f"{name}: {WORKLOAD_DESC[name]}", "pairs": total, "pairs_per_rank": pairs,
-                   "reads_per_rank": [int(r[2]) for r in rows], "read_length": w.cfg["l"],
-                   "seeds": [args.seed + r for r in range(world)],
-                   "parallelism": f"x{world} weak: one process per GPU, each scoring its own read set's "
-                                  f"device-enumerated list (graph builds side by side, as the reference's joblib "
-                                  f"workers), results into each rank's pinned host arrays; no data-path collective",
-                   "kernel": w.kernel, "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band}},
-        **ident,
-        "per_rank_ms_per_step": [r[0] / args.steps * 1e3 for r in rows],
-        "roofline": roof,
-        "in_step_kernels": table,
-        "step_roofline": step_roof,
-        "kernel_only_roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": ach / HBM_PEAK_GBS, "kernel_ms": max(r[3] for r in rows),
-                                 "algorithmic_bytes_per_launch": algo, "traffic": load_traffic(name, kernel_name(w, 0, w.n_pairs)),
-                                 "what": "rank 0's list through the HBM-output kernel alone (not in the step)"},
-        "cpu_baseline": None,
-        "cpu_baseline_note": "the CPU baseline runs on rank 0 at N = 1 only (bench contract); see the N = 1 line",
-    }
-    if strong is not None:
-        line["cfg4_strong_scaling"] = strong
+    top = sharded_list(name, world, rank, dev, backend, args)
+    w = top["w"]
+    extras = {}
+    for item in extra_plan(args, world):
+        if item == "weak_scaling":
+            extras[item] = weak_scaling(name, world, rank, dev, backend, args)
+        elif item == "cfg4_strong":
+            extras[item] = strong_scaling("cfg4", world, rank, dev, backend, max(5, args.steps // 2), 2)
+        elif item == "cfg5_sharded_band_sweep":
+            extras[item] = sharded_band_sweep(world, rank, dev, w.eng, SHARDED_SWEEP_BANDS, args.sweep_indel, 3,
+                                              backend)
+        elif item == "single_process_all_gpus":
+            extras[item] = single_process_all_gpus(rank, world, shared, w.reads, w.cfg["k"], args.steps, w.eng)
+        dist.barrier()
+    line = multi_line(args, world, ident, top, extras) if rank == 0 else None
+    w.close()
     return line
 
 
@@ -876,9 +1051,8 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default=None, choices=sorted(WORKLOAD_DESC),
                     help="workload at every N (default: the north_star target point)")
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="N > 1: weak = a read set per rank, strong = one list sharded over the ranks")
-    ap.add_argument("--seed", type=int, default=0, help="read-set seed (weak scaling: rank r uses seed + r)")
+    ap.add_argument("--seed", type=int, default=0,
+                    help="read-set seed (the secondary weak-scaling field: rank r uses seed + r)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra configs and stages")
     ap.add_argument("--no-numa-bind", action="store_true",
@@ -897,6 +1071,9 @@ def parse_args(argv=None):
     # multi-process line's collectives, gathers and sharded step for real (tests/test_gpu_bench_dist.py)
     ap.add_argument("--dist-path", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    # profiling aid at N = 1: time only shard R of N of the list (what rank R scores at N ranks), so rocprofv3 and
+    # PMC passes on a one-GPU box see a rank's launches (tools/gpu_r04_shard_profile.sh)
+    ap.add_argument("--shard", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -919,7 +1096,9 @@ def launch_plan(gpus: int, env) -> str:
 
 
 def dry_run(args) -> int:
-    """The launch path alone (no GPU): join the process group over gloo, report what the ranks saw."""
+    """The launch path alone (no GPU): join the process group over gloo and print the line rank 0 would print,
+    built by the same code (multi_line) with every measurement left null, so the launcher tests see which
+    fields and secondary shapes a run at this N carries."""
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -930,9 +1109,11 @@ def dry_run(args) -> int:
     if world > 1:
         dist.barrier()
     if rank == 0:
-        print(json.dumps({"n_gpus": args.gpus, "world_size": dist.get_world_size() if world > 1 else 1,
-                          "backend": dist.get_backend() if world > 1 else None, "config": args.config,
-                          "scaling": args.scaling, "steps": args.steps, "warmup": args.warmup}), flush=True)
+        ident = {"world_size": dist.get_world_size() if world > 1 else 1,
+                 "backend": dist.get_backend() if world > 1 else None}
+        line = multi_line(args, world, ident, {}, {k: None for k in extra_plan(args, world)})
+        line["dry_run"] = True
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
@@ -990,9 +1171,18 @@ def main() -> int:
 
     name = args.config or "target"
     w = Workload(name, seed=args.seed, dev=dev, indel=args.indel, band=args.band)
+    if args.shard:
+        r, n = (int(x) for x in args.shard.split("/"))
+        cuts = w.eng.candidate_shards(n)
+        w.set_shard(r, n, cuts[r], cuts[r + 1])
     elapsed = timed_steps(w.step, args.steps, args.warmup, dev, 1)
     ms_step = elapsed / args.steps * 1e3
     roof, table, step_roof = in_step_rooflines(w, ms_step)
+    if args.shard:
+        print(json.dumps({"shard": args.shard, "workload": w.profile_key, "pairs": w.hi - w.lo,
+                          "ms_per_step": ms_step, "pairs_per_s": (w.hi - w.lo) * args.steps / elapsed,
+                          "roofline": roof, "in_step_kernels": table, "step_roofline": step_roof}), flush=True)
+        return 0
     kernel_ms = kernel_timing(w, max(args.steps, 20), dev)
     algo = w.algo_bytes()
     achieved = algo / (kernel_ms * 1e-3) / 1e9
@@ -1006,7 +1196,7 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",

@@ -4,12 +4,13 @@ SURVEY.md §8e: pairs are independent, so each rank scores a contiguous range of
 the ordered candidate list (balanced by Σ len(a)·len(b)) with no exchange during
 compute.  The results are gathered to ONE destination, in reference order:
 
-* ``dest="host"`` (the default of ``ShardedStep``): every rank DMA-copies its
-  ``(score, end)`` slice from its GPU straight into a shared host buffer that
-  rank 0 owns (POSIX shared memory, pinned per rank with ``ovl_host_register``).
-  Each GPU uses its own PCIe link, so the copies run in parallel; no collective
-  moves data, only a barrier orders the step.  This is SURVEY.md §8e's "per-device
-  D2H into pinned host slices".
+* ``dest="host"`` (the default of ``ShardedStep``): every rank's kernels store its
+  ``(score, end)`` slice straight into a shared host buffer that rank 0 owns (POSIX
+  shared memory, pinned per rank with ``ovl_host_register``).  Each GPU uses its own
+  PCIe link, so the slices land in parallel; no collective moves data, and a step
+  fence of a few cache lines in the buffer's header orders the steps (rank 0 waits
+  for every rank's published step number).  This is SURVEY.md §8e's "per-device D2H
+  into pinned host slices".
 * ``dest="rank0"``: the slices stay in HBM and one ``dist.gather`` (RCCL
   send/recv over xGMI on backend "nccl", gloo on CPU) collects them on rank 0's GPU.
 
@@ -123,8 +124,15 @@ class SharedResults:
     """A (score, end) host buffer of n pairs shared by the ranks of one node (POSIX shm).
 
     Rank 0 creates it, the others attach by name; each rank pins only the pages of its own
-    slices (``ovl_host_register``), so its GPU's D2H copies land in place.
+    slices (``ovl_host_register``), so its GPU's stores land in place.  A header page ahead of
+    the two columns holds the step fence (``publish`` / ``wait_all`` / ``release`` /
+    ``wait_released``): one int64 counter per rank, each on its own 64-byte line and written by
+    that rank only, plus rank 0's release counter.
     """
+
+    LINE = 64
+    PAGE = 4096
+    TIMEOUT_S = 300.0
 
     def __init__(self, n_pairs: int, group=None, tag: str = ""):
         import torch.distributed as dist
@@ -133,11 +141,14 @@ class SharedResults:
         global _shm_seq
         self.n = int(n_pairs)
         self.rank = dist.get_rank(group)
-        size = max(8, 8 * self.n)
+        self.world = dist.get_world_size(group)
+        self.hdr_bytes = -(-self.LINE * (self.world + 1) // self.PAGE) * self.PAGE
+        size = self.hdr_bytes + max(8, 8 * self.n)
         _shm_seq += 1  # several buffers may be alive at once (one per ShardedStep)
         name = [f"ovl_{os.getpid()}_{_shm_seq}_{tag}"[:30] if self.rank == 0 else None]
         if self.rank == 0:
             self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=size)
+            self.shm.buf[: self.hdr_bytes] = bytes(self.hdr_bytes)
         dist.broadcast_object_list(name, src=0, group=group)
         if self.rank != 0:
             self.shm = shared_memory.SharedMemory(name=name[0], create=False)
@@ -146,10 +157,45 @@ class SharedResults:
                 resource_tracker.unregister(self.shm._name, "shared_memory")
             except Exception:
                 pass
-        self.buf = np.frombuffer(self.shm.buf, dtype=np.int32, count=2 * self.n)
+        stride = self.LINE // 8
+        self.hdr = np.frombuffer(self.shm.buf, dtype=np.int64, count=self.hdr_bytes // 8)
+        self.done = self.hdr[: stride * self.world: stride]  # done[r]: the last step rank r published
+        self.released = self.hdr[stride * self.world: stride * self.world + 1]  # rank 0: last step consumed
+        self.buf = np.frombuffer(self.shm.buf, dtype=np.int32, count=2 * self.n, offset=self.hdr_bytes)
         self.score = self.buf[: self.n]
         self.end = self.buf[self.n:]
         self._pinned: List[int] = []
+
+    # ---- the step fence: no collective, a few cache lines of shared host memory
+    def publish(self, step: int) -> None:
+        """This rank's slice of `step` is in the buffer (its scoring call has returned)."""
+        self.done[self.rank] = step
+
+    def _spin(self, ready, what: str) -> None:
+        import time
+        if ready():
+            return
+        t0 = time.perf_counter()
+        spins = 0
+        while not ready():
+            spins += 1
+            if spins > 2000:  # ~a few hundred microseconds of tight polling, then yield the CPU
+                time.sleep(20e-6)
+                if time.perf_counter() - t0 > self.TIMEOUT_S:
+                    raise RuntimeError(f"shared results: timed out waiting for {what} "
+                                       f"(done={self.done.tolist()}, released={int(self.released[0])})")
+
+    def wait_all(self, step: int) -> None:
+        """Rank 0: until every rank has published `step` (every slice has landed)."""
+        self._spin(lambda: int(self.done.min()) >= step, f"every rank's step {step}")
+
+    def release(self, step: int) -> None:
+        """Rank 0: it is done reading the results of `step`; ranks may overwrite them."""
+        self.released[0] = step
+
+    def wait_released(self, step: int) -> None:
+        """Ranks > 0: until rank 0 has released `step` (before writing over its results)."""
+        self._spin(lambda: int(self.released[0]) >= step, f"rank 0 to release step {step}")
 
     def pin(self, lo: int, hi: int) -> None:
         """Pin the pages that hold pairs [lo, hi) of both columns in this process."""
@@ -175,7 +221,7 @@ class SharedResults:
             for s in self._pinned:
                 L.ovl_host_unregister(ctypes.c_void_p(s))
             self._pinned = []
-        self.score = self.end = self.buf = None
+        self.score = self.end = self.buf = self.hdr = self.done = self.released = None
         try:
             self.shm.close()
         except BufferError:
@@ -195,8 +241,15 @@ class ShardedStep:
     Σ n·m-balanced shard, the scoring (``match``, ``mismatch``, ``indel``, ``band``) and the
     destination.  ``step()`` scores the shard and gathers:
 
-    * ``dest="host"``: the shard's results DMA into rank 0's shared host arrays; ``step()``
-      returns after this rank's copies are done and a barrier (every slice has landed);
+    * ``dest="host"``: the shard's results land in rank 0's shared host arrays (the kernels
+      store into the rank's pinned slice).  On rank 0 ``step()`` returns once every slice of
+      this step has landed; on the other ranks once their own slice has.  The order comes from
+      the step fence in the buffer's header page (``fence="shm"``, the default): each rank
+      publishes its step number after its call returns, rank 0 waits for all of them, and a
+      rank writes step k only after rank 0 has called step k (so it is done reading step
+      k - 1).  No collective runs per step.  ``fence="barrier"`` puts a ``dist.barrier`` after
+      every step instead (the round-3 form; a barrier over RCCL costs tens of microseconds,
+      about what a shard of the target list takes to score at N = 8);
     * ``dest="rank0"``: the shard's results stay in HBM and ``dist.gather`` collects them on
       rank 0 (RCCL send/recv on "nccl").
 
@@ -207,12 +260,16 @@ class ShardedStep:
     def __init__(self, reads: Sequence[str], a_idx=None, b_idx=None, k: Optional[int] = None,
                  match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT, group=None,
                  engine: Optional[OverlapEngine] = None, local_scorer: Optional[Callable] = None,
-                 dest: str = "host", balance: bool = True, band: int = -1):
+                 dest: str = "host", balance: bool = True, band: int = -1, fence: str = "shm"):
         import torch
         import torch.distributed as dist
 
         if dest not in ("host", "rank0"):
             raise ValueError("dest must be 'host' or 'rank0'")
+        if fence not in ("shm", "barrier"):
+            raise ValueError("fence must be 'shm' or 'barrier'")
+        self.fence = fence
+        self.steps = 0
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -286,6 +343,13 @@ class ShardedStep:
 
         lo, hi = self.lo, self.hi
         if self.dest == "host":
+            self.steps += 1
+            k = self.steps
+            if self.fence == "shm":
+                if self.rank == 0:
+                    self.shared.release(k - 1)  # rank 0 is done with step k - 1's results
+                else:
+                    self.shared.wait_released(k - 1)
             if hi > lo:
                 out = (self.shared.score[lo:hi], self.shared.end[lo:hi])
                 if self.eng is None:
@@ -296,7 +360,12 @@ class ShardedStep:
                     self.eng.score_candidates_range(lo, hi, *self.scoring, out=out)
                 else:
                     self.eng.score(self.a[lo:hi], self.b[lo:hi], *self.scoring, out=out)
-            dist.barrier(group=self.group)
+            if self.fence == "barrier":
+                dist.barrier(group=self.group)
+                return
+            self.shared.publish(k)
+            if self.rank == 0:
+                self.shared.wait_all(k)
             return
         if self._launch is not None:
             self._launch()
@@ -329,6 +398,8 @@ class ShardedStep:
     def close(self) -> None:
         import torch.distributed as dist
         if self.shared is not None:
+            if self.fence == "shm" and self.rank == 0:
+                self.shared.release(self.steps)
             dist.barrier(group=self.group)  # rank 0 unlinks only after every rank is done
             self.shared.close()
             self.shared = None

@@ -35,21 +35,49 @@ def test_launch_plan():
 
 def test_args_defaults():
     a = bench.parse_args([])
-    assert (a.gpus, a.config, a.scaling, a.seed) == (1, None, "weak", 0)
+    assert (a.gpus, a.config, a.seed) == (1, None, 0)
     with pytest.raises(SystemExit):
         bench.parse_args(["--gpus", "0"])
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_spawn_runs_n_ranks(n):
-    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--config", "cfg4", "--steps", "7", "--dry-run"],
+def _dry(n, *extra):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--steps", "7", "--dry-run", *extra],
                        capture_output=True, text=True, timeout=240, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # one JSON line, from rank 0 only
-    got = json.loads(lines[0])
-    assert got == {"n_gpus": n, "world_size": n, "backend": "gloo", "config": "cfg4", "scaling": "weak",
-                   "steps": 7, "warmup": 5}
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_spawn_runs_n_ranks(n):
+    got = _dry(n, "--config", "cfg4")
+    assert (got["n_gpus"], got["world_size"], got["backend"], got["steps"], got["warmup"]) == (n, n, "gloo", 7, 5)
+    assert got["dry_run"] is True and got["config"]["workload"].startswith("cfg4")
+
+
+def test_n2_line_is_the_sharded_target_list():
+    """at N > 1 the line's value is the north_star target list sharded over the ranks (strong
+    scaling against the N = 1 line's list), with the same-run one-GPU time, parity flag, rank 0's roofline and
+    the gather used; the weak shape, cfg4 pair-sharded and the cfg5 band sweep sharded ride beside it."""
+    got = _dry(2)
+    assert got["metric"] == bench.METRIC and got["unit"] == "overlap-pairs/s" and got["scaling"] == "strong"
+    assert got["config"]["workload"].startswith("target: PhiX N=50000 l=100")
+    assert "pair-sharded x2" in got["config"]["parallelism"]
+    for k in ("value", "ms_per_step", "one_gpu_ms_per_step", "speedup_vs_one_gpu", "matches_one_gpu", "roofline",
+              "in_step_kernels", "step_roofline", "per_rank_ms_per_step", "rccl_gather", "cpu_baseline"):
+        assert k in got, k
+    assert got["gather"]["dest"] == "host" and got["gather"]["fence"] == "shm"
+    assert set(("weak_scaling", "cfg4_strong", "cfg5_sharded_band_sweep", "single_process_all_gpus")) <= set(got)
+    # the secondary shapes are skipped with --no-extra, and a cfg4 run does not repeat cfg4 beside itself
+    assert not set(("weak_scaling", "cfg4_strong")) & set(_dry(2, "--no-extra"))
+    assert "cfg4_strong" not in _dry(2, "--config", "cfg4")
+
+
+def test_n1_and_n2_lines_share_metric_and_workload():
+    a = bench.parse_args([])
+    line = bench.multi_line(a, 1, {}, {}, {})
+    assert line["scaling"] == "strong" and line["config"]["workload"].startswith("target:")
 
 
 def test_failing_rank_fails_the_run():

@@ -1,7 +1,7 @@
 """bench.py's multi-process line on the one-GPU box: the N > 1 code path run at world size 1 over RCCL
 (--dist-path), so its collectives (all_gather of the per-rank times), the in-step rooflines, the weak-scaling
 line and the strong-scaling cfg4 shard (ShardedStep into rank 0's shared pinned buffer, checked against one
-GPU scoring the whole list) all run for real; and the strong line on its own."""
+GPU scoring the whole list) all run for real."""
 import json
 import os
 import subprocess
@@ -27,17 +27,20 @@ def _run(*args):
     return json.loads(lines[0])
 
 
-def test_weak_line_over_rccl_world1():
+def test_sharded_line_over_rccl_world1():
+    """The N > 1 line at world 1: the sharded list (one shard = the whole list) through ShardedStep and its step
+    fence, the RCCL gather variant, and every secondary shape, each checked against one GPU."""
     d = _run("--config", "cfg2", "--steps", "5", "--warmup", "1")
-    assert d["n_gpus"] == 1 and d["world_size"] == 1 and d["backend"] == "nccl" and d["scaling"] == "weak"
-    assert d["config"]["pairs_per_rank"] == [d["config"]["pairs"]] and d["value"] > 0
-    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    assert d["n_gpus"] == 1 and d["world_size"] == 1 and d["backend"] == "nccl" and d["scaling"] == "strong"
+    assert d["matches_one_gpu"] is True and d["one_gpu_ms_per_step"] > 0 and d["value"] > 0
+    assert d["config"]["pairs_per_rank"] == [d["config"]["pairs"]]
+    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1 and "traffic_source" in d["roofline"]
     assert d["in_step_kernels"] and d["step_roofline"]["frac"] > 0
-    s = d["cfg4_strong_scaling"]
+    assert d["rccl_gather"]["matches_one_gpu"] is True and d["rccl_gather"]["backend"] == "nccl"
+    assert d["weak_scaling"]["pairs_per_rank"] and d["weak_scaling"]["value"] > 0
+    s = d["cfg4_strong"]
     assert s["matches_one_gpu"] is True and s["pairs"] > 30_000_000 and s["speedup_vs_one_gpu"] > 0
-
-
-def test_strong_line_over_rccl_world1():
-    d = _run("--config", "cfg2", "--scaling", "strong", "--steps", "5", "--warmup", "1")
-    assert d["scaling"] == "strong" and d["world_size"] == 1 and d["matches_one_gpu"] is True
-    assert d["one_gpu_ms_per_step"] > 0 and d["value"] > 0
+    sw = d["cfg5_sharded_band_sweep"]
+    assert [p["band"] for p in sw["points"]] == [4, 8, 16, 32, 64, -1]
+    assert all(p["matches_single_gpu"] is True for p in sw["points"])
+    assert d["single_process_all_gpus"]["matches_single_gpu"] is True
