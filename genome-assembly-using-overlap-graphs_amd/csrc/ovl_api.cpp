@@ -71,41 +71,40 @@ struct DevBuf {
 
 thread_local std::string g_err;
 
-// Tuning / test knobs, read from the environment once per context.
+// Test knobs, read from the environment once per context: they force a kernel form or a transport that the
+// planner would otherwise pick by size or scoring, so the tests reach every form on small inputs.  (The A/B
+// knobs of rounds 1-3 -- lane split, copy-engine transfers, spin waits, ordinary-store expansion, grid cap, heavy
+// tiles, lane strip width and hand-off forms, read packing, pool spin, coarse-grained host memory -- are gone
+// with the forms they measured; DESIGN.md records each measurement.)
 struct Knobs {
-    int32_t split_override = -1;  // OVL_SPLIT env: force the lane split / latency mode, tuning only
     int32_t band_form = -1;       // OVL_BAND_FORM env (lane|diag|rows|fast|strip): band knob kernel (tests)
     int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
     int32_t dp_lane = -1;         // OVL_DP_LANE env: lane-per-pair full DP (-1 auto by list size, 0 off, 1 forced)
-    int32_t lane_cw = 32;         // OVL_LANE_CW env: lane kernel strip width (16 or 32 columns)
-    int64_t lane_min_pairs = 65536;  // OVL_LANE_MIN_PAIRS env: auto threshold (one tile per SIMD)
     int32_t lane_prof = 1;        // OVL_LANE_PROF=0: compare/select scores instead of the byte profile (tests)
-    int32_t lane_col16 = 1;       // OVL_LANE_COL16=0: int32 hand-off column even when int16 holds (tests)
-    int32_t lane_lds = 1;         // OVL_LANE_LDS=0: hand-off column in HBM even when the LDS form holds (tests)
     int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
-    int32_t blocks_per_cu = 32;   // OVL_BLOCKS_PER_CU env: ungapped grid cap (blocks of 256 per CU); 32: ~1 tile per
-                                  // wavefront at the target point, the dispatcher balances the tail (measured -2.3%)
-    int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic)
-    int32_t pipe_direct = 1;      // OVL_PIPE_DIRECT=0: copy-engine H2D / D2H transfers instead of kernels reading
-                                  // and storing host memory through its device mapping (A/B knob)
+    int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
     int32_t pack = 1;             // OVL_PACK=0: host-array results cross the link as int32 pairs even when the
-                                  // packed form (2 bytes per pair) holds (A/B knob)
+                                  // packed form (2 bytes per pair) holds (tests)
     int64_t pack_min = 1 << 18;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
-    int32_t pack_nt = 1;          // OVL_PACK_NT=0: the host expansion writes with ordinary stores (A/B knob)
-    int32_t spin_wait = 1;        // OVL_SPIN_WAIT=0: pipeline waits through hipEventSynchronize (A/B knob)
-    int32_t heavy_first = 1;      // OVL_HEAVY_FIRST=0: uniform_kernel tiles in list order (A/B knob)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
     int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
-                                  // instead of the compact encoding (encode_chunk; A/B knob)
-    int64_t compact_min = 1 << 16;  // OVL_PAIRS_COMPACT_MIN: compact encoding from this many pairs per call
+                                  // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
-                                  // instead of uniform_kernel reading b16 + tile deltas in place (A/B knob)
+                                  // instead of uniform_kernel reading b16 + tile deltas in place (tests)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
                                   // processes: 0 % 0.16-0.26 ms, 10 % 0.16-0.25, 18 % 0.157-0.226, 25 % 0.175-0.209)
 };
+
+// Lane-per-pair DP kernels from this many pairs per launch (one 64-pair tile per SIMD); below, a wavefront per pair
+constexpr int64_t kLaneMinPairs = 65536;
+// uniform_kernel grid cap, blocks of 256 per CU: ~1 tile per wavefront at the target point, the dispatcher
+// balances the tail (measured -2.3 % against 8 per CU; 16 / 32 / 64: 69.2 / 68.6 / 68.4 us)
+constexpr int64_t kBlocksPerCu = 32;
+// compact host pair lists from this many pairs per call
+constexpr int64_t kCompactMin = int64_t(1) << 16;
 
 }  // namespace
 
@@ -116,22 +115,15 @@ struct Dev {
     ovl_ctx* owner = nullptr;
     int32_t device = 0;
     hipStream_t stream = nullptr;  // kernels
-    hipStream_t s_in = nullptr;    // H2D copies of host-array calls
-    hipStream_t s_out = nullptr;   // D2H copies of host-array calls
+    hipStream_t s_in = nullptr;    // host-array calls: the pair list's copies and decodes, beside the kernels
     int32_t cu_count = 256;
     Knobs k;
     // knob aliases used by the launch code
-    int32_t& split_override = k.split_override;
     int32_t& band_form = k.band_form;
     int32_t& dp_classic = k.dp_classic;
     int32_t& dp_lane = k.dp_lane;
-    int32_t& lane_cw = k.lane_cw;
-    int64_t& lane_min_pairs = k.lane_min_pairs;
     int32_t& lane_prof = k.lane_prof;
-    int32_t& lane_col16 = k.lane_col16;
-    int32_t& lane_lds = k.lane_lds;
     int32_t& lane_sfx = k.lane_sfx;
-    int32_t& blocks_per_cu = k.blocks_per_cu;
     // resident reads
     int32_t n_reads = -1;
     int32_t lmax = 0;
@@ -171,7 +163,7 @@ struct Dev {
     int8_t* l_tb_host = nullptr;
     size_t l_tb_host_bytes = 0;
     // host-array pipeline: events per slot and pinned staging (slots x cap pairs x {a, b} / {score, end})
-    hipEvent_t ev_h2d[kSlots] = {}, ev_in[kSlots] = {}, ev_k[kSlots] = {}, ev_out[kSlots] = {};
+    hipEvent_t ev_k[kSlots] = {};
     int32_t* st_in = nullptr;
     int32_t* st_out = nullptr;
     int32_t* st_in_dev = nullptr;   // device addresses of the staging rings (kernels read / store them)
@@ -233,6 +225,7 @@ struct ovl_ctx {
     };
     std::vector<Launch> t_launches;  // timing on: every scoring launch of the last host-array call
     int64_t x_link_bytes = 0, x_packed_pairs = 0;  // ovl_last_transfer
+    int64_t x_ix_pairs = 0, x_dec_pairs = 0;       // ovl_last_pair_list
 };
 
 namespace {
@@ -418,7 +411,7 @@ bool use_dp_lane(const Dev* c, int64_t match, int64_t mismatch, int64_t indel, i
     const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
     if (L > kLaneMaxLen || (4 * L + 4) * M >= (int64_t(1) << 30) || c->codes_bytes + 64 >= (int64_t(1) << 32))
         return false;
-    return c->dp_lane == 1 || n_pairs >= c->lane_min_pairs;
+    return c->dp_lane == 1 || n_pairs >= kLaneMinPairs;
 }
 
 // Kernels queue pair indices as int32 (LDS side ring); split huge lists.
@@ -463,7 +456,6 @@ int32_t ungapped_rs_log2(const Dev* c, int64_t n_pairs) {
     const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
     while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
     if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * 8) ? 1 : 0;
-    if (c->split_override >= 0) rs_log2 = c->split_override;  // OVL_SPLIT tuning knob
     return rs_log2;
 }
 
@@ -523,14 +515,14 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.planes = c->planes;
         g.wmax = c->wmax;
         g.key64 = pl.key64 ? 1 : 0;
-        g.max_blocks = (int64_t)c->cu_count * c->blocks_per_cu;
+        g.max_blocks = (int64_t)c->cu_count * kBlocksPerCu;
         g.host_out = c->out_mode;
         g.ix_b16 = c->ix_b16;
         g.ix_d8 = c->ix_d8;
         g.ix_base = c->ix_base;
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
-        if (c->k.heavy_first && !g.ix_b16 && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
+        if (!g.ix_b16 && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
             d_a < ca + c->cand_n && d_b == as<int32_t>(c->cand_b) + (d_a - ca) && (d_a - ca) % 64 == 0) {
             int rc = ensure_heavy(c);
             if (rc != OVL_OK) return rc;
@@ -568,7 +560,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.classic = c->dp_classic;
         if (g.band < 0 && !g.wide && !g.classic && use_dp_lane(c, match, mismatch, indel, n_pairs)) {
             OvlLaneArgs k{};
-            k.cw = c->lane_cw;
+            k.cw = 32;
             k.slots = (int64_t)c->cu_count * 4 * ovl_dp_lane_waves_per_simd(k.cw);
             const size_t col_bytes = (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t);
             HIPCHK(c, scratch_acquire(c, s, {{&c->lane_col, col_bytes}}));
@@ -577,11 +569,11 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
             const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
             k.prof = c->lane_prof && c->planes == 2 && indel <= 0 && sma >= -128 && sma <= 127 && smm >= -128 &&
                      smm <= 127;
-            k.ho = c->lane_col16 && (4 * L + 4) * M < (int64_t(1) << 15) ? 1 : 0;
+            k.ho = (4 * L + 4) * M < (int64_t(1) << 15) ? 1 : 0;
             k.sfx = k.prof && c->lane_sfx && c->wmax > 0;
             // column steps G[i][j] - G[i-1][j] lie in [0, max(match, mismatch) - 2*indel]: 4 bits in LDS
             const int64_t step_max = std::max<int64_t>(match, mismatch) - 2 * indel;
-            if (c->lane_lds && k.sfx && k.cw != 16 && indel <= 0 && std::max<int64_t>(match, mismatch) >= indel &&
+            if (k.sfx && indel <= 0 && std::max<int64_t>(match, mismatch) >= indel &&
                 step_max <= 15 && g.mcap <= 256)
                 k.ho = 2;
             k.sfx_words = as<uint32_t>(c->sfx);
@@ -618,7 +610,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                     g.band_form = lane_ok ? OVL_BAND_FORM_LANE : (diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST);
                     break;
                 default:
-                    g.band_form = (lane_ok && n_pairs >= c->lane_min_pairs)
+                    g.band_form = (lane_ok && n_pairs >= kLaneMinPairs)
                                       ? OVL_BAND_FORM_LANE
                                       : (diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST);
                     break;
@@ -657,10 +649,6 @@ struct DeviceGuard {
 
 Knobs read_knobs() {
     Knobs k;
-    if (const char* sp = getenv("OVL_SPLIT")) {
-        const int v = atoi(sp);
-        if (v >= 0 && v <= 2) k.split_override = v;
-    }
     if (const char* e = getenv("OVL_BAND_FORM")) {
         if (!strcmp(e, "diag")) k.band_form = OVL_BAND_FORM_DIAG;
         else if (!strcmp(e, "rows")) k.band_form = OVL_BAND_FORM_ROWS;
@@ -670,28 +658,15 @@ Knobs read_knobs() {
     }
     if (const char* e = getenv("OVL_DP_CLASSIC")) k.dp_classic = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_DP_LANE")) k.dp_lane = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_CW")) k.lane_cw = atoi(e) == 32 ? 32 : 16;
-    if (const char* e = getenv("OVL_LANE_MIN_PAIRS")) k.lane_min_pairs = atoll(e);
     if (const char* e = getenv("OVL_LANE_PROF")) k.lane_prof = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_COL16")) k.lane_col16 = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_LDS")) k.lane_lds = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_LANE_SFX")) k.lane_sfx = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_BLOCKS_PER_CU")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 1024) k.blocks_per_cu = v;
-    }
-    if (const char* e = getenv("OVL_PIPE_DIRECT")) k.pipe_direct = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PACK")) k.pack = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
-    if (const char* e = getenv("OVL_PACK_NT")) k.pack_nt = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_SPIN_WAIT")) k.spin_wait = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_HEAVY_FIRST")) k.heavy_first = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
         k.pack_adapt = 0;  // a fixed share
     }
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PAIRS_COMPACT_MIN")) k.compact_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
@@ -730,15 +705,8 @@ class CpuShare {
         last_ = now;
         if (fd_ < 0) fd_ = bind_slot(-1);
         int bound = 0;
-        for (int i = 0; i < kSlots; ++i) {
-            if (i == slot_) {
-                ++bound;
-                continue;
-            }
-            const int f = bind_slot(i);
-            if (f == -2) ++bound;  // in use: a live process holds it
-            else if (f >= 0) close(f);
-        }
+        for (int i = 0; i < kSlots; ++i)
+            if (i == slot_ || slot_held(i)) ++bound;
         int ranks = 1;
         if (const char* e = getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1, atoi(e));
         const int n = std::max(std::max(bound, ranks), 1);
@@ -767,26 +735,39 @@ class CpuShare {
         cpus_ = n;
         snprintf(key_, sizeof(key_), "ovl-share-%u-%016llx", (unsigned)getuid(), (unsigned long long)h);
     }
-    // slot < 0: bind the first free slot and keep it (returns its fd, or -1); slot >= 0: probe it (returns a
-    // bound fd the caller closes, -2 when it is in use, -1 on any other failure)
-    int bind_slot(int slot) {
-        for (int i = slot < 0 ? 0 : slot; i < (slot < 0 ? kSlots : slot + 1); ++i) {
+    socklen_t slot_addr(int i, sockaddr_un& a) const {
+        memset(&a, 0, sizeof(a));
+        a.sun_family = AF_UNIX;
+        const int len = snprintf(a.sun_path + 1, sizeof(a.sun_path) - 1, "%s-%d", key_, i);
+        return (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + len);
+    }
+    // bind the first free slot and keep it (returns its fd, or -1)
+    int bind_slot(int) {
+        for (int i = 0; i < kSlots; ++i) {
             const int fd = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
             if (fd < 0) return -1;
             sockaddr_un a;
-            memset(&a, 0, sizeof(a));
-            a.sun_family = AF_UNIX;
-            const int len = snprintf(a.sun_path + 1, sizeof(a.sun_path) - 1, "%s-%d", key_, i);
-            if (bind(fd, reinterpret_cast<sockaddr*>(&a), (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + len)) == 0) {
-                if (slot < 0) slot_ = i;
+            const socklen_t n = slot_addr(i, a);
+            if (bind(fd, reinterpret_cast<sockaddr*>(&a), n) == 0) {
+                slot_ = i;
                 return fd;
             }
             const int err = errno;
             close(fd);
             if (err != EADDRINUSE) return -1;
-            if (slot >= 0) return -2;
         }
         return -1;
+    }
+    // a live process holds slot i: a datagram socket can connect to it (connect binds nothing, so two
+    // processes probing at once never see each other's probes as holders)
+    bool slot_held(int i) const {
+        const int fd = socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+        if (fd < 0) return false;
+        sockaddr_un a;
+        const socklen_t n = slot_addr(i, a);
+        const bool held = connect(fd, reinterpret_cast<sockaddr*>(&a), n) == 0;
+        close(fd);
+        return held;
     }
     pid_t pid_;
     int cpus_ = 1;
@@ -846,6 +827,9 @@ class CopyPool {
     }
     // f(i, lo, hi) for every part i of `b` (from cut), on the workers and the calling thread (part 0); `pre`,
     // when given, runs on the calling thread once the workers have their parts, before its own
+    // `pre` runs on the calling thread while the workers take the parts (encode_chunk issues the previous
+    // chunk there).  A pool call made from inside `pre` or `f` on this thread (the pool is busy with this
+    // batch, and call_mu_ is held) runs its parts inline instead of waiting on itself.
     void parallel_parts(const std::vector<size_t>& b, const std::function<void(size_t, size_t, size_t)>& f,
                         const std::function<void()>& pre = nullptr) {
         spin_us_.store(CpuShare::get().sharers() > 1 ? 0 : spin_cfg_, std::memory_order_relaxed);
@@ -855,7 +839,16 @@ class CopyPool {
             f(0, b[0], b[parts]);
             return;
         }
+        if (in_batch_) {
+            if (pre) pre();
+            for (size_t i = 0; i < parts; ++i) f(i, b[i], b[i + 1]);
+            return;
+        }
         std::lock_guard<std::mutex> one_call(call_mu_);  // calls from several host threads take turns
+        struct InBatch {
+            InBatch() { in_batch_ = true; }
+            ~InBatch() { in_batch_ = false; }
+        } in_batch;
         {
             std::lock_guard<std::mutex> lk(mu_);
             for (size_t i = 1; i < parts; ++i) {
@@ -900,7 +893,6 @@ class CopyPool {
     CopyPool() : pid_(getpid()) {
         // workers for this process alone (sharers 1); calls with more sharers use fewer of them
         const int n = pool_rule(CpuShare::get().cpus(), 1, env_pool_threads());
-        if (const char* e = getenv("OVL_POOL_SPIN_US")) spin_cfg_ = std::max(0, std::min(100000, atoi(e)));
         spin_us_.store(spin_cfg_, std::memory_order_relaxed);
         for (int i = 0; i + 1 < n; ++i) {
             std::thread t([this] { run(); });
@@ -947,7 +939,9 @@ class CopyPool {
     std::vector<std::function<void()>> tasks_;
     std::atomic<size_t> queued_{0};   // tasks_.size(), readable without mu_ by polling workers
     std::atomic<size_t> pending_{0};  // tasks of the current batch not finished yet
-    int spin_cfg_ = 100;              // OVL_POOL_SPIN_US
+    int spin_cfg_ = 100;              // microseconds a worker polls for work after its last task
+    static inline thread_local bool in_batch_ = false;  // this thread is inside parallel_parts (nested calls
+                                                        // run inline)
     std::atomic<int> spin_us_{100};   // 0 while other processes share this CPU set
     std::mutex mu_, call_mu_;
     std::condition_variable cv_, done_;
@@ -969,9 +963,9 @@ void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc,
 }
 
 // The pipeline's waits for a chunk: polled (a chunk is tens of microseconds away; a blocking wait can
-// add its own wake-up latency per chunk, depending on the device's scheduling flags) or hipEventSynchronize.
+// add its own wake-up latency per chunk, depending on the device's scheduling flags).
 hipError_t wait_event(const Dev* d, hipEvent_t ev) {
-    if (!d->k.spin_wait) return hipEventSynchronize(ev);
+    (void)d;
     for (;;) {
         const hipError_t e = hipEventQuery(ev);
         if (e != hipErrorNotReady) return e;
@@ -987,7 +981,7 @@ void free_staging(int32_t*& p) {
 void destroy_dev(Dev* d) {
     if (!d) return;
     (void)hipSetDevice(d->device);
-    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
+    for (hipStream_t s : {d->stream, d->s_in})
         if (s) (void)hipStreamSynchronize(s);
     for (DevBuf* b : {&d->codes, &d->off, &d->len, &d->sfx, &d->pfx, &d->lut, &d->full, &d->raw, &d->rd, &d->a, &d->b,
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
@@ -1003,13 +997,12 @@ void destroy_dev(Dev* d) {
     for (hipEvent_t e : d->dec_ev)
         if (e) (void)hipEventDestroy(e);
     for (int i = 0; i < kSlots; ++i)
-        for (hipEvent_t e : {d->ev_h2d[i], d->ev_in[i], d->ev_k[i], d->ev_out[i]})
-            if (e) (void)hipEventDestroy(e);
+        if (d->ev_k[i]) (void)hipEventDestroy(d->ev_k[i]);
     for (hipEvent_t e : d->t_ev)
         if (e) (void)hipEventDestroy(e);
     if (d->scratch_evt) (void)hipEventDestroy(d->scratch_evt);
     if (d->ev_last) (void)hipEventDestroy(d->ev_last);
-    for (hipStream_t s : {d->stream, d->s_in, d->s_out})
+    for (hipStream_t s : {d->stream, d->s_in})
         if (s) (void)hipStreamDestroy(s);
     delete d;
 }
@@ -1020,15 +1013,14 @@ hipError_t init_dev(Dev* d) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
         d->cu_count = prop.multiProcessorCount;
-    for (hipStream_t* s : {&d->stream, &d->s_in, &d->s_out}) {
+    for (hipStream_t* s : {&d->stream, &d->s_in}) {
         e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
         if (e != hipSuccess) return e;
     }
-    for (int i = 0; i < kSlots; ++i)
-        for (hipEvent_t* ev : {&d->ev_h2d[i], &d->ev_in[i], &d->ev_k[i], &d->ev_out[i]}) {
-            e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-            if (e != hipSuccess) return e;
-        }
+    for (int i = 0; i < kSlots; ++i) {
+        e = hipEventCreateWithFlags(&d->ev_k[i], hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
     e = hipEventCreateWithFlags(&d->scratch_evt, hipEventDisableTiming);
     if (e != hipSuccess) return e;
     e = hipEventCreateWithFlags(&d->ev_last, hipEventDisableTiming);
@@ -1110,9 +1102,9 @@ bool host_pinned(const void* p, size_t bytes) {
 // Direct kernel stores into pinned arrays need no chunks at all.  Packed results (pack_ok) are expanded
 // on the host chunk by chunk while the next chunk is scored: 1 M pairs (tools/host_paths_ab.py at the
 // target point: 128 K 0.53 ms, 256 K 0.38, 512 K 0.30, 1 M 0.25, one chunk 0.29).
-int64_t pick_chunk(const Dev* d, int64_t n, bool staged, bool direct, bool pack) {
+int64_t pick_chunk(const Dev* d, int64_t n, bool staged, bool pack) {
     if (d->k.pipe_chunk > 0) return d->k.pipe_chunk;
-    const int64_t cap = int64_t(1) << (pack ? 20 : (direct ? 19 : 22));
+    const int64_t cap = int64_t(1) << (pack ? 20 : 19);
     return std::max<int64_t>(1, staged ? std::min(n, cap) : n);
 }
 
@@ -1133,12 +1125,10 @@ struct Call {
     int32_t* out_e = nullptr;
     int64_t out_base = 0;
     bool out_pinned = false;
-    bool direct = false;           // kernels read host pair lists and store results through host mappings
-                                   // (the caller's pinned arrays, or pinned staging slots for pageable ones)
-    bool pack = false;             // direct: results cross the link packed (2 bytes per pair) into the staging
+    bool pack = false;             // results cross the link packed (2 bytes per pair) into the staging
                                    // slots and are expanded into the caller's arrays on the host (all chunks for
                                    // pageable arrays; for pinned ones all but a last direct chunk, Job::n_packed)
-    bool compact = false;          // direct, one device: the host pair list is encoded per chunk (encode_chunk)
+    bool compact = false;          // one device: the host pair list is encoded per chunk (encode_chunk)
                                    // and decoded into HBM by kernels reading it through the host mapping
     bool timing = false;
 };
@@ -1173,7 +1163,7 @@ int setup_job(const Call& C, Job& J) {
     if (n <= 0) return OVL_OK;
     HIPCHK(d, hipSetDevice(d->device));
     const bool need_in = C.h_a && !C.in_pinned && !C.compact, need_out = !C.out_pinned || C.pack;
-    J.chunk = pick_chunk(d, n, need_in || need_out, C.direct, C.pack);
+    J.chunk = pick_chunk(d, n, need_in || need_out, C.pack);
     // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
     if (C.pack) {
@@ -1219,13 +1209,7 @@ int setup_job(const Call& C, Job& J) {
         }
         d->cp_link = 0;
     }
-    if (C.h_a && !C.direct) {
-        HIPCHK(d, ensure(d->a, bytes));
-        HIPCHK(d, ensure(d->b, bytes));
-        J.ka = as<int32_t>(d->a);
-        J.kb = as<int32_t>(d->b);
-    }
-    if (C.h_a && C.direct && C.in_pinned && !C.compact) {
+    if (C.h_a && C.in_pinned && !C.compact) {
         // the kernels read this device's slice of the caller's pinned pair arrays in place
         void* pa = nullptr;
         void* pb = nullptr;
@@ -1234,7 +1218,7 @@ int setup_job(const Call& C, Job& J) {
         J.za = reinterpret_cast<const int32_t*>(pa);
         J.zb = reinterpret_cast<const int32_t*>(pb);
     }
-    if (C.direct && C.out_pinned) {
+    if (C.out_pinned) {
         // the device's address of this slice of the caller's pinned arrays
         void* ps = nullptr;
         void* pe = nullptr;
@@ -1242,11 +1226,6 @@ int setup_job(const Call& C, Job& J) {
         HIPCHK(d, hipHostGetDevicePointer(&pe, C.out_e + (J.lo - C.out_base), 0));
         J.d_score = reinterpret_cast<int32_t*>(ps);
         J.d_end = reinterpret_cast<int32_t*>(pe);
-    } else if (!C.direct) {
-        HIPCHK(d, ensure(d->score, bytes));
-        HIPCHK(d, ensure(d->end, bytes));
-        J.d_score = as<int32_t>(d->score);
-        J.d_end = as<int32_t>(d->end);
     }
     // pinned staging rings for pageable caller arrays, both allocated with capacity d->st_cap
     if ((need_in || need_out) && J.chunk > d->st_cap) {
@@ -1351,7 +1330,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
             run_pre);
         if (pre_rc != OVL_OK) return pre_rc;
         if (std::find(bad.begin(), bad.end(), 1) == bad.end()) {
-            J.ixk[(size_t)k] = 1;  // (issue_chunk_direct copies the chunk into HBM and launches on it)
+            J.ixk[(size_t)k] = 1;  // (issue_chunk copies the chunk into HBM and launches on it)
             if (g_trace) g_trace->mark('e', k);
             d->cp_link += 3 * (int64_t)n + 4 * ((n + 63) / 64);
             return OVL_OK;
@@ -1422,9 +1401,10 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
     return OVL_OK;
 }
 
-// Direct mode: the kernels read the pair list and store the results through host mappings (no copy-engine
-// transfers); pageable arrays are copied into / out of the pinned staging slots on the host.
-int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
+// The kernels read the pair list and store the results through host mappings (no copy-engine transfers);
+// pageable arrays are copied into / out of the pinned staging slots on the host.  (Round 1's copy-engine
+// form -- H2D, kernel, D2H per chunk -- took 0.395 against 0.186 ms for the target point's step and is gone.)
+int issue_chunk(const Call& C, Job& J, int64_t k) {
     Dev* d = J.d;
     HIPCHK(d, hipSetDevice(d->device));
     const int64_t off = J.cb[(size_t)k];
@@ -1489,72 +1469,15 @@ int issue_chunk_direct(const Call& C, Job& J, int64_t k) {
     return OVL_OK;
 }
 
-int issue_chunk(const Call& C, Job& J, int64_t k) {
-    if (C.direct) return issue_chunk_direct(C, J, k);
-    Dev* d = J.d;
-    HIPCHK(d, hipSetDevice(d->device));
-    const int64_t off = J.cb[(size_t)k];
-    const int64_t g = J.lo + off;
-    const int64_t n = J.cb[(size_t)k + 1] - off;
-    const size_t nb = sizeof(int32_t) * (size_t)n;
-    const int slot = (int)(k % kSlots);
-    const int32_t* ka;
-    const int32_t* kb;
-    if (C.h_a) {
-        const int32_t* sa = C.h_a + g;
-        const int32_t* sb = C.h_b + g;
-        if (!C.in_pinned) {
-            // the slot's previous H2D (chunk k - kSlots) must have read it
-            if (k >= kSlots) HIPCHK(d, wait_event(d, d->ev_in[slot]));
-            int32_t* st = d->st_in + (size_t)slot * 2 * (size_t)d->st_cap;
-            host_copy(st, sa, nb);
-            host_copy(st + d->st_cap, sb, nb);
-            sa = st;
-            sb = st + d->st_cap;
-        }
-        HIPCHK(d, hipMemcpyAsync(J.ka + off, sa, nb, hipMemcpyHostToDevice, d->s_in));
-        HIPCHK(d, hipMemcpyAsync(J.kb + off, sb, nb, hipMemcpyHostToDevice, d->s_in));
-        if (!C.in_pinned) HIPCHK(d, hipEventRecord(d->ev_in[slot], d->s_in));
-        HIPCHK(d, hipEventRecord(d->ev_h2d[slot], d->s_in));
-        HIPCHK(d, hipStreamWaitEvent(d->stream, d->ev_h2d[slot], 0));
-        ka = J.ka + off;
-        kb = J.kb + off;
-    } else {
-        ka = J.dev_a + g;
-        kb = J.dev_b + g;
-    }
-    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
-    int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, J.d_score + off, J.d_end + off,
-                          d->stream);
-    if (rc != OVL_OK) return rc;
-    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
-    HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
-    HIPCHK(d, hipStreamWaitEvent(d->s_out, d->ev_k[slot], 0));
-    int32_t* ds;
-    int32_t* de;
-    if (C.out_pinned) {
-        ds = C.out_s + (g - C.out_base);
-        de = C.out_e + (g - C.out_base);
-    } else {
-        ds = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
-        de = ds + d->st_cap;
-    }
-    HIPCHK(d, hipMemcpyAsync(ds, J.d_score + off, nb, hipMemcpyDeviceToHost, d->s_out));
-    HIPCHK(d, hipMemcpyAsync(de, J.d_end + off, nb, hipMemcpyDeviceToHost, d->s_out));
-    HIPCHK(d, hipEventRecord(d->ev_out[slot], d->s_out));
-    return OVL_OK;
-}
-
-
-// Pageable outputs: copy chunk k out of its staging slot once its results are there (the D2H copy, or in
-// direct mode the kernel that stored them).
+// Pageable outputs: copy chunk k out of its staging slot once its results are there (the kernel that stored
+// them has finished).
 int drain_chunk(const Call& C, Job& J, int64_t k) {
     Dev* d = J.d;
     const int64_t off = J.cb[(size_t)k];
     const int64_t g = J.lo + off;
     const int64_t n = J.cb[(size_t)k + 1] - off;
     const int slot = (int)(k % kSlots);
-    HIPCHK(d, wait_event(d, C.direct ? d->ev_k[slot] : d->ev_out[slot]));
+    HIPCHK(d, wait_event(d, d->ev_k[slot]));
     if (g_trace) g_trace->mark('w', k);
     struct Drained {
         int64_t k;
@@ -1565,7 +1488,7 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
     if (C.pack) {
         host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
-                    ss + d->st_cap, C.match, C.mismatch, d->k.pack_nt != 0, (size_t)n);
+                    ss + d->st_cap, C.match, C.mismatch, true, (size_t)n);
         return OVL_OK;
     }
     host_copy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);
@@ -1576,7 +1499,7 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
 void quiesce(std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         (void)hipSetDevice(J.d->device);
-        for (hipStream_t s : {J.d->stream, J.d->s_in, J.d->s_out}) (void)hipStreamSynchronize(s);
+        for (hipStream_t s : {J.d->stream, J.d->s_in}) (void)hipStreamSynchronize(s);
     }
 }
 
@@ -1607,7 +1530,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         ~Unset() { g_trace = nullptr; }
     } unset;
     int rc = OVL_OK;
-    HostFlag host_flag(jobs, C.direct ? 1 : 0);  // (direct chunks set their own sink: issue_chunk_direct)
+    HostFlag host_flag(jobs, 1);  // (each chunk sets its own sink: issue_chunk)
     for (Job& J : jobs)
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
     trace.mark('s', 0);
@@ -1615,7 +1538,10 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (const Job& J : jobs) maxch = std::max(maxch, J.nchunks);
     if (C.compact)
         for (Job& J : jobs)
-            if (J.nchunks > 0 && (rc = encode_chunk(C, J, 0)) != OVL_OK) return rc;
+            if (J.nchunks > 0 && (rc = encode_chunk(C, J, 0)) != OVL_OK) {
+                quiesce(jobs);  // (its decode kernels may already be queued, reading the pinned encoding)
+                return rc;
+            }
     for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
@@ -1663,7 +1589,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         if (J.nchunks == 0) continue;
         HIPCHK(c, hipSetDevice(J.d->device));
-        HIPCHK(c, hipStreamSynchronize(C.direct ? J.d->stream : J.d->s_out));
+        HIPCHK(c, hipStreamSynchronize(J.d->stream));
     }
     trace.mark('y', 0);
     double kms = 0.0;
@@ -1680,9 +1606,8 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
             for (int64_t k = 0; k < J.nchunks; ++k) {
                 float ms = 0.f;
                 if (hipEventElapsedTime(&ms, d->t_ev[2 * k], d->t_ev[2 * k + 1]) == hipSuccess) s += ms;
-                // the chunk's result sink (issue_chunk_direct): packed staging, int32 into host memory; copy-engine
-                // mode stores into HBM
-                const int32_t sink = !C.direct ? 0 : (C.pack && k < J.n_packed ? 2 : 1);
+                // the chunk's result sink (issue_chunk): packed staging, or int32 into host memory
+                const int32_t sink = C.pack && k < J.n_packed ? 2 : 1;
                 c->t_launches.push_back({d->device, sink, J.cb[(size_t)k + 1] - J.cb[(size_t)k], (double)ms});
             }
             kms = std::max(kms, s);
@@ -1690,16 +1615,21 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     }
     c->t_kernel_ms = kms;
     c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    int64_t link = 0, packed = 0;
+    int64_t link = 0, packed = 0, ix = 0, dec = 0;
     for (const Job& J : jobs) {
         const int64_t n = J.hi - J.lo;
         if (n <= 0) continue;
         const int64_t np = J.n_packed ? J.cb[(size_t)J.n_packed] : 0;
         packed += np;
         link += (C.compact ? J.d->cp_link : (C.h_a ? 8 * n : 0)) + 2 * np + 8 * (n - np);
+        if (C.compact)
+            for (int64_t k = 0; k < J.nchunks; ++k)
+                (J.ixk[(size_t)k] ? ix : dec) += J.cb[(size_t)k + 1] - J.cb[(size_t)k];
     }
     c->x_link_bytes = link;
     c->x_packed_pairs = packed;
+    c->x_ix_pairs = ix;
+    c->x_dec_pairs = dec;
     return rc;
 }
 
@@ -1764,7 +1694,7 @@ bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) 
     const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 4;
     // (the expansion needs the host pool: with fewer than 6 threads -- several processes on one CPU set, e.g.
     // joblib workers or many ranks on one quota (CpuShare) -- the int32 stores over the link are faster)
-    return c->devs.size() == 1 && d->k.pack && d->k.pipe_direct && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
+    return c->devs.size() == 1 && d->k.pack && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
            p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
@@ -1840,13 +1770,10 @@ OVL_API int ovl_host_alloc(int64_t bytes, void** out_ptr) {
     if (!out_ptr) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "out_ptr is NULL");
     *out_ptr = nullptr;
     if (bytes < 0) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "bytes < 0");
-    // fine-grained (coherent) by default: kernels store results into it while host code may hold cached
-    // copies of the same lines (a caller reusing its arrays); OVL_HOST_COHERENT=0 gives the coarse-grained
-    // kind (A/B knob: no difference in step time, profiles/r02_pack_ab_target.json)
-    unsigned flags = hipHostMallocPortable | hipHostMallocCoherent;
-    if (const char* e = getenv("OVL_HOST_COHERENT"))
-        if (!atoi(e)) flags = hipHostMallocPortable | hipHostMallocNonCoherent;
-    HIPCHK((ovl_ctx*)nullptr, hipHostMalloc(out_ptr, (size_t)std::max<int64_t>(bytes, 64), flags));
+    // fine-grained (coherent): kernels store results into it while host code may hold cached copies of the
+    // same lines (a caller reusing its arrays); the coarse-grained kind made no difference in step time
+    // (profiles/r02_pack_ab_target.json)
+    HIPCHK((ovl_ctx*)nullptr, hipHostMalloc(out_ptr, (size_t)std::max<int64_t>(bytes, 64), kHostShared));
     return OVL_OK;
 }
 
@@ -1892,6 +1819,13 @@ OVL_API int ovl_last_transfer(const ovl_ctx* c, int64_t* link_bytes, int64_t* pa
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (link_bytes) *link_bytes = c->x_link_bytes;
     if (packed_pairs) *packed_pairs = c->x_packed_pairs;
+    return OVL_OK;
+}
+
+OVL_API int ovl_last_pair_list(const ovl_ctx* c, int64_t* in_place_pairs, int64_t* decoded_pairs) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (in_place_pairs) *in_place_pairs = c->x_ix_pairs;
+    if (decoded_pairs) *decoded_pairs = c->x_dec_pairs;
     return OVL_OK;
 }
 
@@ -1995,14 +1929,8 @@ int stage_reads(ovl_ctx* c, ReadStage& st, HostReads& h) {
         std::vector<uint8_t> ok(parts.size() - 1, 0);  // (cut gives parts + 1 bounds)
         const uint8_t* src = h.src;
         uint8_t* pk = reinterpret_cast<uint8_t*>(st.p + st.o_pk);
-        // OVL_READS_PACK2=0 (A/B knob): the bytes are uploaded as they are
-        static const bool pack2 = !(getenv("OVL_READS_PACK2") && atoi(getenv("OVL_READS_PACK2")) == 0);
         pool.parallel_parts(parts, [&](size_t i, size_t lo, size_t hi) {
-            if (pack2) {
-                ok[i] = ovl_scan::scan_pack(src, lo, hi, seen[i].data(), pk);
-            } else {
-                ovl_scan::scan_bytes(src + lo, hi - lo, seen[i].data());
-            }
+            ok[i] = ovl_scan::scan_pack(src, lo, hi, seen[i].data(), pk);
         });
         for (const auto& t : seen)
             for (int v = 0; v < 256; ++v) present[v] = present[v] || t[(size_t)v];
@@ -2213,9 +2141,8 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.out_e = out_end;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = c->timing != 0;
-    C.direct = c->devs[0]->k.pipe_direct != 0;
     C.pack = pack_ok(c, p, n_pairs, C.out_pinned);
-    C.compact = C.direct && c->devs.size() == 1 && c->devs[0]->k.compact && n_pairs >= c->devs[0]->k.compact_min;
+    C.compact = c->devs.size() == 1 && c->devs[0]->k.compact && n_pairs >= kCompactMin;
     const int32_t S = (int32_t)c->devs.size();
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);
@@ -2464,7 +2391,6 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.out_base = lo;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = ctx->timing != 0;
-    C.direct = ctx->devs[0]->k.pipe_direct != 0;
     C.pack = pack_ok(ctx, p, hi - lo, C.out_pinned);
     const int32_t S = (int32_t)ctx->devs.size();
     std::vector<int64_t> cuts;

@@ -453,7 +453,7 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
     Layout L;
     memset(&L, 0, sizeof(L));
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
-    PyObject **sin = NULL, **pin = NULL, **dptr = NULL;
+    PyObject **sin = NULL, **pin = NULL;
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t *dout = NULL, *din = NULL;
     if (!ints) { PyErr_NoMemory(); goto done; }
@@ -484,10 +484,9 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
         /* live degrees: every dict is created at its final size */
         dout = (int64_t*)PyMem_Calloc((size_t)(L.N ? L.N : 1), sizeof(int64_t));
         din = (int64_t*)PyMem_Calloc((size_t)(L.N ? L.N : 1), sizeof(int64_t));
-        dptr = (PyObject**)PyMem_Calloc((size_t)(L.E ? L.E : 1), sizeof(PyObject*));
         sin = (PyObject**)PyMem_Malloc(sizeof(PyObject*) * (size_t)(L.N ? L.N : 1));
         pin = (PyObject**)PyMem_Malloc(sizeof(PyObject*) * (size_t)(L.N ? L.N : 1));
-        if (!dout || !din || !dptr || !sin || !pin) { PyErr_NoMemory(); goto done; }
+        if (!dout || !din || !sin || !pin) { PyErr_NoMemory(); goto done; }
         for (Py_ssize_t g = 0; g < (Py_ssize_t)L.goff[L.R]; ++g) {
             const int64_t p = L.plist[g];
             for (int64_t u = L.first[a[p]]; u < L.first[a[p] + 1]; ++u) {
@@ -528,43 +527,33 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
             tmpl = PyDict_New();
             if (!tmpl || PyDict_SetItem(tmpl, kw, Py_None) || PyDict_SetItem(tmpl, ke, Py_None)) goto done;
         }
-        /* successors: row by row in CSR order (for a node, the global insertion order of its out-edges) */
-        for (Py_ssize_t r = 0; r < L.R; ++r) {
-            for (int64_t u = L.first[r]; u < L.first[r + 1]; ++u) {
-                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                    const int64_t p = L.plist[g];
-                    const int64_t e0 = L.off[u] + L.pstart[p];
-                    PyObject *wv = NULL, *ev = NULL;
-                    for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                        if (alive && !alive[e0 + cb]) continue;
-                        if (!wv) {
-                            wv = int_of(ints, sc[p]);
-                            ev = int_of(ints, en[p]);
-                            if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
-                        }
-                        PyObject* d = PyDict_Copy(tmpl);
-                        const int bad = !d || PyDict_SetItem(d, kw, wv) || PyDict_SetItem(d, ke, ev) ||
-                                        PyDict_SetItem(sin[u], PyList_GET_ITEM(names, L.first[b[p]] + cb), d);
-                        Py_XDECREF(d);
-                        if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
-                        dptr[e0 + cb] = d;  /* borrowed: the successor dict holds it */
-                    }
-                    Py_XDECREF(wv);
-                    Py_XDECREF(ev);
-                }
-            }
-        }
-        /* predecessors: edges in global insertion order (pair, copy of a, copy of b: overlapGraphs.py:43-60) */
+        /* one pass over the edges in global insertion order (pair, copy of a, copy of b: overlapGraphs.py:43-60):
+           each attribute dict goes into its tail's successor dict and its head's predecessor dict while it is
+           still in cache.  A node's successors arrive in that order too, which is its CSR row order. */
         for (Py_ssize_t p = 0; p < L.P; ++p) {
             if (keep && !keep[p]) continue;
+            PyObject *wv = NULL, *ev = NULL;
+            const int64_t vb = L.first[b[p]];
             for (int64_t u = L.first[a[p]]; u < L.first[a[p] + 1]; ++u) {
                 const int64_t e0 = L.off[u] + L.pstart[p];
                 PyObject* un = PyList_GET_ITEM(names, u);
                 for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                    PyObject* d = dptr[e0 + cb];
-                    if (d && PyDict_SetItem(pin[L.first[b[p]] + cb], un, d)) goto done;
+                    if (alive && !alive[e0 + cb]) continue;
+                    if (!wv) {
+                        wv = int_of(ints, sc[p]);
+                        ev = int_of(ints, en[p]);
+                        if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
+                    }
+                    PyObject* d = PyDict_Copy(tmpl);
+                    const int bad = !d || PyDict_SetItem(d, kw, wv) || PyDict_SetItem(d, ke, ev) ||
+                                    PyDict_SetItem(sin[u], PyList_GET_ITEM(names, vb + cb), d) ||
+                                    PyDict_SetItem(pin[vb + cb], un, d);
+                    Py_XDECREF(d);
+                    if (bad) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
                 }
             }
+            Py_XDECREF(wv);
+            Py_XDECREF(ev);
         }
         out = PyTuple_Pack(3, node, succ, pred);
     }
@@ -580,7 +569,6 @@ done:
     }
     PyMem_Free(dout);
     PyMem_Free(din);
-    PyMem_Free(dptr);
     PyMem_Free(sin);
     PyMem_Free(pin);
     Py_XDECREF(node);

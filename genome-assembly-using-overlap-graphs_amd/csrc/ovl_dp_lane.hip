@@ -542,9 +542,9 @@ using ovl::dp_lane_kernel;
 
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap) { return ((lcap + 31) & ~31) + 4; }
 
-// waves per SIMD each strip width is compiled for: 16 columns at 6, 32 columns at 4 (64 columns spill even
-// at 3 waves per SIMD: the 4-row body keeps two rows of the strip live)
-extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw) { return cw == 16 ? 6 : 4; }
+// waves per SIMD the strip width is compiled for: 32 columns at 4 (64 columns spill even at 3 waves per SIMD:
+// the 4-row body keeps two rows of the strip live; 16 columns at 6 waves per SIMD were slower, round 1)
+extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw) { return cw == 32 ? 4 : 0; }
 
 // the LDS hand-off (HO 2): rows rounded to 32, 4 bits per row, a dword per 8 rows, per wavefront of the block
 extern "C" int32_t ovl_dp_lane_lds_bytes(int32_t lcap) { return ((lcap + 31) & ~31) / 8 * 4 * 64 * 4; }
@@ -557,22 +557,16 @@ extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* 
     const int32_t lcap = g->mcap;
     const int32_t rcap = ovl_dp_lane_rcap(lcap);
     if (k->sfx && (!k->prof || !k->sfx_words || k->wsfx * 32 < lcap)) return hipErrorInvalidValue;
-    if (k->ho == 2 && (!k->sfx || k->cw == 16 || lcap > ovl::kLaneLdsMaxLen)) return hipErrorInvalidValue;
+    if (k->cw != 32) return hipErrorInvalidValue;
+    if (k->ho == 2 && (!k->sfx || lcap > ovl::kLaneLdsMaxLen)) return hipErrorInvalidValue;
     const size_t shmem = k->ho == 2 ? (size_t)ovl_dp_lane_lds_bytes(lcap) : 0;
 #define OVL_LANE(CW, OCC, PR, HO, SX)                                                                         \
     dp_lane_kernel<CW, OCC, PR, HO, SX><<<(unsigned)blocks, 256, shmem, stream>>>(                           \
         g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx, g->n_pairs, \
         lcap, rcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, k->colbuf, g->out_score,     \
         g->out_end, g->err_flag)
-    const int cwk = k->cw == 32 ? 1 : (k->cw == 16 ? 0 : 3);
-    const int key = cwk << 5 | (k->prof ? 8 : 0) | (k->ho & 3) << 1 | (k->sfx ? 1 : 0);
+    const int key = 1 << 5 | (k->prof ? 8 : 0) | (k->ho & 3) << 1 | (k->sfx ? 1 : 0);
     switch (key) {
-        case 0x00: OVL_LANE(16, 6, false, 0, false); break;
-        case 0x02: OVL_LANE(16, 6, false, 1, false); break;
-        case 0x08: OVL_LANE(16, 6, true, 0, false); break;
-        case 0x09: OVL_LANE(16, 6, true, 0, true); break;
-        case 0x0A: OVL_LANE(16, 6, true, 1, false); break;
-        case 0x0B: OVL_LANE(16, 6, true, 1, true); break;
         case 0x20: OVL_LANE(32, 4, false, 0, false); break;
         case 0x22: OVL_LANE(32, 4, false, 1, false); break;
         case 0x28: OVL_LANE(32, 4, true, 0, false); break;

@@ -43,10 +43,14 @@
 
 namespace {
 
+// One undo-log record per iterator advance of `node` (its old position).  A yield that reaches a node for the
+// first time also carries that node (`first`; -1 otherwise): its first visit and 'seen' insertion happen at
+// that yield (a yielded head becomes the next current node unless the edge closes a cycle, which rewinds past
+// the yield), so one record undoes all three.
 struct Event {
-    int32_t kind;   // 0: first visit of node, 1: iterator advance (old position), 2: 'seen' insertion
     int32_t node;
-    int64_t old;
+    int32_t old;
+    int32_t first;
 };
 
 // The settled set, kept exact after every removal: settled = the nodes that cannot reach a cycle over the
@@ -129,7 +133,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
         if (head[e] < 0 || head[e] >= n_nodes) return OVL_E_ARG;
     if (n_edges > 0 && !removed) return OVL_E_ARG;
 
-    if (n_edges >= (int64_t(1) << 31) - 1) return OVL_E_UNSUPPORTED;  // int32 skip deltas
+    if (n_edges >= (int64_t(1) << 31) - 1) return OVL_E_UNSUPPORTED;  // int32 positions and skip deltas
 
     // Per edge, what one yield touches, in one 16-byte record: the head, the skip delta to the next edge
     // that may still be yielded (0: this one; edges removed or into explored / settled nodes are spliced
@@ -142,23 +146,33 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<Edge> ed((size_t)n_edges + 1);
     for (int64_t e = 0; e < n_edges; ++e) ed[(size_t)e] = {head[e], 0, weight[e]};
     ed[(size_t)n_edges] = {0, 0, 0};
-    std::vector<uint8_t> alive(n_edges, 1), visited(n_nodes, 0), active(n_nodes, 0), seen(n_nodes, 0),
-        done(n_nodes, 0);  // done = explored | settled (both only grow)
-    std::vector<int64_t> pos(n_nodes, 0);  // out-edge iterator position (CSR index) of visited nodes
-    // find_cycle's `edges`: the active path, one record per path edge: its CSR index, the undo-log size just
-    // before it was yielded, its weight, its tail (the node whose iterator yielded it) and head
+    std::vector<uint8_t> alive(n_edges, 1), done(n_nodes, 0);  // done = explored | settled (both only grow)
+    // per node, what a yield touches, in one record: the out-edge iterator position (CSR index) of a visited
+    // node, the index of the path edge leaving it (valid while active), visited (= seen: both happen at the
+    // yield that first reaches it) and on the active path
+    struct Node {
+        int32_t pos;
+        int32_t tail_pos;
+        uint8_t visited;
+        uint8_t active;
+    };
+    std::vector<Node> nd((size_t)n_nodes, Node{0, 0, 0, 0});
+    // find_cycle's `edges`: the active path, one record per path edge: the undo-log size just before it was
+    // yielded, its weight, CSR index, tail (the node whose iterator yielded it), head, and `link`: the last
+    // earlier path edge whose weight is <= this one's (-1: none).  From the path's end, the link chain visits
+    // the suffix minima, so the first minimum of the cycle path[i0..] is the last chain entry >= i0.
     struct PathEdge {
-        int64_t q;
         int64_t ckpt;
         int64_t w;
+        int32_t q;
         int32_t tail;
         int32_t head;
+        int32_t link;
     };
     std::vector<PathEdge> path;
-    std::vector<int32_t> stack;            // edge_dfs stack: the start node, then the path heads
+    std::vector<int32_t> stack;  // edge_dfs stack: the start node, then the path heads
     std::vector<int32_t> seen_list;
     std::vector<Event> log;
-    std::vector<int64_t> tail_pos(n_nodes, 0);  // node -> index of the path edge leaving it (valid while active)
     int64_t nrem = 0;
 
     // OVL_CYCLES_SETTLE=0 (a test knob): no settled-node pruning, only the explored nodes are skipped
@@ -166,6 +180,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     Sinks sinks(off, head, n_nodes, done.data(), !(env_settle && atoi(env_settle) == 0));
 
     Edge* E = ed.data();
+    Node* N = nd.data();
     for (int32_t s = 0; s < n_nodes; ++s) {
         if (done[s]) continue;
         log.clear();
@@ -173,29 +188,26 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
         seen_list.clear();
         stack.assign(1, s);
         int32_t root = s;  // find_cycle's path root (the start node; a reset re-roots at the tail)
-        active[s] = 1;
-        seen[s] = 1;
+        // the start node's first visit is never rewound (every rewind target is a later yield's checkpoint)
+        N[s].visited = 1;
+        N[s].pos = (int32_t)off[s];
+        N[s].active = 1;
         seen_list.push_back(s);
         int32_t prev_head = -1;
         for (;;) {
             if (stack.empty()) {
                 // no cycle reachable from s: everything seen is explored for the later starts
                 for (int32_t v : seen_list) done[v] = 1;
-                active[root] = 0;
+                N[root].active = 0;
                 break;
             }
             const int32_t cur = stack.back();
-            if (!visited[cur]) {
-                visited[cur] = 1;
-                pos[cur] = off[cur];
-                log.push_back({0, cur, 0});
-            }
             // next yield of cur's iterator.  Edges into explored or settled nodes are walked by edge_dfs
             // without any effect on find_cycle, and both sets only grow, so such an edge is spliced out
             // of every later iteration (skip deltas, shared with the removed edges) instead of being
             // yielded; the iterator advance over a run of them is logged once with the yield after it.
             const int64_t end = off[cur + 1];
-            int64_t q = pos[cur];
+            int64_t q = N[cur].pos;
             for (;;) {
                 while (E[q].skip) {  // first live edge at or after q (path halving)
                     const int64_t p1 = q + E[q].skip;
@@ -211,51 +223,49 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 E[q].skip = 1;
             }
             if (q == end) {  // iterator exhausted: pop
-                if (pos[cur] != q) {
-                    log.push_back({1, cur, pos[cur]});
-                    pos[cur] = q;
+                if (N[cur].pos != q) {
+                    log.push_back({cur, N[cur].pos, -1});
+                    N[cur].pos = (int32_t)q;
                 }
                 stack.pop_back();
                 continue;
             }
             // yield edge q = (cur, h)
             const int64_t mark = (int64_t)log.size();
-            log.push_back({1, cur, pos[cur]});
-            pos[cur] = q + 1;
+            log.push_back({cur, N[cur].pos, -1});
+            N[cur].pos = (int32_t)(q + 1);
             const int32_t h = E[q].head;
             stack.push_back(h);
             if (prev_head >= 0 && cur != prev_head) {
                 // backtracking: pop the path back to the edge whose head is cur (or empty it)
                 while (true) {
                     if (path.empty()) {  // popped everything: active_nodes = {tail}
-                        active[root] = 0;
+                        N[root].active = 0;
                         root = cur;
-                        active[root] = 1;
+                        N[root].active = 1;
                         break;
                     }
-                    active[path.back().head] = 0;
+                    N[path.back().head].active = 0;
                     path.pop_back();
                     if (!path.empty() && path.back().head == cur) break;
                 }
             }
-            tail_pos[cur] = (int64_t)path.size();
-            path.push_back({q, mark, E[q].w, cur, h});
-            if (active[h]) {
+            const int64_t w = E[q].w;
+            int32_t link = (int32_t)path.size() - 1;
+            while (link >= 0 && path[(size_t)link].w > w) link = path[(size_t)link].link;
+            N[cur].tail_pos = (int32_t)path.size();
+            path.push_back({mark, w, (int32_t)q, cur, h, link});
+            if (N[h].active) {
                 // cycle: the path suffix from the first edge leaving h (the path is simple, so that edge is
                 // tail_pos[h]); remove its weakest edge, the first minimum in cycle order
-                const size_t i0 = (size_t)tail_pos[h];
+                const int32_t i0 = N[h].tail_pos;
                 const PathEdge* pp = path.data();
-                size_t kmin = i0;
-                int64_t wmin = pp[i0].w;
-                for (size_t k = i0 + 1; k < path.size(); ++k)
-                    if (pp[k].w < wmin) {
-                        wmin = pp[k].w;
-                        kmin = k;
-                    }
+                int32_t kmin = (int32_t)path.size() - 1;
+                while (pp[kmin].link >= i0) kmin = pp[kmin].link;
                 const int64_t dead = pp[kmin].q;
                 const int32_t tail_of_dead = pp[kmin].tail;
                 removed[nrem++] = dead;
-                alive[dead] = 0;
+                alive[(size_t)dead] = 0;
                 E[dead].skip = 1;
                 sinks.removed(dead, alive.data());
                 // rewind the DFS to the moment `dead` was about to be yielded
@@ -263,37 +273,35 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 while ((int64_t)log.size() > target) {
                     const Event ev = log.back();
                     log.pop_back();
-                    if (ev.kind == 0) {
-                        visited[ev.node] = 0;
-                    } else if (ev.kind == 1) {
-                        pos[ev.node] = ev.old;
-                    } else {
-                        seen[ev.node] = 0;
+                    N[ev.node].pos = ev.old;
+                    if (ev.first >= 0) {
+                        N[ev.first].visited = 0;
                         seen_list.pop_back();
                     }
                 }
                 // heads leaving the path (not the closing edge's: that node is on the surviving path)
-                for (size_t k = kmin; k + 1 < path.size(); ++k) active[pp[k].head] = 0;
-                active[root] = 1;  // (the root is unchanged since path[kmin] was yielded)
-                path.resize(kmin);
+                for (size_t k = (size_t)kmin; k + 1 < path.size(); ++k) N[pp[k].head].active = 0;
+                N[root].active = 1;  // (the root is unchanged since path[kmin] was yielded)
+                path.resize((size_t)kmin);
                 // the edge_dfs stack at that moment: the root (= the start node: only it can be on the
                 // stack without being a path head) and the surviving path heads
-                stack.resize(kmin + 1);
+                stack.resize((size_t)kmin + 1);
                 if (kmin == 0) {
                     // the path root was the yielding node itself: active_nodes = {tail}
-                    active[root] = 0;
+                    N[root].active = 0;
                     root = tail_of_dead;
-                    active[root] = 1;
+                    N[root].active = 1;
                 }
-                prev_head = kmin > 0 ? path[kmin - 1].head : -1;
+                prev_head = kmin > 0 ? path[(size_t)kmin - 1].head : -1;
                 continue;
             }
-            if (!seen[h]) {
-                seen[h] = 1;
+            if (!N[h].visited) {  // first visit (and 'seen' insertion) of h, undone with this yield
+                N[h].visited = 1;
+                N[h].pos = (int32_t)off[h];
                 seen_list.push_back(h);
-                log.push_back({2, h, 0});
+                log.back().first = h;
             }
-            active[h] = 1;
+            N[h].active = 1;
             prev_head = h;
         }
     }

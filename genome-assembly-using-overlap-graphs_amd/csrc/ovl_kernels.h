@@ -34,9 +34,10 @@ struct OvlUngappedArgs {
     const uint8_t* tile_flags;  // ids, ascending; per-list-tile flags); null: natural order
     int32_t heavy_n;            // heavy tiles of this launch: heavy_ids[0 .. heavy_n)
     int64_t tile_base;          // the launch's first pair / 64 within the list
-    const uint16_t* ix_b16;  // non-null: uniform_kernel (throughput mode, int32 keys) reads a host-encoded pair
-    const uint8_t* ix_d8;    // list through the host mapping instead of a_idx / b_idx: b = ix_b16[p] (0xFFFF:
-    const int32_t* ix_base;  // a bad index), a = ix_base[p / 64] + ix_d8[p] (ovl_api.cpp encode_chunk)
+    const uint16_t* ix_b16;  // non-null: uniform_kernel (throughput mode, int32 keys) reads a compact pair list
+    const uint8_t* ix_d8;    // instead of a_idx / b_idx: b = ix_b16[p] (0xFFFF: a bad index), a = ix_base[p / 64]
+    const int32_t* ix_base;  // + ix_d8[p]; the host pool encodes each chunk (ovl_api.cpp encode_chunk) and the
+                             // copy engine moves it into HBM on the second stream, where the kernel reads it
     int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
                          // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
                          // out_score as uint16, the score of the few pairs that need it in out_end

@@ -838,9 +838,9 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
 // most that fits without spilling
 #define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : 4))) \
                                   : ((W) <= 4 ? 7 : ((W) <= 5 ? 6 : ((W) <= 6 ? 5 : 4))))
-// IX: the pair list is read in its host encoding through the host mapping (b = ix_b16[p], 0xFFFF a bad
-// index; a = ix_base[tile] + ix_d8[p]): 3 bytes per pair plus 4 per tile cross the link inside the launch,
-// no decode launch before it (ovl_api.cpp encode_chunk).
+// IX: the pair list is read in its compact encoding (b = ix_b16[p], 0xFFFF a bad index; a = ix_base[tile] +
+// ix_d8[p]), which the copy engine moved into HBM beside the previous chunk's launch (3 bytes per pair plus 4 per
+// tile over the link; ovl_api.cpp encode_chunk / issue_chunk): no decode launch before it.
 template <int W, int KM, bool LAT, int OM, bool IX = false>
 __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
@@ -1057,22 +1057,13 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
 #ifndef OVL_ABLATE_DRAIN
         if constexpr (!LAT) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#ifdef OVL_DRAIN_PRIO
-            if (tail - head >= 16) __builtin_amdgcn_s_setprio(OVL_DRAIN_PRIO);
-#endif
             while (tail - head >= 16) drain(16);
-#ifdef OVL_DRAIN_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
         }
 #endif
     }
 #ifndef OVL_ABLATE_DRAIN
     if constexpr (!LAT) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#ifdef OVL_DRAIN_PRIO
-        __builtin_amdgcn_s_setprio(OVL_DRAIN_PRIO);
-#endif
         if (tail > head) drain(tail - head);
     }
 #endif

@@ -154,6 +154,13 @@ class OverlapEngine:
         check(self._L.ovl_last_transfer(self._ctx, ctypes.byref(b), ctypes.byref(p)), self._ctx)
         return {"link_bytes": b.value, "packed_pairs": p.value}
 
+    def last_pair_list(self) -> Dict[str, int]:
+        """{in_place_pairs, decoded_pairs} of the last host-array call (ovl_last_pair_list): how the compact
+        host pair list reached the kernels (read in place by uniform_kernel, or decoded into HBM first)."""
+        i, d = ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.ovl_last_pair_list(self._ctx, ctypes.byref(i), ctypes.byref(d)), self._ctx)
+        return {"in_place_pairs": i.value, "decoded_pairs": d.value}
+
     # ---------------------------------------------------------------- lifecycle
     def close(self) -> None:
         if getattr(self, "_ctx", None):

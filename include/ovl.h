@@ -99,8 +99,8 @@ int32_t ovl_host_pool_rule(int32_t cpus, int32_t sharers, int32_t env_threads);
 int ovl_set_timing(ovl_ctx* ctx, int32_t on);
 int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 /* The scoring launches of the last host-array call made with timing on, in issue order: *out_n = count;
- * entry i < cap gives the device ordinal, the result sink (0 HBM, then copied by the copy engine; 1 int32
- * stored into host memory; 2 packed 2 B/pair into host staging, expanded by host threads), the pairs and
+ * entry i < cap gives the device ordinal, the result sink (1 int32 stored into host memory; 2 packed 2 B/pair
+ * into host staging, expanded by host threads; 0, HBM, only in ovl_score_device), the pairs and
  * the launch's duration in ms (HIP events on its stream).  Any output pointer may be NULL. */
 int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs, double* ms,
                       int32_t* out_n);
@@ -109,6 +109,11 @@ int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t*
  * otherwise; the few packed pairs whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose results crossed packed and
  * were expanded on the host. */
 int ovl_last_transfer(const ovl_ctx* ctx, int64_t* link_bytes, int64_t* packed_pairs);
+/* How the last host-array call's pair list reached the kernels (always recorded): in_place_pairs = pairs of
+ * chunks the scoring kernel read in their compact encoding (b as uint16, a as tile deltas); decoded_pairs =
+ * pairs of compact chunks decoded into HBM first (runs / widen kernels).  Both 0 for a call whose list crossed
+ * as the caller's int32 arrays, or that had no host list. */
+int ovl_last_pair_list(const ovl_ctx* ctx, int64_t* in_place_pairs, int64_t* decoded_pairs);
 
 /* Last error message of `ctx`, or of the calling thread when ctx is NULL. */
 const char* ovl_last_error(const ovl_ctx* ctx);

@@ -176,7 +176,8 @@ def _pair_link_bytes(eng, n):
 @pytest.mark.parametrize("pinned", [False, True])
 def test_ix_in_place_vs_decode(oracle_mod, target, pinned):
     """The a-major target list is read in place (3 B per pair + 4 B per tile); OVL_PAIRS_IX=0 decodes the
-    same encoding's runs into HBM first.  Same results, each path visible in its link bytes."""
+    same encoding's runs into HBM first.  Same results; the path each call took is asserted from
+    ovl_last_pair_list (pairs read in place / decoded), not inferred from its link bytes."""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = target
     n = a.shape[0]
@@ -194,11 +195,11 @@ def test_ix_in_place_vs_decode(oracle_mod, target, pinned):
             s, en = ix.score(a, b)
             np.testing.assert_array_equal(s, ref_s)
             np.testing.assert_array_equal(en, ref_e)
-            lb = _pair_link_bytes(ix, n)
-            assert 3 * n + 4 * (n // 64) <= lb <= 3 * n + 4 * (n // 64 + 64), lb
+            assert ix.last_pair_list() == {"in_place_pairs": n, "decoded_pairs": 0}
         s, en = dec.score(a, b)
         np.testing.assert_array_equal(s, ref_s)
         np.testing.assert_array_equal(en, ref_e)
+        assert dec.last_pair_list() == {"in_place_pairs": 0, "decoded_pairs": n}
         assert _pair_link_bytes(dec, n) < 3 * n  # b16 + runs
     finally:
         ix.close()
@@ -226,7 +227,8 @@ def test_ix_tile_jumps_fall_back(oracle_mod, target):
         s, e = eng.score(a, b)
         np.testing.assert_array_equal(s, ref_s)
         np.testing.assert_array_equal(e, ref_e)
-        assert _pair_link_bytes(eng, n) < 3 * n + 4 * (n // 64)  # some chunks took the runs
+        got = eng.last_pair_list()
+        assert got["decoded_pairs"] > 0 and sum(got.values()) == n, got  # the chunks with a jump took the runs
     finally:
         eng.close()
 

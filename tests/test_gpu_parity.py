@@ -364,29 +364,24 @@ def test_clustered_side_pairs_vs_oracle(engine, oracle_mod, n_short):
     np.testing.assert_array_equal(en, re_)
 
 
-def test_split_knob_equivalence(oracle_mod):
-    """OVL_SPLIT (0 = one wavefront per tile, >0 = latency mode with a side-pair
-    wavefront beside each sweeping one) must not change results, including a list
-    long enough (6250 tiles) to make latency-mode blocks loop over tiles."""
-    import os
+@pytest.mark.parametrize("n_pairs", [100_000, 400_000])
+def test_latency_and_throughput_modes(oracle_mod, n_pairs):
+    """The planner's two uniform-kernel modes give the reference's results: latency mode (a side-pair
+    wavefront beside each sweeping one) up to 8 tiles per CU (131,072 pairs on 256 CUs), throughput mode
+    above -- 400,000 pairs (6,250 tiles) also make its blocks loop over tiles."""
     from ovlgraph import OverlapEngine
     rng = random.Random(42)
     reads = [_rand(rng, 100) for _ in range(400)] + [_rand(rng, rng.randint(1, 99)) for _ in range(30)]
     n = len(reads)
     nr = np.random.default_rng(42)
-    a = nr.integers(0, n, 400_000, dtype=np.int32)
-    b = nr.integers(0, n, 400_000, dtype=np.int32)
+    a = nr.integers(0, n, n_pairs, dtype=np.int32)
+    b = nr.integers(0, n, n_pairs, dtype=np.int32)
     rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
-    for split in ("0", "1", "2"):
-        os.environ["OVL_SPLIT"] = split
-        try:
-            with OverlapEngine(0) as eng:
-                eng.set_reads(reads)
-                sc, en = eng.score(a, b)
-        finally:
-            del os.environ["OVL_SPLIT"]
-        np.testing.assert_array_equal(sc, rs)
-        np.testing.assert_array_equal(en, re_)
+    with OverlapEngine(0) as eng:
+        eng.set_reads(reads)
+        sc, en = eng.score(a, b)
+    np.testing.assert_array_equal(sc, rs)
+    np.testing.assert_array_equal(en, re_)
 
 
 @pytest.mark.parametrize("lw", [31, 32, 64, 100, 128, 150, 250])
@@ -394,11 +389,11 @@ def test_split_knob_equivalence(oracle_mod):
 def test_t_truncated_pairs_in_sweep(oracle_mod, lw, split):
     """Pairs (full-length a, truncated b) are scored inside the uniform sweep (snapshot of block m/32
     after shift m % 32): every m in 0..lw-1, b cut from a's continuation so that the best end sits at
-    or next to m, in throughput (OVL_SPLIT=0) and latency mode (1), several truncated lanes per
-    wavefront with equal and distinct m % 32."""
-    import os
+    or next to m, in throughput mode ("0": 200,000 pairs, above 8 tiles per CU) and latency mode ("1":
+    120,000 pairs), several truncated lanes per wavefront with equal and distinct m % 32."""
     from ovlgraph import OverlapEngine
     rng = random.Random(lw * 3 + int(split))
+    n_list = 200_000 if split == "0" else 120_000
     genome = _rand(rng, 40 * lw)
     starts = list(range(0, 30 * lw, max(1, lw // 5)))
     full = [genome[i:i + lw] for i in starts]
@@ -410,18 +405,14 @@ def test_t_truncated_pairs_in_sweep(oracle_mod, lw, split):
     reads = full + short
     n_full, n = len(full), len(reads)
     nr = np.random.default_rng(lw)
-    a = nr.integers(0, n_full, 120_000, dtype=np.int32)
-    b = np.where(nr.random(120_000) < 0.3, nr.integers(n_full, n, 120_000), nr.integers(0, n, 120_000)).astype(np.int32)
+    a = nr.integers(0, n_full, n_list, dtype=np.int32)
+    b = np.where(nr.random(n_list) < 0.3, nr.integers(n_full, n, n_list), nr.integers(0, n, n_list)).astype(np.int32)
     rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
-    os.environ["OVL_SPLIT"] = split
-    try:
-        with OverlapEngine(0) as eng:
-            eng.set_reads(reads)
-            assert eng.plan() == "ungapped"
-            sc, en = eng.score(a, b)
-            sc_small, en_small = eng.score(a[:3000], b[:3000])
-    finally:
-        del os.environ["OVL_SPLIT"]
+    with OverlapEngine(0) as eng:
+        eng.set_reads(reads)
+        assert eng.plan() == "ungapped"
+        sc, en = eng.score(a, b)
+        sc_small, en_small = eng.score(a[:3000], b[:3000])
     np.testing.assert_array_equal(sc, rs)
     np.testing.assert_array_equal(en, re_)
     np.testing.assert_array_equal(sc_small, rs[:3000])

@@ -101,21 +101,20 @@ def test_pipeline_host_list_pinned_and_pageable(oracle_mod, cfg2, cfg2_ref, chun
         eng.close()
 
 
-@pytest.mark.parametrize("pack,nt,pct", [("1", "1", "25"), ("1", "0", "25"), ("1", "1", "0"), ("1", "1", "60"),
-                                         ("1", "1", "100"), ("0", "1", "25")])
+@pytest.mark.parametrize("pack,pct", [("1", "25"), ("1", "0"), ("1", "60"), ("1", "100"), ("0", "25")])
 @pytest.mark.parametrize("chunk", ["0", "1000"])
-def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, nt, pct, chunk):
+def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk):
     """Results cross the link packed (uint16 score | end << 8) and are expanded on the host: pinned,
     pageable and misaligned caller arrays, list lengths that are not a multiple of the 8-pair step, staging
     slot reuse (many chunks, 1000-pair chunks that are not a multiple of the 64-pair rounding), bad pairs
-    expanded to (-1, -1); non-temporal or ordinary host stores; pinned arrays with 0-100 % of the pairs in
+    expanded to (-1, -1); pinned arrays with 0-100 % of the pairs in
     direct int32 chunks after the packed ones; OVL_PACK=0 is the int32 transport.  (OVL_PACK_MIN=0: packed
     below the default 1 M-pair threshold; OVL_PAIRS_COMPACT=0: the pair list crosses as int32, 8 B/pair --
     the compact encoding has its own tests, test_gpu_compact_pairs.py.)"""
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
-    eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_NT": nt, "OVL_PACK_DIRECT_PCT": pct,
+    eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_DIRECT_PCT": pct,
                        "OVL_PIPE_CHUNK": chunk, "OVL_PAIRS_COMPACT": "0"})
     try:
         eng.set_reads(reads)
@@ -314,14 +313,14 @@ def test_multi_device_context(oracle_mod, cfg2, cfg2_ref):
 
 
 @pytest.mark.parametrize("slots", [2, 3])
-@pytest.mark.parametrize("direct", ["1", "0"])
-def test_multi_device_sharding_on_shared_gpu(oracle_mod, cfg2, cfg2_ref, slots, direct):
+@pytest.mark.parametrize("chunk", ["20000", "0"])
+def test_multi_device_sharding_on_shared_gpu(oracle_mod, cfg2, cfg2_ref, slots, chunk):
     """N-device contexts with every slot on GPU 0 (OVL_SHARE_DEVICES=1): the Σ n·m shards of host and
     device lists, per-device kernels and their slices of pinned / pageable results, the gapped and banded
-    kernels, with kernels storing through host mappings (direct) and through copy-engine transfers."""
+    kernels storing through host mappings, in 20,000-pair pipeline chunks and in the automatic ones."""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
-    eng = _engine_env({"OVL_SHARE_DEVICES": "1", "OVL_PIPE_DIRECT": direct, "OVL_PIPE_CHUNK": "20000"},
+    eng = _engine_env({"OVL_SHARE_DEVICES": "1", "OVL_PIPE_CHUNK": chunk},
                       devices=[0] * slots)
     try:
         assert eng.devices == [0] * slots
