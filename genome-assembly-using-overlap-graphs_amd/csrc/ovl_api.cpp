@@ -103,6 +103,9 @@ constexpr int64_t kLaneMinPairs = 65536;
 // uniform_kernel grid cap, blocks of 256 per CU: ~1 tile per wavefront at the target point, the dispatcher
 // balances the tail (measured -2.3 % against 8 per CU; 16 / 32 / 64: 69.2 / 68.6 / 68.4 us)
 constexpr int64_t kBlocksPerCu = 32;
+// band knob: two lanes per pair (band_lane2_kernel) from this half-width (one lane's 2W+1 band cells no longer fit
+// the registers of several waves per SIMD)
+constexpr int32_t kBandLane2Min = 40;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
 
@@ -607,6 +610,8 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                 case OVL_BAND_FORM_STRIP: g.band_form = OVL_BAND_FORM_STRIP; break;
                 case OVL_BAND_FORM_DIAG: g.band_form = diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST; break;
                 case OVL_BAND_FORM_LANE:
+                case OVL_BAND_FORM_LANE1:
+                case OVL_BAND_FORM_LANE2:
                     g.band_form = lane_ok ? OVL_BAND_FORM_LANE : (diag_ok ? OVL_BAND_FORM_DIAG : OVL_BAND_FORM_FAST);
                     break;
                 default:
@@ -623,6 +628,8 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                 k.pfx_words = as<uint32_t>(c->pfx);
                 k.srow = c->srow;
                 k.wsfx = c->wmax;
+                k.split = c->band_form == OVL_BAND_FORM_LANE2 ||
+                          (c->band_form != OVL_BAND_FORM_LANE1 && g.band >= kBandLane2Min);
                 HIPCHK(c, ovl_launch_band_lane(&g, &k, s));
                 HIPCHK(c, scratch_release(c, s));
                 return OVL_OK;
@@ -655,6 +662,8 @@ Knobs read_knobs() {
         else if (!strcmp(e, "fast")) k.band_form = OVL_BAND_FORM_FAST;
         else if (!strcmp(e, "strip")) k.band_form = OVL_BAND_FORM_STRIP;
         else if (!strcmp(e, "lane")) k.band_form = OVL_BAND_FORM_LANE;
+        else if (!strcmp(e, "lane1")) k.band_form = OVL_BAND_FORM_LANE1;
+        else if (!strcmp(e, "lane2")) k.band_form = OVL_BAND_FORM_LANE2;
     }
     if (const char* e = getenv("OVL_DP_CLASSIC")) k.dp_classic = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_DP_LANE")) k.dp_lane = atoi(e) ? 1 : 0;

@@ -469,15 +469,16 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
                 tnew = it + ub < 0 ? PAD : tnew;
             }
             const uint32_t x4 = __builtin_amdgcn_perm(0u, x, 0u);  // x in every byte
-            uint32_t P[NBW];
-#pragma unroll
-            for (int w = 0; w < NBW; ++w) {
-                P[w] = __builtin_amdgcn_perm(tbl_hi, tbl_lo, T[w] ^ x4);
-                if constexpr (MASKED) P[w] = it < sk ? p_virt : P[w];
-            }
+            // the profile word of cells 4w..4w+3, built just before its cells (one live word, not NBW: band 64
+            // keeps 129 cells and 33 window words in registers)
+            uint32_t P = 0;
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
-                const int32_t d = V[k] + (int32_t)(int8_t)(uint8_t)(P[k >> 2] >> (8 * (k & 3)));
+                if ((k & 3) == 0) {
+                    P = __builtin_amdgcn_perm(tbl_hi, tbl_lo, T[k >> 2] ^ x4);
+                    if constexpr (MASKED) P = it < sk ? p_virt : P;
+                }
+                const int32_t d = V[k] + (int32_t)(int8_t)(uint8_t)(P >> (8 * (k & 3)));
                 if constexpr (NB == 1) V[k] = d;
                 else if (k == 0) V[k] = max(d, V[k + 1]);
                 else if (k == NB - 1) V[k] = max(d, V[k - 1]);
@@ -531,6 +532,229 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
             } else {
                 out_score[p] = best;
                 out_end[p] = bend;
+            }
+        }
+    }
+}
+
+
+// ----------------------------------------------------------------------------- band knob, two lanes per pair
+//
+// band_lane_kernel keeps a pair's NB = 2W+1 band cells in one lane: at band 64 that is 129 cells plus 33
+// window words, one wavefront per SIMD.  Here lanes 2q and 2q+1 share pair q, each with H = (NB + 1) / 2
+// cells: lane 0 holds diagonals k = -1 .. H-2 (k = -1 a dummy held at -inf, the left edge of k = 0), lane 1
+// holds k = H-1 .. NB-1.  A row's update is serial in k (the left move), and a row needs the previous row's
+// k+1 (the up move), so the two halves of one row cannot run at once -- but lane 1 can run one row BEHIND
+// lane 0: at step t lane 0 updates row iteration t and lane 1 row iteration t-1.  Then
+//   * lane 1's first cell (k = H-1) takes as left lane 0's last cell (k = H-2) of iteration t-1, which
+//     lane 0 finished in step t-1 (one DPP swap at the step's start);
+//   * lane 0's last cell takes as up the value of cell k = H-1 after iteration t-1, which lane 1 computes
+//     as the FIRST cell of this same step, before lane 0 reaches its last (one DPP swap after cell 0);
+//   * the window slides one position per row, and the code entering lane 0's top is the one at lane 1's
+//     bottom after lane 1's slide of the same step (one DPP swap); lane 1's top takes the code entering the
+//     band, as in band_lane_kernel.
+// Both lanes derive the row symbol and the entering code of iteration t; lane 1 uses the previous step's.
+// Lane 1's extra first step (iteration -1) is a virtual row, which maps the row-0 pattern onto itself, so
+// its cells start one iteration earlier; lane 0 is done after step R-1 (its row-n scan runs then) and lane
+// 1 after step R.  The cells are the oracle's band edges exactly as in band_lane_kernel.
+template <int NB, int OCC, bool PL>
+__global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __restrict__ codes,
+                                                              const int64_t* __restrict__ off,
+                                                              const int32_t* __restrict__ len, int32_t n_reads,
+                                                              const uint32_t* __restrict__ sfx,
+                                                              const uint32_t* __restrict__ pfx, int32_t prow,
+                                                              int32_t wpl, const int32_t* __restrict__ a_idx,
+                                                              const int32_t* __restrict__ b_idx, int64_t n_pairs,
+                                                              int32_t lcap, int32_t match, int32_t mismatch,
+                                                              int32_t indel, int32_t* __restrict__ out_score,
+                                                              int32_t* __restrict__ out_end,
+                                                              const int32_t* __restrict__ seed,
+                                                              uint32_t* __restrict__ err_flag) {
+    static_assert(NB % 2 == 1 && NB >= 3, "NB = 2W + 1");
+    constexpr int W = (NB - 1) / 2;
+    constexpr int H = (NB + 1) / 2;   // cells per lane (lane 0: one dummy)
+    constexpr int HW = (H + 3) / 4;   // window words per lane
+    constexpr uint32_t PAD = 4;       // t code left of the read
+    constexpr int32_t NEG = -(1 << 30);
+    const int lane = threadIdx.x & 63;
+    const int h = lane & 1;           // which half of its pair
+    const int64_t wslot = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t nslots = (int64_t)gridDim.x * 4;
+    const int64_t ntiles = (n_pairs + 31) >> 5;  // 32 pairs per wavefront
+    const int32_t g = indel;
+    const uint32_t b_ma = (uint32_t)(match - 2 * g) & 0xFFu;
+    const uint32_t b_mm = (uint32_t)(mismatch - 2 * g) & 0xFFu;
+    const uint32_t b_pad = (uint32_t)(-2 * g) & 0xFFu;
+    const uint32_t tbl_lo = b_ma | (b_mm << 8) | (b_mm << 16) | (b_mm << 24);  // x ^ t = 0..3
+    const uint32_t tbl_hi = b_pad * 0x01010101u;                             // x ^ t = 4..7
+    const uint32_t p_virt = ((uint32_t)(-g) & 0xFFu) * 0x01010101u;
+    const int32_t kbase = h ? H - 1 : -1;  // diagonal of local cell 0
+    // the partner lane's value (lanes 2q <-> 2q+1)
+    auto swap = [](int32_t v) -> int32_t { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); };
+    for (int64_t tile = wslot; tile < ntiles; tile += nslots) {
+        const int64_t p = tile * 32 + (lane >> 1);
+        const bool live = p < n_pairs;
+        int32_t a = live ? a_idx[p] : 0;
+        int32_t b = live ? b_idx[p] : 0;
+        bool bad = live && (a < 0 || a >= n_reads || b < 0 || b >= n_reads);
+        if (!live || bad) { a = 0; b = 0; }
+        int32_t n = (live && !bad) ? len[a] : 0;
+        int32_t m = (live && !bad) ? len[b] : 0;
+        int32_t jstar = (live && !bad) ? seed[p] : 0;
+        if (n > lcap || m > lcap || jstar < 0 || jstar > m) { bad = bad || live; n = 0; m = 0; jstar = 0; }
+        const uint32_t sa = (uint32_t)off[a];
+        const uint32_t tb = (uint32_t)off[b];
+        const int32_t cc = n - jstar + W;  // j = i - cc + k
+        const int32_t nmax = wave_max(n);
+        const int32_t nmin = wave_min(n);
+        constexpr int RQ = PL ? 32 : 4;
+        const int32_t R = (nmax + RQ - 1) / RQ * RQ;  // row iterations (end-aligned rows)
+        const int32_t sk = R - n;
+        const int32_t mcut = R - nmin;
+        auto tcode = [&](int32_t u) -> uint32_t {
+            const int32_t uc = u < 0 ? 0 : (u >= m ? (m > 0 ? m - 1 : 0) : u);
+            const uint32_t v = (uint32_t)codes[tb + (uint32_t)uc];
+            return u < 0 ? PAD : v;
+        };
+        // the window of the lane's first iteration (-h): local cell j is diagonal kbase + j, t position
+        // u0 - h + kbase + j; the cells start as the row pattern G = -indel * j before that iteration
+        const int32_t u0 = -sk - cc;
+        const int32_t uw = u0 - h + kbase;
+        uint32_t T[HW];
+#pragma unroll
+        for (int w = 0; w < HW; ++w) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * w + q < H) word |= tcode(uw + 4 * w + q) << (8 * q);
+            T[w] = word;
+        }
+        int32_t V[H];
+#pragma unroll
+        for (int j = 0; j < H; ++j) V[j] = -g * (uw + j);
+        if (!h) V[0] = NEG;
+        const int32_t ub = NB - sk - cc;  // the code entering after iteration it is at t position it + ub
+        constexpr int NQ = PL ? 1 : 4;
+        uint32_t qs[NQ], qt[NQ];
+        auto fetch4 = [&](int32_t it4) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const int32_t i0 = it4 + k - sk;  // s index i - 1
+                const int32_t ic = i0 < 0 ? 0 : (i0 >= n ? (n > 0 ? n - 1 : 0) : i0);
+                qs[k] = (uint32_t)codes[sa + (uint32_t)ic];
+                qt[k] = tcode(it4 + k + ub);
+            }
+        };
+        const uint32_t* __restrict__ sp = sfx + (int64_t)a * prow + 2 * (wpl - R / 32);
+        const uint32_t* __restrict__ tp = pfx + (int64_t)b * prow;
+        const uint32_t tsh = (uint32_t)ub & 31u;
+        uint32_t S0 = 0, S1 = 0, T0 = 0, T1 = 0;
+        uint2 sn = make_uint2(0, 0), t0n = sn, t1n = sn;
+        auto fetch_planes = [&](int32_t kb) {
+            sn = *reinterpret_cast<const uint2*>(sp + 2 * kb);
+            const int32_t q = (32 * kb + ub) >> 5;  // floor
+            const int32_t q0 = q < 0 ? 0 : (q >= wpl ? wpl - 1 : q);
+            const int32_t q1 = q + 1 < 0 ? 0 : (q + 1 >= wpl ? wpl - 1 : q + 1);
+            t0n = *reinterpret_cast<const uint2*>(tp + 2 * q0);
+            t1n = *reinterpret_cast<const uint2*>(tp + 2 * q1);
+        };
+        uint32_t x_prev = 0, tn_prev = 0;  // the row symbol / entering code of the previous step's iteration
+        // step t: lane 0 runs iteration t, lane 1 iteration t - 1 (x_c / tn_c: iteration t's)
+        auto step = [&](int32_t t, uint32_t x_c, uint32_t tn_c, auto masked_tag) {
+            constexpr bool MASKED = decltype(masked_tag)::value;
+            const int32_t it = t - h;
+            const uint32_t x = h ? x_prev : x_c;
+            const uint32_t tnew = h ? tn_prev : tn_c;
+            x_prev = x_c;
+            tn_prev = tn_c;
+            const uint32_t x4 = __builtin_amdgcn_perm(0u, x, 0u);  // x in every byte
+            // left of local cell 0: lane 1 takes lane 0's last cell of iteration t - 1 (finished last step)
+            const int32_t carry = swap(V[H - 1]);
+            int32_t left = h ? carry : NEG;
+            int32_t upin = NEG;
+            uint32_t P = 0;
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                if ((j & 3) == 0) {
+                    P = __builtin_amdgcn_perm(tbl_hi, tbl_lo, T[j >> 2] ^ x4);
+                    if constexpr (MASKED) P = it < sk ? p_virt : P;
+                }
+                const int32_t d = V[j] + (int32_t)(int8_t)(uint8_t)(P >> (8 * (j & 3)));
+                const int32_t up = j + 1 < H ? V[j + 1] : upin;
+                int32_t v = max(max(d, up), left);
+                if (j == 0) {
+                    if (!h) v = NEG;  // lane 0's dummy: the missing left of k = 0
+                    // lane 0's last cell takes as up lane 1's cell 0 after iteration t - 1 (just computed)
+                    const int32_t r = swap(v);
+                    upin = h ? NEG : r;
+                }
+                V[j] = v;
+                left = v;
+            }
+            // slide the window one position; lane 0's top takes lane 1's new bottom code, lane 1's top the
+            // code entering the band
+#pragma unroll
+            for (int w = 0; w < HW; ++w) T[w] = __builtin_amdgcn_alignbit(w + 1 < HW ? T[w + 1] : 0u, T[w], 8);
+            const uint32_t bottom = (uint32_t)swap((int32_t)(T[0] & 0xFFu));
+            T[(H - 1) >> 2] |= (h ? tnew : bottom) << (8 * ((H - 1) & 3));
+        };
+        auto body = [&](int32_t t, auto masked_tag) {
+            if constexpr (PL) {
+                if ((t & 31) == 0) {  // next 32 rows: rotate the block words, prefetch the block after
+                    S0 = sn.x;
+                    S1 = sn.y;
+                    T0 = __builtin_amdgcn_alignbit(t1n.x, t0n.x, tsh);
+                    T1 = __builtin_amdgcn_alignbit(t1n.y, t0n.y, tsh);
+                    if (t + 32 < R) fetch_planes((t + 32) >> 5);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t r = (uint32_t)(t + k) & 31u;
+                    const uint32_t xc = __builtin_amdgcn_ubfe(S0, r, 1) | (__builtin_amdgcn_ubfe(S1, r, 1) << 1);
+                    uint32_t tc = __builtin_amdgcn_ubfe(T0, r, 1) | (__builtin_amdgcn_ubfe(T1, r, 1) << 1);
+                    tc = t + k + ub < 0 ? PAD : tc;
+                    step(t + k, xc, tc, masked_tag);
+                }
+            } else {
+                uint32_t s4[4], t4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { s4[k] = qs[k]; t4[k] = qt[k]; }
+                if (t + 4 < R) fetch4(t + 4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) step(t + k, s4[k], t4[k], masked_tag);
+            }
+        };
+        // row n on this lane's cells: in-band cells with 0 <= j <= m, largest value, first j
+        int32_t best = INT32_MIN, bend = -1;
+        auto scan = [&]() {
+#pragma unroll
+            for (int jl = 0; jl < H; ++jl) {
+                const int32_t j = jstar - W + kbase + jl;
+                const int32_t v = V[jl] + g * (n + j);
+                const bool better = (h || jl > 0) && j >= 0 && j <= m && v > best;
+                best = better ? v : best;
+                bend = better ? j : bend;
+            }
+        };
+        if constexpr (PL) fetch_planes(0);
+        else fetch4(0);
+        int32_t t = 0;
+        for (; t < mcut + 1 && t < R; t += 4) body(t, std::true_type{});
+        for (; t < R; t += 4) body(t, std::false_type{});
+        if (!h) scan();  // lane 0 has finished iteration R - 1
+        // step R: lane 1's last iteration (R - 1); lane 0's cells are no longer read
+        step(R, 0u, 0u, std::true_type{});
+        if (h) scan();
+        const int32_t ob = swap(best), oe = swap(bend);
+        if (live && !h) {
+            if (bad) {
+                ovl_flag_error(err_flag);
+                out_score[p] = -1;
+                out_end[p] = -1;
+            } else {
+                const bool hi_wins = ob > best;  // lane 1's cells lie right of lane 0's: ties keep lane 0's
+                out_score[p] = hi_wins ? ob : best;
+                out_end[p] = hi_wins ? oe : bend;
             }
         }
     }
@@ -595,15 +819,36 @@ hipError_t launch_band_lane_w(const OvlDpArgs* g, const OvlLaneArgs* k, int64_t 
     return hipGetLastError();
 }
 
+// two lanes per pair (band_lane2_kernel): H = W + 1 cells per lane, 32 pairs per wavefront
+template <int W, bool PL>
+hipError_t launch_band_lane2_w(const OvlDpArgs* g, const OvlLaneArgs* k, hipStream_t stream) {
+    constexpr int NB = 2 * W + 1;
+    constexpr int H = W + 1;
+    constexpr int OCC = H <= 17 ? 6 : (H <= 33 ? 4 : 3);
+    const int64_t tiles = (g->n_pairs + 31) / 32;
+    int64_t blocks = (std::min<int64_t>(k->slots / 6 * OCC, tiles) + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    ovl::band_lane2_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
+        g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx,
+        g->n_pairs, g->mcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,
+        g->seed, g->err_flag);
+    return hipGetLastError();
+}
+
 // every half-width up to 32, then 40, 48, 56, 64 (other widths above 32 take the anti-diagonal form)
 constexpr int next_band_lane(int w) { return w < 32 ? w + 1 : w + 8; }
 
 template <int W>
 hipError_t dispatch_band_lane(int band, const OvlDpArgs* g, const OvlLaneArgs* k, int64_t blocks,
                               hipStream_t stream) {
-    if (band == W)
+    if (band == W) {
+        if constexpr (W >= 1)
+            if (k->split)
+                return k->sfx ? launch_band_lane2_w<W, true>(g, k, stream)
+                              : launch_band_lane2_w<W, false>(g, k, stream);
         return k->sfx ? launch_band_lane_w<W, true>(g, k, blocks, stream)
                       : launch_band_lane_w<W, false>(g, k, blocks, stream);
+    }
     if constexpr (W < kBandLaneMax) return dispatch_band_lane<next_band_lane(W)>(band, g, k, blocks, stream);
     return hipErrorInvalidValue;
 }

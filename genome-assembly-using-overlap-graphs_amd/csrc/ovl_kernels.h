@@ -49,7 +49,10 @@ enum {
     OVL_BAND_FORM_ROWS = 1,   // band_row_kernel: lanes on band diagonals, a row per step (<= 192 lanes)
     OVL_BAND_FORM_FAST = 2,   // dp_fast_kernel<int32_t, true>: chunked strips with band masks
     OVL_BAND_FORM_DIAG = 3,   // band_diag_kernel: lanes on band diagonals, an anti-diagonal per step
-    OVL_BAND_FORM_LANE = 4,   // band_lane_kernel: a lane per pair, band diagonals in registers (band <= 32)
+    OVL_BAND_FORM_LANE = 4,   // band_lane_kernel (a lane per pair, band diagonals in registers) or, from
+                              // kBandLane2Min, band_lane2_kernel (two lanes per pair, one row apart)
+    OVL_BAND_FORM_LANE1 = 5,  // band_lane_kernel at every width it has (tests, A/B)
+    OVL_BAND_FORM_LANE2 = 6,  // band_lane2_kernel at every width it has (tests, A/B)
 };
 
 struct OvlDpArgs {
@@ -109,6 +112,7 @@ struct OvlLaneArgs {
     int32_t wsfx;
     uint32_t* colbuf;
     int64_t slots;              // resident wavefront slots (one hand-off column each)
+    int32_t split;              // band knob: two lanes per pair (band_lane2_kernel) instead of one
 };
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);

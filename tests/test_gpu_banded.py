@@ -94,8 +94,8 @@ def test_banded_cfg5_sample(engine, oracle_mod):
 
 def test_banded_cfg5_full_list(engine, oracle_mod):
     """Config 5 at full size: every one of the 3.38 M candidate pairs at band 8 (the sweep's lane-kernel
-    form over the whole list, every tile and length mix), and a 500k strided sample at band 64 (one
-    wavefront per SIMD, the widest lane-kernel band), against oracle_overlap_banded."""
+    form over the whole list, every tile and length mix), and a 500k strided sample at band 64 (two lanes
+    per pair, one row apart: the widest lane-kernel band), against oracle_overlap_banded."""
     from ovlgraph.candidates import dedup_reads, enumerate_candidates
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads("cfg5"))
@@ -120,7 +120,8 @@ def test_banded_unsupported_magnitudes(engine):
         engine.score([0], [1], 2 ** 28, -1, -1, 4)
 
 
-FORMS = {"default": {}, "lane": {"OVL_BAND_FORM": "lane"}, "diag": {"OVL_BAND_FORM": "diag"},
+FORMS = {"default": {}, "lane": {"OVL_BAND_FORM": "lane"}, "lane1": {"OVL_BAND_FORM": "lane1"},
+         "lane2": {"OVL_BAND_FORM": "lane2"}, "diag": {"OVL_BAND_FORM": "diag"},
          "rows": {"OVL_BAND_FORM": "rows"}, "fast": {"OVL_BAND_FORM": "fast"}, "strip": {"OVL_BAND_FORM": "strip"}}
 
 
@@ -140,7 +141,9 @@ def _score_with_env(env, reads, a, b, params, band):
 @pytest.mark.parametrize("band", [0, 1, 2, 3, 8, 15, 16, 31, 32, 33, 63, 64, 95, 96, 150, 255, 256])
 @pytest.mark.parametrize("form", sorted(FORMS))
 def test_band_forms_agree_with_oracle(oracle_mod, reads_pairs, band, form):
-    """The band knob has five kernels: a lane per pair (band <= 32; the default for >= 65,536 pairs),
+    """The band knob has six kernels: a lane per pair (band <= 32, or <= 64 in steps of 8; the default for
+    >= 65,536 pairs), two lanes per pair one row apart (the lane form's choice from band 40; lane1 / lane2
+    force either),
     the anti-diagonal form (the default below that), the row form (lanes on band diagonals, a row per
     step; up to 192 lanes), the chunked strip kernel with band masks and the classic strip form,
     picked with OVL_BAND_FORM: each must equal the oracle (lane falls back above band 32)."""
@@ -171,11 +174,13 @@ def test_banded_long_reads_vs_oracle(engine, oracle_mod, band):
                                     (5, -4, 0), (0, 0, -1), (-1, -2, -1), (100, -90, -60), (2, -1, 3)])
 @pytest.mark.parametrize("band", [0, 1, 4, 8, 13, 24, 32, 40, 48, 56, 64])
 @pytest.mark.parametrize("planes", ["1", "0"])
-def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes):
-    """The lane-per-pair band kernel over mixed lengths (empty reads, reads shorter than the band,
-    seed diagonals left and right of the table) and scorings inside and outside its int8 byte scores
-    (those fall back to the anti-diagonal form).  planes=1 reads row symbols and t codes from the
-    resident bit planes, planes=0 gathers code bytes (OVL_LANE_SFX)."""
+@pytest.mark.parametrize("lanes", ["1", "2"])
+def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes, lanes):
+    """The band lane kernels over mixed lengths (empty reads, reads shorter than the band, seed
+    diagonals left and right of the table) and scorings inside and outside their int8 byte scores
+    (those fall back to the anti-diagonal form): one lane per pair (lanes=1) and two lanes per pair one
+    row apart (lanes=2; band 0 has one cell and stays on one lane).  planes=1 reads row symbols and t
+    codes from the resident bit planes, planes=0 gathers code bytes (OVL_LANE_SFX)."""
     rng = random.Random(band * 31 + sum(params) % 97)
     lens = [0, 1, 2, 3, 7, 16, 31, 33, 64, 100, 180, 250]
     reads = ["".join(rng.choice("ACGT") for _ in range(rng.choice(lens))) for _ in range(160)]
@@ -184,6 +189,6 @@ def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes):
     a = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
     b = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
     rs, re_ = oracle_mod.batch_banded(reads, a, b, *params, band)
-    sc, en = _score_with_env({"OVL_BAND_FORM": "lane", "OVL_LANE_SFX": planes}, reads, a, b, params, band)
+    sc, en = _score_with_env({"OVL_BAND_FORM": "lane" + lanes, "OVL_LANE_SFX": planes}, reads, a, b, params, band)
     np.testing.assert_array_equal(sc, rs)
     np.testing.assert_array_equal(en, re_)

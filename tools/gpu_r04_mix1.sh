@@ -11,3 +11,6 @@ tail -2 $OUT/tests.log
 bash tools/gpu_r04_shard_ab.sh ${1:-r04d} || exit 1
 timeout -k 10 400 python -u tools/replay_ab.py 5 > $OUT/replay_ab.json 2> $OUT/replay_ab.err || { echo "replay ab failed"; tail -30 $OUT/replay_ab.err; exit 1; }
 echo "replay ab ok"
+OVL_TRACE_PIPE=1 timeout -k 10 200 python -u tools/one_shot_timeline.py 20 > $OUT/one_shot.txt 2> $OUT/one_shot_trace.txt || { echo "one-shot timeline failed"; tail -20 $OUT/one_shot_trace.txt; exit 1; }
+cat $OUT/one_shot.txt
+bash tools/gpu_r04_mix2.sh ${1:-r04d} || exit 1
