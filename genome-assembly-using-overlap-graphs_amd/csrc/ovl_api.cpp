@@ -217,6 +217,12 @@ struct ovl_ctx {
     std::vector<Dev*> devs;
     ReadStage stage;             // pinned upload stage of ovl_set_reads
     HostReads hreads;            // ovl_set_reads' host arrays (reused)
+    // the read set resident on every device after the last complete ovl_set_reads: its offsets relative to
+    // offsets[0] and its bytes, so that a call with the same read set (a graph build per k over one read set,
+    // the one-shot ovl_score_pairs per build) keeps it instead of uploading and packing it again
+    std::vector<int64_t> res_off;
+    std::vector<uint8_t> res_bytes;
+    bool res_valid = false;
     std::string err;
     std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
     int32_t timing = 0;          // ovl_set_timing
@@ -2008,6 +2014,29 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
 
 namespace {
 
+// The caller's read set equals the resident one, byte for byte (offsets relative to offsets[0], then the bytes;
+// compared over the host pool, a part stops at its first difference).
+bool same_reads(const ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
+    if (!c->res_valid || (int64_t)c->res_off.size() != (int64_t)n_reads + 1) return false;
+    for (const Dev* d : c->devs)
+        if (d->n_reads != n_reads) return false;
+    const int64_t base = n_reads > 0 ? offsets[0] : 0;
+    if (n_reads > 0 && offsets[n_reads] - base != (int64_t)c->res_bytes.size()) return false;
+    CopyPool& pool = CopyPool::get();
+    std::atomic<bool> differ{false};
+    pool.parallel((size_t)n_reads + 1, size_t(1) << 14, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi && !differ.load(std::memory_order_relaxed); ++i)
+            if (offsets[i] - base != c->res_off[i]) differ.store(true, std::memory_order_relaxed);
+    });
+    if (differ.load() || c->res_bytes.empty()) return !differ.load();
+    if (!seqs) return false;
+    pool.parallel(c->res_bytes.size(), size_t(1) << 18, [&](size_t lo, size_t hi) {
+        if (!differ.load(std::memory_order_relaxed) && memcmp(seqs + base + lo, c->res_bytes.data() + lo, hi - lo))
+            differ.store(true, std::memory_order_relaxed);
+    });
+    return !differ.load();
+}
+
 // ovl_set_reads; sync = false (ovl_score_pairs) leaves the uploads running on each device's kernel stream --
 // the scoring launches queue behind them there -- and the caller synchronises those streams before it returns
 // (the pinned stage must outlive the copy)
@@ -2015,7 +2044,18 @@ int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
     if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
+    if (n_reads > 0 && offsets[0] < 0) return fail(c, OVL_E_ARG, "offsets[0] < 0");
+    if (n_reads > 0 && offsets[n_reads] > offsets[0] && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
     DeviceGuard guard;
+    if (same_reads(c, seqs, offsets, n_reads)) {
+        // already resident on every device: only the candidate list goes, as after an upload
+        for (Dev* d : c->devs) {
+            d->cand_n = -1;
+            d->heavy_for = -1;
+        }
+        return OVL_OK;
+    }
+    c->res_valid = false;
     PipeTrace trace;  // OVL_TRACE_PIPE: r recount, p prepared, s staged, u uploads issued, y synchronised
     CpuShare::get().refresh();
     trace.mark('r', 0);
@@ -2058,6 +2098,13 @@ int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n
         d->n_reads = n_reads;
     }
     c->h_len.assign(h.len.begin(), h.len.begin() + n_reads);
+    // what is resident now (for same_reads)
+    const int64_t base = n_reads > 0 ? offsets[0] : 0;
+    c->res_off.resize((size_t)n_reads + 1);
+    for (int32_t i = 0; i <= n_reads; ++i) c->res_off[(size_t)i] = n_reads > 0 ? offsets[i] - base : 0;
+    c->res_bytes.resize((size_t)h.total);
+    if (h.total > 0) host_copy(c->res_bytes.data(), seqs + base, (size_t)h.total);
+    c->res_valid = true;
     return OVL_OK;
 }
 

@@ -43,6 +43,47 @@ static int take(PyObject* obj, Py_buffer* view, Py_ssize_t itemsize, const char*
     return 0;
 }
 
+/* Attribute dicts: a copy of the two-key template with its values set.  On CPython 3.10 a split-table
+   template (PEP 412 key-sharing: an instance __dict__) is copied with its values array, and the two values
+   are written into that array directly (indices iw / ie of the template's key table, found once by
+   attr_slots) instead of two PyDict_SetItem lookups; any other dict takes the SetItem path. */
+static void attr_slots(PyObject* tmpl, PyObject* kw, PyObject* ke, Py_ssize_t* iw, Py_ssize_t* ie) {
+    *iw = *ie = -1;
+#if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030B0000
+    if (((PyDictObject*)tmpl)->ma_values == NULL || PyDict_GET_SIZE(tmpl) != 2) return;
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    while (PyDict_Next(tmpl, &pos, &k, &v)) {  /* (split table: pos - 1 is the slot in ma_values) */
+        if (k == kw) *iw = pos - 1;
+        else if (k == ke) *ie = pos - 1;
+    }
+    if (*iw < 0 || *ie < 0) *iw = *ie = -1;
+#else
+    (void)tmpl; (void)kw; (void)ke;
+#endif
+}
+
+static PyObject* new_attr(PyObject* tmpl, PyObject* kw, PyObject* ke, Py_ssize_t iw, Py_ssize_t ie, PyObject* wv,
+                          PyObject* ev) {
+    PyObject* d = PyDict_Copy(tmpl);
+    if (!d) return NULL;
+#if PY_VERSION_HEX >= 0x030A0000 && PY_VERSION_HEX < 0x030B0000
+    PyObject** vals = ((PyDictObject*)d)->ma_values;
+    if (iw >= 0 && vals) {
+        Py_INCREF(wv);
+        Py_XSETREF(vals[iw], wv);
+        Py_INCREF(ev);
+        Py_XSETREF(vals[ie], ev);
+        return d;
+    }
+#endif
+    if (PyDict_SetItem(d, kw, wv) || PyDict_SetItem(d, ke, ev)) {
+        Py_DECREF(d);
+        return NULL;
+    }
+    return d;
+}
+
 static PyObject* build(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *names, *ou, *ov, *ow, *oe, *shared = NULL;
@@ -527,6 +568,8 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
             tmpl = PyDict_New();
             if (!tmpl || PyDict_SetItem(tmpl, kw, Py_None) || PyDict_SetItem(tmpl, ke, Py_None)) goto done;
         }
+        Py_ssize_t iw, ie;
+        attr_slots(tmpl, kw, ke, &iw, &ie);
         /* one pass over the edges in global insertion order (pair, copy of a, copy of b: overlapGraphs.py:43-60):
            each attribute dict goes into its tail's successor dict and its head's predecessor dict while it is
            still in cache.  A node's successors arrive in that order too, which is its CSR row order. */
@@ -544,9 +587,8 @@ static PyObject* build_overlap(PyObject* self, PyObject* args) {
                         ev = int_of(ints, en[p]);
                         if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
                     }
-                    PyObject* d = PyDict_Copy(tmpl);
-                    const int bad = !d || PyDict_SetItem(d, kw, wv) || PyDict_SetItem(d, ke, ev) ||
-                                    PyDict_SetItem(sin[u], PyList_GET_ITEM(names, vb + cb), d) ||
+                    PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
+                    const int bad = !d || PyDict_SetItem(sin[u], PyList_GET_ITEM(names, vb + cb), d) ||
                                     PyDict_SetItem(pin[vb + cb], un, d);
                     Py_XDECREF(d);
                     if (bad) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }

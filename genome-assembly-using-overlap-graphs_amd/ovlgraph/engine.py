@@ -251,6 +251,24 @@ class OverlapEngine:
                                                  _ptr(sc), _ptr(en)), self._ctx)
         return sc, en
 
+    def range_scorer(self, lo: int, hi: int, out, match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT,
+                     band: int = -1):
+        """Pre-bound ``score_candidates_range(lo, hi, ..., out=out)`` for repeated steps over the same shard and
+        arrays: every argument converted to its ctypes form once, so a step costs one foreign call (the
+        sharded step of a multi-process job calls it every step).  ``out`` must stay alive while it is used."""
+        sc, en = _outputs(int(hi) - int(lo), out)
+        fn = self._L.ovl_score_candidates_range
+        ctx = self._ctx
+        args = (ctx, ctypes.c_int64(int(lo)), ctypes.c_int64(int(hi)), ctypes.c_int32(match), ctypes.c_int32(mismatch),
+                ctypes.c_int64(indel), ctypes.c_int32(band), _ptr(sc), _ptr(en))
+        check(self._L.ovl_plan(ctx, match, mismatch, indel, band, ctypes.byref(ctypes.c_int32())), ctx)
+
+        def score() -> None:
+            rc = fn(*args)
+            if rc:
+                check(rc, ctx)
+        return score
+
     def candidate_shards(self, n_shards: int) -> List[int]:
         """Shard bounds of the resident candidate list balanced by sum len(a)*len(b) + 1 (on the device)."""
         bounds = np.zeros(int(n_shards) + 1, dtype=np.int64)

@@ -308,6 +308,10 @@ class ShardedStep:
             self.shared = SharedResults(self.n_pairs, group, tag=str(os.environ.get("MASTER_PORT", "")))
             if self.eng is not None:
                 self.shared.pin(lo, hi)
+                if self.on_device_list and hi > lo:
+                    # one foreign call per step (ctypes arguments converted once)
+                    self._launch = self.eng.range_scorer(lo, hi, (self.shared.score[lo:hi], self.shared.end[lo:hi]),
+                                                         match, mismatch, indel, band)
         else:
             self.packed = torch.full((2, self.width), -1, dtype=torch.int32, device=self.device)
             self.rows = ([torch.empty_like(self.packed) for _ in range(self.world)] if self.rank == 0 else None)
@@ -350,14 +354,14 @@ class ShardedStep:
                     self.shared.release(k - 1)  # rank 0 is done with step k - 1's results
                 else:
                     self.shared.wait_released(k - 1)
-            if hi > lo:
+            if self._launch is not None:
+                self._launch()
+            elif hi > lo:
                 out = (self.shared.score[lo:hi], self.shared.end[lo:hi])
                 if self.eng is None:
                     sc, en = self._local()
                     out[0][:] = sc
                     out[1][:] = en
-                elif self.on_device_list:
-                    self.eng.score_candidates_range(lo, hi, *self.scoring, out=out)
                 else:
                     self.eng.score(self.a[lo:hi], self.b[lo:hi], *self.scoring, out=out)
             if self.fence == "barrier":
@@ -397,6 +401,7 @@ class ShardedStep:
 
     def close(self) -> None:
         import torch.distributed as dist
+        self._launch = None  # (holds views of the shared buffer)
         if self.shared is not None:
             if self.fence == "shm" and self.rank == 0:
                 self.shared.release(self.steps)
