@@ -841,10 +841,9 @@ class CopyPool {
         return b;
     }
     // f(i, lo, hi) for every part i of `b` (from cut), on the workers and the calling thread (part 0); `pre`,
-    // when given, runs on the calling thread once the workers have their parts, before its own
-    // `pre` runs on the calling thread while the workers take the parts (encode_chunk issues the previous
-    // chunk there).  A pool call made from inside `pre` or `f` on this thread (the pool is busy with this
-    // batch, and call_mu_ is held) runs its parts inline instead of waiting on itself.
+    // when given, runs on the calling thread once the workers have their parts, before its own (encode_chunk
+    // issues the previous chunk there).  A pool call made from inside `pre` or `f` on this thread (the pool
+    // is busy with this batch, and call_mu_ is held) runs its parts inline instead of waiting on itself.
     void parallel_parts(const std::vector<size_t>& b, const std::function<void(size_t, size_t, size_t)>& f,
                         const std::function<void()>& pre = nullptr) {
         spin_us_.store(CpuShare::get().sharers() > 1 ? 0 : spin_cfg_, std::memory_order_relaxed);

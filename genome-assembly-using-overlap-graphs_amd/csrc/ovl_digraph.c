@@ -32,6 +32,8 @@
 #include <Python.h>
 #include <stdint.h>
 #include <string.h>
+#include <pthread.h>
+#include <sched.h>
 
 static int take(PyObject* obj, Py_buffer* view, Py_ssize_t itemsize, const char* what) {
     if (PyObject_GetBuffer(obj, view, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) return -1;
@@ -622,9 +624,261 @@ done:
     return out;
 }
 
+/* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
+ *     -> (node, succ, pred, removed, n_removed)
+ * remove_cycles_from_graph on a graph that is still columns, with the replay and the dicts overlapped: the replay
+ * (replay_fn = the address of libovl's ovl_remove_cycles_stream) runs on a second thread over the CSR (off,
+ * heads, weights: OverlapEdges.csr()), and this thread builds each node's successor dict as soon as the replay
+ * publishes that node's out-edges as final (they can no longer be removed), with the edges' attribute dicts;
+ * then, the replay done, the predecessor dicts in global insertion order (pair, copy of a, copy of b:
+ * overlapGraphs.py:43-60) and the node-ordered top-level dicts.  The result is build_overlap's for the alive
+ * mask of the replay; removed holds the replay's removed CSR indices (int64) in removal order. */
+typedef int (*replay_stream_fn)(const int64_t*, const int32_t*, const int64_t*, int32_t, int64_t*, int64_t*,
+                                uint8_t*, int32_t*, int64_t*);
+typedef struct {
+    replay_stream_fn fn;
+    const int64_t* off;
+    const int32_t* heads;
+    const int64_t* w;
+    int32_t n;
+    int64_t* removed;
+    int64_t n_removed;
+    uint8_t* alive;
+    int32_t* final_nodes;
+    int64_t n_final;
+    int rc;
+    int finished;
+} ReplayJob;
+
+static void* replay_main(void* arg) {
+    ReplayJob* j = (ReplayJob*)arg;
+    j->rc = j->fn(j->off, j->heads, j->w, j->n, j->removed, &j->n_removed, j->alive, j->final_nodes, &j->n_final);
+    __atomic_store_n(&j->finished, 1, __ATOMIC_RELEASE);
+    return NULL;
+}
+
+static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
+    (void)self;
+    PyObject *names, *oc, *oa, *ob, *os, *oe, *ok, *shared, *ooff, *oh, *ow;
+    unsigned long long fn_addr;
+    if (!PyArg_ParseTuple(args, "O!OOOOOOOKOOO", &PyList_Type, &names, &oc, &oa, &ob, &os, &oe, &ok, &shared,
+                          &fn_addr, &ooff, &oh, &ow))
+        return NULL;
+    Cols C;
+    memset(&C, 0, sizeof(C));
+    Py_buffer bs, be, boff, bh, bw;
+    memset(&bs, 0, sizeof(bs));
+    memset(&be, 0, sizeof(be));
+    memset(&boff, 0, sizeof(boff));
+    memset(&bh, 0, sizeof(bh));
+    memset(&bw, 0, sizeof(bw));
+    Layout L;
+    memset(&L, 0, sizeof(L));
+    ReplayJob job;
+    memset(&job, 0, sizeof(job));
+    pthread_t th;
+    int started = 0;
+    PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
+    PyObject **rows = NULL, **dptr = NULL, **pin = NULL;
+    PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
+    int64_t* din = NULL;
+    int64_t* rread = NULL;
+    if (!ints) { PyErr_NoMemory(); goto done; }
+    if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end") ||
+        take(ooff, &boff, 8, "off") || take(oh, &bh, 4, "heads") || take(ow, &bw, 8, "weights"))
+        goto done;
+    if (bs.len != C.a.len || be.len != C.a.len) {
+        PyErr_SetString(PyExc_ValueError, "score and end must have one entry per pair");
+        goto done;
+    }
+    {
+        const int32_t* counts = (const int32_t*)C.c.buf;
+        const int32_t* a = (const int32_t*)C.a.buf;
+        const int32_t* b = (const int32_t*)C.b.buf;
+        const int32_t* sc = (const int32_t*)bs.buf;
+        const int32_t* en = (const int32_t*)be.buf;
+        const uint8_t* keep = C.has_k ? (const uint8_t*)C.k.buf : NULL;
+        if (layout(&L, counts, C.c.len / 4, a, b, C.a.len / 4, keep)) goto done;
+        const Py_ssize_t n_nodes = PyList_GET_SIZE(names);
+        if (n_nodes != L.N || boff.len / 8 != L.N + 1 || bh.len / 4 != L.E || bw.len / 8 != L.E ||
+            L.N >= ((Py_ssize_t)1 << 31)) {
+            PyErr_SetString(PyExc_ValueError, "names / CSR do not match the columns' graph");
+            goto done;
+        }
+        const int64_t E = L.E, N = L.N;
+        job.fn = (replay_stream_fn)(uintptr_t)fn_addr;
+        job.off = (const int64_t*)boff.buf;
+        job.heads = (const int32_t*)bh.buf;
+        job.w = (const int64_t*)bw.buf;
+        job.n = (int32_t)N;
+        job.removed = (int64_t*)PyMem_RawMalloc(sizeof(int64_t) * (size_t)(E ? E : 1));
+        job.alive = (uint8_t*)PyMem_RawMalloc((size_t)(E ? E : 1));
+        job.final_nodes = (int32_t*)PyMem_RawMalloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+        rows = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
+        pin = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
+        dptr = (PyObject**)PyMem_Calloc((size_t)(E ? E : 1), sizeof(PyObject*));
+        din = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
+        rread = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !din || !rread) {
+            PyErr_NoMemory();
+            goto done;
+        }
+        for (Py_ssize_t r = 0; r < L.R; ++r)
+            for (int64_t u = L.first[r]; u < L.first[r + 1]; ++u) rread[u] = r;
+        kw = PyUnicode_InternFromString("weight");
+        ke = PyUnicode_InternFromString("end_position");
+        if (!kw || !ke) goto done;
+        if (shared && shared != Py_None && PyDict_Check(shared) && PyDict_GET_SIZE(shared) == 2 &&
+            PyDict_Contains(shared, kw) == 1 && PyDict_Contains(shared, ke) == 1) {
+            tmpl = shared;
+            Py_INCREF(tmpl);
+        } else {
+            tmpl = PyDict_New();
+            if (!tmpl || PyDict_SetItem(tmpl, kw, Py_None) || PyDict_SetItem(tmpl, ke, Py_None)) goto done;
+        }
+        Py_ssize_t iw, ie;
+        attr_slots(tmpl, kw, ke, &iw, &ie);
+        if (pthread_create(&th, NULL, replay_main, &job) != 0) {
+            PyErr_SetString(PyExc_RuntimeError, "cannot start the replay thread");
+            goto done;
+        }
+        started = 1;
+        /* successors of each node as its out-edges become final (row order: kept pairs with a == its read in
+           list order, then the copies of b) */
+        int64_t k_done = 0;
+        for (;;) {
+            const int64_t avail = __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE);
+            if (avail > k_done) {
+                for (; k_done < avail; ++k_done) {
+                    const int64_t u = job.final_nodes[k_done];
+                    const Py_ssize_t r = rread[u];
+                    int64_t live = 0;
+                    for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                        const int64_t p = L.plist[g];
+                        const int64_t e0 = L.off[u] + L.pstart[p];
+                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb) live += job.alive[e0 + cb];
+                    }
+                    PyObject* sd = _PyDict_NewPresized(live);
+                    if (!sd) goto done;
+                    rows[u] = sd;
+                    for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                        const int64_t p = L.plist[g];
+                        const int64_t e0 = L.off[u] + L.pstart[p];
+                        const int64_t vb = L.first[b[p]];
+                        PyObject *wv = NULL, *ev = NULL;
+                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
+                            if (!job.alive[e0 + cb]) continue;
+                            if (!wv) {
+                                wv = int_of(ints, sc[p]);
+                                ev = int_of(ints, en[p]);
+                                if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
+                            }
+                            PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
+                            const int bad = !d || PyDict_SetItem(sd, PyList_GET_ITEM(names, vb + cb), d);
+                            Py_XDECREF(d);
+                            if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
+                            dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
+                            ++din[vb + cb];
+                        }
+                        Py_XDECREF(wv);
+                        Py_XDECREF(ev);
+                    }
+                }
+                continue;
+            }
+            if (__atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
+                if (__atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE) > k_done) continue;
+                break;
+            }
+            Py_BEGIN_ALLOW_THREADS
+            sched_yield();
+            Py_END_ALLOW_THREADS
+        }
+        pthread_join(th, NULL);
+        started = 0;
+        if (job.rc != 0 || k_done != N) {
+            PyErr_Format(PyExc_RuntimeError, "ovl_remove_cycles_stream failed (rc %d, %lld of %lld nodes final)",
+                         job.rc, (long long)k_done, (long long)N);
+            goto done;
+        }
+        /* predecessors: presized by the live in-degrees, edges in global insertion order */
+        for (Py_ssize_t v = 0; v < N; ++v) {
+            pin[v] = _PyDict_NewPresized(din[v]);
+            if (!pin[v]) goto done;
+        }
+        for (Py_ssize_t p = 0; p < L.P; ++p) {
+            if (keep && !keep[p]) continue;
+            for (int64_t u = L.first[a[p]]; u < L.first[a[p] + 1]; ++u) {
+                const int64_t e0 = L.off[u] + L.pstart[p];
+                PyObject* un = PyList_GET_ITEM(names, u);
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
+                    PyObject* d = dptr[e0 + cb];
+                    if (d && PyDict_SetItem(pin[L.first[b[p]] + cb], un, d)) goto done;
+                }
+            }
+        }
+        node = PyDict_New();
+        succ = PyDict_New();
+        pred = PyDict_New();
+        if (!node || !succ || !pred) goto done;
+        for (Py_ssize_t i = 0; i < N; ++i) {
+            PyObject* name = PyList_GET_ITEM(names, i);
+            PyObject* x = PyDict_New();
+            const int bad = !x || PyDict_SetItem(node, name, x) || PyDict_SetItem(succ, name, rows[i]) ||
+                            PyDict_SetItem(pred, name, pin[i]);
+            Py_XDECREF(x);
+            if (bad) goto done;
+        }
+        PyObject* rem = PyBytes_FromStringAndSize((const char*)job.removed, (Py_ssize_t)(8 * job.n_removed));
+        if (!rem) goto done;
+        out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
+    }
+done:
+    if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */
+        Py_BEGIN_ALLOW_THREADS
+        pthread_join(th, NULL);
+        Py_END_ALLOW_THREADS
+    }
+    layout_free(&L);
+    cols_release(&C);
+    if (bs.obj) PyBuffer_Release(&bs);
+    if (be.obj) PyBuffer_Release(&be);
+    if (boff.obj) PyBuffer_Release(&boff);
+    if (bh.obj) PyBuffer_Release(&bh);
+    if (bw.obj) PyBuffer_Release(&bw);
+    if (ints) {
+        for (int i = 0; i < kIntHi - kIntLo; ++i) Py_XDECREF(ints[i]);
+        PyMem_Free(ints);
+    }
+    if (rows) {
+        for (Py_ssize_t i = 0; i < L.N; ++i) Py_XDECREF(rows[i]);
+        PyMem_Free(rows);
+    }
+    if (pin) {
+        for (Py_ssize_t i = 0; i < L.N; ++i) Py_XDECREF(pin[i]);
+        PyMem_Free(pin);
+    }
+    PyMem_Free(dptr);
+    PyMem_Free(din);
+    PyMem_Free(rread);
+    PyMem_RawFree(job.removed);
+    PyMem_RawFree(job.alive);
+    PyMem_RawFree(job.final_nodes);
+    Py_XDECREF(node);
+    Py_XDECREF(succ);
+    Py_XDECREF(pred);
+    Py_XDECREF(tmpl);
+    Py_XDECREF(kw);
+    Py_XDECREF(ke);
+    return out;
+}
+
 static PyMethodDef methods[] = {
     {"overlap_csr", overlap_csr, METH_VARARGS,
      "overlap_csr(counts, a, b, score[, keep]) -> (off int64, heads int32, weights int64) bytearrays"},
+    {"build_overlap_stream", build_overlap_stream, METH_VARARGS,
+     "build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights) -> "
+     "(node, succ, pred, removed, n_removed)"},
     {"build_overlap", build_overlap, METH_VARARGS,
      "build_overlap(names, counts, a, b, score, end[, keep[, alive[, shared]]]) -> (node, succ, pred)"},
     {"build", build, METH_VARARGS, "build(names, u, v, weight, end) -> (node, succ, pred) dicts of a networkx DiGraph"},

@@ -36,6 +36,7 @@
 #include <stdint.h>
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <vector>
 
@@ -53,6 +54,21 @@ struct Event {
     int32_t first;
 };
 
+// Nodes whose out-edges are final, published as they become so (ovl_remove_cycles_stream): a node that is
+// settled (below) or explored (reached by a start whose walk found no cycle) can reach no cycle, so none of its
+// out-edges is ever removed.  nodes[0 .. *count) are published with a release store of *count; a consumer on
+// another thread reads *count with an acquire load, then those nodes' rows of the caller's alive array.
+struct Publish {
+    int32_t* nodes = nullptr;
+    int64_t* count = nullptr;
+    int64_t k = 0;
+    void push(int32_t v) {
+        if (!nodes) return;
+        nodes[k++] = v;
+        __atomic_store_n(count, k, __ATOMIC_RELEASE);
+    }
+};
+
 // The settled set, kept exact after every removal: settled = the nodes that cannot reach a cycle over the
 // live edges.  cnt[x] counts x's live out-edges into unsettled nodes, and x is settled iff cnt[x] == 0 (a node
 // whose every path ends in a sink), which propagation from the sinks computes exactly: a node left with
@@ -62,8 +78,8 @@ struct Event {
 // the whole run is O(E).  Settling sets done[v].
 class Sinks {
   public:
-    Sinks(const int64_t* off, const int32_t* head, int32_t n, uint8_t* done, bool on)
-        : head_(head), done_(done), on_(on) {
+    Sinks(const int64_t* off, const int32_t* head, int32_t n, uint8_t* done, bool on, Publish* pub)
+        : head_(head), done_(done), on_(on), pub_(pub) {
         if (!on_) return;
         const int64_t E = off[n];
         tail_.resize((size_t)E);
@@ -101,6 +117,7 @@ class Sinks {
             const int32_t v = q_.back();
             q_.pop_back();
             done_[v] = 1;
+            pub_->push(v);
             for (int64_t k = roff_[(size_t)v]; k < roff_[(size_t)v + 1]; ++k) {
                 const int32_t e = rin_[(size_t)k];
                 if (alive && !alive[e]) continue;
@@ -113,15 +130,17 @@ class Sinks {
     const int32_t* head_;
     uint8_t* done_;
     bool on_;
+    Publish* pub_;
     std::vector<int32_t> tail_, rin_, cnt_, q_;  // edge tails, in-edges by head, counts, settle queue
     std::vector<int64_t> roff_;                  // in-edge rows
 };
 
 }  // namespace
 
-extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const int64_t* off, const int32_t* head,
-                                                                      const int64_t* weight, int32_t n_nodes,
-                                                                      int64_t* removed, int64_t* n_removed) {
+namespace {
+
+int replay(const int64_t* off, const int32_t* head, const int64_t* weight, int32_t n_nodes, int64_t* removed,
+           int64_t* n_removed, uint8_t* alive_out, Publish& pub) {
     if (!n_removed || n_nodes < 0 || (n_nodes > 0 && (!off || !head || !weight))) return OVL_E_ARG;
     *n_removed = 0;
     if (n_nodes == 0) return OVL_OK;
@@ -146,7 +165,10 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     std::vector<Edge> ed((size_t)n_edges + 1);
     for (int64_t e = 0; e < n_edges; ++e) ed[(size_t)e] = {head[e], 0, weight[e]};
     ed[(size_t)n_edges] = {0, 0, 0};
-    std::vector<uint8_t> alive(n_edges, 1), done(n_nodes, 0);  // done = explored | settled (both only grow)
+    std::vector<uint8_t> alive_own(alive_out ? 0 : (size_t)n_edges, 1), done(n_nodes, 0);  // done = explored |
+                                                                                            // settled (only grow)
+    uint8_t* alive = alive_out ? alive_out : alive_own.data();
+    if (alive_out) memset(alive_out, 1, (size_t)n_edges);
     // per node, what a yield touches, in one record: the out-edge iterator position (CSR index) of a visited
     // node, the index of the path edge leaving it (valid while active), visited (= seen: both happen at the
     // yield that first reaches it) and on the active path
@@ -177,7 +199,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
 
     // OVL_CYCLES_SETTLE=0 (a test knob): no settled-node pruning, only the explored nodes are skipped
     const char* env_settle = getenv("OVL_CYCLES_SETTLE");
-    Sinks sinks(off, head, n_nodes, done.data(), !(env_settle && atoi(env_settle) == 0));
+    Sinks sinks(off, head, n_nodes, done.data(), !(env_settle && atoi(env_settle) == 0), &pub);
 
     Edge* E = ed.data();
     Node* N = nd.data();
@@ -197,7 +219,11 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
         for (;;) {
             if (stack.empty()) {
                 // no cycle reachable from s: everything seen is explored for the later starts
-                for (int32_t v : seen_list) done[v] = 1;
+                for (int32_t v : seen_list)
+                    if (!done[v]) {
+                        done[v] = 1;
+                        pub.push(v);
+                    }
                 N[root].active = 0;
                 break;
             }
@@ -267,7 +293,7 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
                 removed[nrem++] = dead;
                 alive[(size_t)dead] = 0;
                 E[dead].skip = 1;
-                sinks.removed(dead, alive.data());
+                sinks.removed(dead, alive);
                 // rewind the DFS to the moment `dead` was about to be yielded
                 const int64_t target = pp[kmin].ckpt;
                 while ((int64_t)log.size() > target) {
@@ -307,4 +333,27 @@ extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const in
     }
     *n_removed = nrem;
     return OVL_OK;
+}
+
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles(const int64_t* off, const int32_t* head,
+                                                                      const int64_t* weight, int32_t n_nodes,
+                                                                      int64_t* removed, int64_t* n_removed) {
+    Publish none;
+    return replay(off, head, weight, n_nodes, removed, n_removed, nullptr, none);
+}
+
+// The same replay, publishing its progress for a consumer on another thread: alive[e] (n_edges entries, set to
+// 1 here, 0 when edge e is removed) and the nodes whose out-edges are final, final_nodes[0 .. *n_final), each
+// node once, in the order they become final; *n_final reaches n_nodes before the call returns (Publish).
+extern "C" __attribute__((visibility("default"))) int ovl_remove_cycles_stream(
+    const int64_t* off, const int32_t* head, const int64_t* weight, int32_t n_nodes, int64_t* removed,
+    int64_t* n_removed, uint8_t* alive, int32_t* final_nodes, int64_t* n_final) {
+    if (!alive || !final_nodes || !n_final) return OVL_E_ARG;
+    __atomic_store_n(n_final, (int64_t)0, __ATOMIC_RELEASE);
+    Publish pub;
+    pub.nodes = final_nodes;
+    pub.count = n_final;
+    return replay(off, head, weight, n_nodes, removed, n_removed, alive, pub);
 }

@@ -67,6 +67,7 @@ SIGNATURES = {
     "ovl_local_align": (ctypes.c_int, [_P, _P, _i32, _P, _i32, _i32, _i32, _i64, _pi32, _pi32, _pi32, _pi32,
                                        _pi32, _P, _i64, _pi64]),
     "ovl_remove_cycles": (ctypes.c_int, [_P, _P, _P, _i32, _P, _pi64]),
+    "ovl_remove_cycles_stream": (ctypes.c_int, [_P, _P, _P, _i32, _P, _pi64, _P, _P, _P]),
 }
 
 

@@ -233,6 +233,15 @@ int ovl_local_align(ovl_ctx* ctx, const uint8_t* query, int32_t n, const uint8_t
  * cycle (edge DFS from the first unexplored node in node order), its first minimum-weight edge. */
 int ovl_remove_cycles(const int64_t* off, const int32_t* head, const int64_t* weight, int32_t n_nodes,
                       int64_t* removed, int64_t* n_removed);
+/* ovl_remove_cycles publishing its progress to a consumer on another thread (the C builder of the surviving
+ * edges' dicts, ovlgraph/_digraph build_overlap_stream, builds each node's successors as soon as they are
+ * final): alive[e] (off[n_nodes] entries) is set to 1, then 0 when edge e is removed; final_nodes[0 .. *n_final)
+ * lists each node once, when its out-edges are final (it can reach no cycle: settled, or explored by a start
+ * whose walk found none); *n_final is stored with release order (read it with an acquire load) and reaches
+ * n_nodes before a successful call returns. */
+int ovl_remove_cycles_stream(const int64_t* off, const int32_t* head, const int64_t* weight, int32_t n_nodes,
+                             int64_t* removed, int64_t* n_removed, uint8_t* alive, int32_t* final_nodes,
+                             int64_t* n_final);
 
 #ifdef __cplusplus
 }

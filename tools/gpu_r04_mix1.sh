@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/${1:-r04d}
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dp_lane.py tests/test_gpu_pipeline.py tests/test_gpu_compact_pairs.py tests/test_gpu_c_abi.py -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dp_lane.py tests/test_gpu_pipeline.py tests/test_gpu_compact_pairs.py tests/test_gpu_c_abi.py tests/test_gpu_reads_resident.py tests/test_gpu_bench_dist.py tests/test_gpu_assembly.py -m gpu -x -q --timeout 300 --timeout-method thread \
   > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -40 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 bash tools/gpu_r04_shard_ab.sh ${1:-r04d} || exit 1

@@ -71,6 +71,21 @@ def main():
             sig = h
             del G
             gc.collect()
+    # the whole lazy-graph removal (what end_to_end times): replay then survivors' dicts, or both overlapped
+    og._digraph_mod = None  # (the tree's own build)
+    res["remove_cycles_s"] = {"serial": [], "stream": []}
+    for _ in range(rounds):
+        for mode in ("serial", "stream"):
+            og._STREAM_OFF = mode == "serial"
+            G = edges.to_digraph()
+            t0 = time.perf_counter()
+            og.remove_cycles_from_graph(G)
+            res["remove_cycles_s"][mode].append(time.perf_counter() - t0)
+            assert G.number_of_edges() == heads.shape[0] - ref.shape[0]
+            del G
+            gc.collect()
+    res["remove_cycles_s"] = {m: {"median": round(float(np.median(v)), 4), "all": [round(x, 4) for x in v]}
+                              for m, v in res["remove_cycles_s"].items()}
     res["removed"] = int(ref.shape[0])
     for k in ("replay_s", "dicts_s"):
         res[k] = {n: {"median": round(float(np.median(v)), 4), "min": round(float(np.min(v)), 4), "all": [round(x, 4) for x in v]}
