@@ -138,3 +138,25 @@ def test_csr_from_columns_matches_graph_csr():
         np.testing.assert_array_equal(off, ref_off)
         np.testing.assert_array_equal(heads, ref_heads)
         np.testing.assert_array_equal(w, ref_w)
+
+
+@pytest.mark.parametrize("ms", [None, 3])
+def test_streamed_removal_equals_serial(monkeypatch, ms):
+    """Cycle removal on a lazy graph with the replay and the survivors' dicts overlapped (ovl_remove_cycles_stream
+    publishing final nodes to build_overlap_stream) leaves the graph the replay-then-dicts path leaves, every
+    view and shared attribute dict included; so does a graph with no cycle and one with no edge."""
+    cases = [_case(s, n_reads=500) for s in (11, 12)] + [_case(13, n_reads=60, alphabet="A")]
+    for d, c, a, b, sc, en in cases:
+        E = og.OverlapEdges(d, c, a, b, sc, en, min_score=ms)
+        out = {}
+        for off in (False, True):
+            monkeypatch.setattr(og, "_STREAM_OFF", off)
+            t = {}
+            out[off] = (og.remove_cycles_from_graph(E.to_digraph(), timing=t), t)
+        (Ls, ts), (Lr, tr) = out[False], out[True]
+        assert ts["overlapped"] and not tr["overlapped"] and ts["removed"] == tr["removed"]
+        _same_views(Ls, Lr)
+        assert nx.is_directed_acyclic_graph(Ls)
+    z = np.zeros(0, np.int32)
+    L = og.remove_cycles_from_graph(og.OverlapEdges(["AC", "CA"], [1, 2], z, z, z, z).to_digraph())
+    assert list(L.nodes()) == ["AC_0", "CA_0", "CA_1"] and L.number_of_edges() == 0
