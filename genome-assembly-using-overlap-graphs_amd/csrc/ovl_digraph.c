@@ -629,10 +629,11 @@ done:
  * remove_cycles_from_graph on a graph that is still columns, with the replay and the dicts overlapped: the replay
  * (replay_fn = the address of libovl's ovl_remove_cycles_stream) runs on a second thread over the CSR (off,
  * heads, weights: OverlapEdges.csr()), and this thread builds each node's successor dict as soon as the replay
- * publishes that node's out-edges as final (they can no longer be removed), with the edges' attribute dicts;
- * then, the replay done, the predecessor dicts in global insertion order (pair, copy of a, copy of b:
- * overlapGraphs.py:43-60) and the node-ordered top-level dicts.  The result is build_overlap's for the alive
- * mask of the replay; removed holds the replay's removed CSR indices (int64) in removal order. */
+ * publishes that node's out-edges as final (they can no longer be removed), with the edges' attribute dicts, and
+ * each node's predecessor dict as soon as every tail of its in-edges is final: its in-edges in global insertion
+ * order (pairs with b = its read in list order, then the copies of a: overlapGraphs.py:43-60); then the
+ * node-ordered top-level dicts.  The result is build_overlap's for the alive mask of the replay; removed holds
+ * the replay's removed CSR indices (int64) in removal order. */
 typedef int (*replay_stream_fn)(const int64_t*, const int32_t*, const int64_t*, int32_t, int64_t*, int64_t*,
                                 uint8_t*, int32_t*, int64_t*);
 typedef struct {
@@ -683,6 +684,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t* din = NULL;
     int64_t* rread = NULL;
+    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL;
     if (!ints) { PyErr_NoMemory(); goto done; }
     if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end") ||
         take(ooff, &boff, 8, "off") || take(oh, &bh, 4, "heads") || take(ow, &bw, 8, "weights"))
@@ -719,12 +721,34 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         dptr = (PyObject**)PyMem_Calloc((size_t)(E ? E : 1), sizeof(PyObject*));
         din = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
         rread = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
-        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !din || !rread) {
+        /* in-edges in insertion order: the kept pairs grouped by b (list order within a group) */
+        bgoff = (int64_t*)PyMem_Calloc((size_t)L.R + 1, sizeof(int64_t));
+        blist = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(L.P ? L.P : 1));
+        pending = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
+        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !din || !rread || !bgoff ||
+            !blist || !pending) {
             PyErr_NoMemory();
             goto done;
         }
         for (Py_ssize_t r = 0; r < L.R; ++r)
             for (int64_t u = L.first[r]; u < L.first[r + 1]; ++u) rread[u] = r;
+        for (Py_ssize_t p = 0; p < L.P; ++p)
+            if (!keep || keep[p]) ++bgoff[b[p] + 1];
+        for (Py_ssize_t r = 0; r < L.R; ++r) bgoff[r + 1] += bgoff[r];
+        {
+            int64_t* fill = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(L.R ? L.R : 1));
+            if (!fill) { PyErr_NoMemory(); goto done; }
+            memcpy(fill, bgoff, sizeof(int64_t) * (size_t)L.R);
+            for (Py_ssize_t p = 0; p < L.P; ++p)
+                if (!keep || keep[p]) blist[fill[b[p]]++] = p;
+            PyMem_Free(fill);
+        }
+        /* a node's in-edges whose tail is not final yet (every copy of one read has the same in-edges) */
+        for (Py_ssize_t r = 0; r < L.R; ++r) {
+            int64_t k = 0;
+            for (int64_t g = bgoff[r]; g < bgoff[r + 1]; ++g) k += L.first[a[blist[g]] + 1] - L.first[a[blist[g]]];
+            for (int64_t v = L.first[r]; v < L.first[r + 1]; ++v) pending[v] = k;
+        }
         kw = PyUnicode_InternFromString("weight");
         ke = PyUnicode_InternFromString("end_position");
         if (!kw || !ke) goto done;
@@ -744,8 +768,13 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         }
         started = 1;
         /* successors of each node as its out-edges become final (row order: kept pairs with a == its read in
-           list order, then the copies of b) */
-        int64_t k_done = 0;
+           list order, then the copies of b); predecessors of each node once every tail of its in-edges is */
+        int64_t k_done = 0, n_pred = 0;
+        int64_t* ready = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        int64_t n_ready = 0;
+        if (!ready) { PyErr_NoMemory(); goto done; }
+        for (int64_t v = 0; v < N; ++v)
+            if (pending[v] == 0) ready[n_ready++] = v;
         for (;;) {
             const int64_t avail = __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE);
             if (avail > k_done) {
@@ -782,6 +811,26 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                         }
                         Py_XDECREF(wv);
                         Py_XDECREF(ev);
+                        /* u's edge to every copy of b is final now */
+                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
+                            if (--pending[vb + cb] == 0) ready[n_ready++] = vb + cb;
+                    }
+                    /* predecessors whose in-edges are all final */
+                    while (n_ready > 0) {
+                        const int64_t v = ready[--n_ready];
+                        const Py_ssize_t rv = rread[v];
+                        const int64_t cv = v - L.first[rv];
+                        PyObject* pd = _PyDict_NewPresized(din[v]);
+                        if (!pd) { PyMem_Free(ready); goto done; }
+                        pin[v] = pd;
+                        for (int64_t g = bgoff[rv]; g < bgoff[rv + 1]; ++g) {
+                            const int64_t q = blist[g];
+                            for (int64_t t = L.first[a[q]]; t < L.first[a[q] + 1]; ++t) {
+                                PyObject* d = dptr[L.off[t] + L.pstart[q] + cv];
+                                if (d && PyDict_SetItem(pd, PyList_GET_ITEM(names, t), d)) { PyMem_Free(ready); goto done; }
+                            }
+                        }
+                        ++n_pred;
                     }
                 }
                 continue;
@@ -794,28 +843,13 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             sched_yield();
             Py_END_ALLOW_THREADS
         }
+        PyMem_Free(ready);
         pthread_join(th, NULL);
         started = 0;
-        if (job.rc != 0 || k_done != N) {
-            PyErr_Format(PyExc_RuntimeError, "ovl_remove_cycles_stream failed (rc %d, %lld of %lld nodes final)",
-                         job.rc, (long long)k_done, (long long)N);
+        if (job.rc != 0 || k_done != N || n_pred != N) {
+            PyErr_Format(PyExc_RuntimeError, "ovl_remove_cycles_stream failed (rc %d, %lld of %lld nodes final, "
+                         "%lld predecessor dicts)", job.rc, (long long)k_done, (long long)N, (long long)n_pred);
             goto done;
-        }
-        /* predecessors: presized by the live in-degrees, edges in global insertion order */
-        for (Py_ssize_t v = 0; v < N; ++v) {
-            pin[v] = _PyDict_NewPresized(din[v]);
-            if (!pin[v]) goto done;
-        }
-        for (Py_ssize_t p = 0; p < L.P; ++p) {
-            if (keep && !keep[p]) continue;
-            for (int64_t u = L.first[a[p]]; u < L.first[a[p] + 1]; ++u) {
-                const int64_t e0 = L.off[u] + L.pstart[p];
-                PyObject* un = PyList_GET_ITEM(names, u);
-                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                    PyObject* d = dptr[e0 + cb];
-                    if (d && PyDict_SetItem(pin[L.first[b[p]] + cb], un, d)) goto done;
-                }
-            }
         }
         node = PyDict_New();
         succ = PyDict_New();
@@ -861,6 +895,9 @@ done:
     PyMem_Free(dptr);
     PyMem_Free(din);
     PyMem_Free(rread);
+    PyMem_Free(bgoff);
+    PyMem_Free(blist);
+    PyMem_Free(pending);
     PyMem_RawFree(job.removed);
     PyMem_RawFree(job.alive);
     PyMem_RawFree(job.final_nodes);
