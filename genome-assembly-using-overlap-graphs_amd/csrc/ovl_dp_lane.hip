@@ -658,7 +658,9 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
             t0n = *reinterpret_cast<const uint2*>(tp + 2 * q0);
             t1n = *reinterpret_cast<const uint2*>(tp + 2 * q1);
         };
-        uint32_t x_prev = 0, tn_prev = 0;  // the row symbol / entering code of the previous step's iteration
+        // the row symbol / entering code of the previous step's iteration; before step 0 that is iteration -1,
+        // a virtual row (its symbol unused) whose entering code lane 1 appends in step 0
+        uint32_t x_prev = 0, tn_prev = tcode(ub - 1);
         // step t: lane 0 runs iteration t, lane 1 iteration t - 1 (x_c / tn_c: iteration t's)
         auto step = [&](int32_t t, uint32_t x_c, uint32_t tn_c, auto masked_tag) {
             constexpr bool MASKED = decltype(masked_tag)::value;
