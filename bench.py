@@ -450,10 +450,23 @@ def end_to_end(w: Workload, seed: int = 0):
     L = edges.to_digraph()  # what construct_overlap_graph_nx_k returns
     t2 = time.perf_counter()
     rc_l = {}
-    og.remove_cycles_from_graph(L, timing=rc_l)
+    og.remove_cycles_from_graph(L, timing=rc_l)  # (replay and survivors' dicts overlapped)
     t3 = time.perf_counter()
     n_kept = L.number_of_edges()
     del L
+    # the same with the replay, then the dicts (OVL_CYCLES_STREAM=0), for comparison
+    saved = og._STREAM_OFF
+    og._STREAM_OFF = True
+    try:
+        L = edges.to_digraph()
+        rc_s = {}
+        ts0 = time.perf_counter()
+        og.remove_cycles_from_graph(L, timing=rc_s)
+        ts1 = time.perf_counter()
+        assert L.number_of_edges() == n_kept
+        del L
+    finally:
+        og._STREAM_OFF = saved
     t4 = time.perf_counter()
     G = edges.to_digraph(lazy=False)
     t5 = time.perf_counter()
@@ -475,9 +488,13 @@ def end_to_end(w: Workload, seed: int = 0):
             "construct_s": round(t2 - t0, 4),
             "remove_cycles_s": round(t3 - t2, 4),
             "remove_cycles_stages_s": {k: round(rc_l[k], 4) for k in ("csr", "replay", "remove")},
+            "remove_cycles_overlapped": bool(rc_l.get("overlapped")),
             "construct_plus_remove_cycles_s": round(t3 - t0, 4),
+            "remove_cycles_serial_s": round(ts1 - ts0, 4),
+            "remove_cycles_serial_stages_s": {k: round(rc_s[k], 4) for k in ("csr", "replay", "remove")},
             "what": "construct_s: overlap_edges_k + the lazy DiGraph (dicts built on first use); remove_cycles_s: "
-                    "on that graph, CSR from the columns, replay, the surviving edges' dicts built (stage 'remove')",
+                    "on that graph, CSR from the columns, then the replay with the surviving edges' dicts built "
+                    "while it runs (stage 'replay' holds both; remove_cycles_serial_s: replay, then the dicts)",
             "eager": {"digraph_direct_s": round(t5 - t4, 4), "digraph_networkx_s": round(t6 - t5, 4),
                       "remove_cycles_s": round(t8 - t7, 4),
                       "remove_cycles_stages_s": {k: round(rc_e[k], 4) for k in ("csr", "replay", "remove")}}}
