@@ -6,12 +6,12 @@
 // host-array calls, pinned staging rings and the device error flag.  Host-array
 // scoring calls shard the pair list over the devices (contiguous ranges balanced
 // by sum n*m) and run a chunked pipeline per device (run_pipeline).
-// In direct mode (the default) the kernels read host pair lists and store results
-// through host mappings: packed (2 bytes per pair, Call::pack) into staging slots
-// that the host pool expands into the caller's int32 arrays while the next chunk
-// scores, with a last share of the pairs stored as int32 straight into pinned
-// arrays; otherwise as int32 into the caller's pinned arrays or staging slots.
-// Copy-engine mode (OVL_PIPE_DIRECT=0) overlaps H2D, kernel and D2H instead.
+// The kernels read host pair lists and store results through host mappings:
+// packed (2 bytes per pair, Call::pack) into staging slots that the host pool
+// expands into the caller's int32 arrays while the next chunk scores, with a
+// last share of the pairs stored as int32 straight into pinned arrays; otherwise
+// as int32 into the caller's pinned arrays or staging slots.  Only the compact
+// in-place pair list (encode_chunk) crosses by copy-engine transfer.
 // Kernel choice per call (ovl_plan): the ungapped popcount kernel whenever gaps
 // provably cannot win and the read store has a bit-plane layout, else a DP kernel.
 // Never falls back to the CPU.
@@ -1111,8 +1111,8 @@ bool host_pinned(const void* p, size_t bytes) {
 // Pairs per pipeline chunk.  Measured on MI355X (tools/pipe_ab.py, profiles/r02_pipe_ab_*.json): every
 // chunk's D2H copy costs ~0.1 ms of fixed overhead, which is more than the kernel time a chunk hides, so
 // copies of pinned arrays run as one chunk; only pageable arrays, which go through pinned staging slots,
-// are cut into chunks (the slot size): 4 M pairs with copy-engine transfers, 512 K pairs when the kernels
-// read and store the staging slots themselves (the host copy of chunk k+1 overlaps the kernel of chunk k).
+// are cut into chunks (the slot size): 512 K pairs, the kernels reading and storing the staging slots
+// themselves (the host copy of chunk k+1 overlaps the kernel of chunk k).
 // Direct kernel stores into pinned arrays need no chunks at all.  Packed results (pack_ok) are expanded
 // on the host chunk by chunk while the next chunk is scored: 1 M pairs (tools/host_paths_ab.py at the
 // target point: 128 K 0.53 ms, 256 K 0.38, 512 K 0.30, 1 M 0.25, one chunk 0.29).
