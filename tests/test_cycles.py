@@ -72,6 +72,19 @@ def test_native_matches_oracle_random(oracle_mod, seed):
         assert _same(oracle_mod.remove_cycles(G.copy()), remove_cycles_from_graph(G.copy()))
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_native_matches_oracle_wide_weights(oracle_mod, seed):
+    """Weights beyond int32 (the replay's 16-byte edge records; int32 weights take the 12-byte ones): ties
+    and order among weights that differ only above bit 31 or only below it."""
+    from ovlgraph.overlapGraphs import remove_cycles_from_graph
+    rng = random.Random(100 + seed)
+    for _ in range(30):
+        G = _random_graph(rng, rng.randint(2, 40), rng.choice([0.05, 0.1, 0.3]), whi=3)
+        for u, v, d in G.edges(data=True):
+            d["weight"] = rng.choice([-1, 0, 1, 2]) * (1 << 33) + d["weight"]
+        assert _same(oracle_mod.remove_cycles(G.copy()), remove_cycles_from_graph(G.copy()))
+
+
 def _layered_graph(rng, blobs):
     """Strongly connected blobs joined by DAG edges, acyclic tails in and out of them, node order
     shuffled: starts that reach only acyclic territory, DFS excursions into nodes that can no longer
