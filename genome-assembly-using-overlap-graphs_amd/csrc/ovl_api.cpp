@@ -92,6 +92,8 @@ struct Knobs {
                                   // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
                                   // instead of uniform_kernel reading b16 + tile deltas in place (tests)
+    int32_t pack_ramp = 1;        // OVL_PACK_RAMP=0 (A/B, round 4): equal packed chunks instead of a ramp
+    int64_t expand_part = 1 << 14;// OVL_EXPAND_PART (A/B, round 4): pairs per host-pool part of an expansion
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -103,11 +105,14 @@ constexpr int64_t kLaneMinPairs = 65536;
 // uniform_kernel grid cap, blocks of 256 per CU: ~1 tile per wavefront at the target point, the dispatcher
 // balances the tail (measured -2.3 % against 8 per CU; 16 / 32 / 64: 69.2 / 68.6 / 68.4 us)
 constexpr int64_t kBlocksPerCu = 32;
-// band knob: two lanes per pair (band_lane2_kernel) from this half-width (one lane's 2W+1 band cells no longer fit
-// the registers of several waves per SIMD)
-constexpr int32_t kBandLane2Min = 40;
+// band knob: two lanes per pair (band_lane2_kernel) from this half-width.  Measured at cfg5 (tools/band_ab.py,
+// profiles/r04_band_lane_ab.json, ms one lane / two lanes): 40: 6.07 / 6.99, 48: 7.13 / 8.04, 56: 8.29 / 9.09,
+// 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD
+constexpr int32_t kBandLane2Min = 64;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
+// packed calls: the first chunk of a ramp (setup_job), then x 1.5 per chunk up to the chunk size
+constexpr int64_t kRampFirst = int64_t(3) << 16;
 
 }  // namespace
 
@@ -682,6 +687,8 @@ Knobs read_knobs() {
         k.pack_adapt = 0;  // a fixed share
     }
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PACK_RAMP")) k.pack_ramp = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_EXPAND_PART")) k.expand_part = std::max(64LL, atoll(e));
     if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
@@ -967,12 +974,12 @@ void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(
 // over the host pool.  The vector width is the widest this CPU runs unless OVL_EXPAND_ISA names one
 // (scalar, sse2, avx2, avx512; A/B knob).
 void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
-                 bool nt, size_t n) {
+                 bool nt, size_t n, size_t min_part) {
     static const ovl_expand::Fn f = [] {
         const ovl_expand::Fn g = ovl_expand::pick(getenv("OVL_EXPAND_ISA"));
         return g ? g : ovl_expand::pick(nullptr);
     }();
-    CopyPool::get().parallel(n, size_t(1) << 16,
+    CopyPool::get().parallel(n, min_part,
                              [=](size_t lo, size_t hi) { f(s, e, pk, esc, match, mismatch, nt, lo, hi); });
 }
 
@@ -1178,7 +1185,8 @@ int setup_job(const Call& C, Job& J) {
     HIPCHK(d, hipSetDevice(d->device));
     const bool need_in = C.h_a && !C.in_pinned && !C.compact, need_out = !C.out_pinned || C.pack;
     J.chunk = pick_chunk(d, n, need_in || need_out, C.pack);
-    // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
+    // packed calls: the packed share in chunks of <= J.chunk (a ramp, or equal), then (pinned arrays) the direct
+    // share
     int64_t packed = 0;
     if (C.pack) {
         double& share = C.compact ? d->pack_pct_h : d->pack_pct;
@@ -1186,10 +1194,24 @@ int setup_job(const Call& C, Job& J) {
         const int64_t pct = d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct;
         packed = C.out_pinned ? (n - n * pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
-        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
-        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
-        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
-        if (packed > 0) J.cb.push_back(packed);
+        if (d->k.pack_ramp && d->k.pipe_chunk == 0 && packed >= 2 * kRampFirst && J.chunk >= kRampFirst) {
+            // a ramp: the host starts expanding after a short first kernel, and each next chunk's kernel
+            // (~48 us per M pairs at the target point) ends before the host has expanded the one before it
+            // (~68 us per M pairs), so the host never waits after the first
+            int64_t c = kRampFirst;
+            for (int64_t o = 0; o < packed;) {
+                int64_t sz = std::min(c, packed - o);
+                if (packed - o - sz < c / 2) sz = packed - o;  // no short tail chunk
+                o += sz;
+                J.cb.push_back(o);
+                c = std::min(J.chunk, ((c * 3 / 2) + 63) & ~int64_t(63));
+            }
+        } else {
+            const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
+            const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+            for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
+            if (packed > 0) J.cb.push_back(packed);
+        }
         J.n_packed = (int64_t)J.cb.size() - 1;
     }
     for (int64_t o = packed; o < n;) {
@@ -1502,7 +1524,7 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
     if (C.pack) {
         host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
-                    ss + d->st_cap, C.match, C.mismatch, true, (size_t)n);
+                    ss + d->st_cap, C.match, C.mismatch, true, (size_t)n, (size_t)d->k.expand_part);
         return OVL_OK;
     }
     host_copy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);

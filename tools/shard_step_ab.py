@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
 import numpy as np  # noqa: E402
 
-KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
+KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN", "OVL_PACK_RAMP", "OVL_EXPAND_PART")
 SETTINGS = (("default", {}),)
 if os.environ.get("SHARD_AB_SETTINGS"):
     SETTINGS = tuple((nm, dict(kv.split(":") for kv in spec.split(",") if kv))
@@ -30,30 +30,34 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     cfg = os.environ.get("SHARD_AB_CONFIG", "target")
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
+    # one engine per (setting, N): the adaptive direct share (pack_share) follows the call size it sees, as in a
+    # rank that scores the same shard every step
     engines = {}
     for name, env in SETTINGS:
-        for k in KNOBS:
-            os.environ.pop(k, None)
-        os.environ.update(env)
-        eng = OverlapEngine(0)
-        for k in KNOBS:
-            os.environ.pop(k, None)
-        eng.set_reads(reads)
-        n = eng.enumerate_candidates(CONFIGS[cfg]["k"])
-        engines[name] = eng
-    cuts = {N: engines[SETTINGS[0][0]].candidate_shards(N) for N in NS}
+        for N in NS:
+            for k in KNOBS:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            eng = OverlapEngine(0)
+            for k in KNOBS:
+                os.environ.pop(k, None)
+            eng.set_reads(reads)
+            n = eng.enumerate_candidates(CONFIGS[cfg]["k"])
+            engines[(name, N)] = eng
+    first = engines[(SETTINGS[0][0], NS[0])]
+    cuts = {N: first.candidate_shards(N) for N in NS}
     out = (pinned_empty(n), pinned_empty(n))
-    ref = engines[SETTINGS[0][0]].score_candidates()
+    ref = first.score_candidates()
     ref = (np.array(ref[0]), np.array(ref[1]))
     times = {(s, N): [] for s, _ in SETTINGS for N in NS}
     plan = {}
-    for _ in range(rounds):
+    for r in range(rounds):
         for name, _ in SETTINGS:
-            eng = engines[name]
             for N in NS:
+                eng = engines[(name, N)]
                 lo, hi = cuts[N][0], cuts[N][1]
                 o = (out[0][lo:hi], out[1][lo:hi])
-                for _ in range(3):
+                for _ in range(60 if r == 0 else 3):
                     eng.score_candidates_range(lo, hi, out=o)
                 t0 = time.perf_counter()
                 for _ in range(reps):
@@ -62,7 +66,7 @@ def main():
                 assert np.array_equal(o[0], ref[0][lo:hi]) and np.array_equal(o[1], ref[1][lo:hi]), (name, N)
                 eng.set_timing(True)
                 eng.score_candidates_range(lo, hi, out=o)
-                plan[(name, N)] = [(r["sink"], r["pairs"], round(r["ms"], 4)) for r in eng.last_launches()]
+                plan[(name, N)] = [(r_["sink"], r_["pairs"], round(r_["ms"], 4)) for r_ in eng.last_launches()]
                 eng.set_timing(False)
     res = {"config": cfg, "pairs": int(n), "rounds": rounds, "reps": reps, "results": []}
     for (name, N), v in times.items():
