@@ -34,6 +34,9 @@
 #include <string.h>
 #include <pthread.h>
 #include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <time.h>
 
 static int take(PyObject* obj, Py_buffer* view, Py_ssize_t itemsize, const char* what) {
     if (PyObject_GetBuffer(obj, view, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) return -1;
@@ -634,6 +637,15 @@ done:
  * order (pairs with b = its read in list order, then the copies of a: overlapGraphs.py:43-60); then the
  * node-ordered top-level dicts.  The result is build_overlap's for the alive mask of the replay; removed holds
  * the replay's removed CSR indices (int64) in removal order. */
+/* OVL_TRACE_STREAM=1 (diagnostics): one stderr line per build_overlap_stream with the millisecond offsets of its
+   phases (s setup done, r replay finished as seen here, with the share of nodes final by then, b dicts built,
+   t top-level dicts) */
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
 typedef int (*replay_stream_fn)(const int64_t*, const int32_t*, const int64_t*, int32_t, int64_t*, int64_t*,
                                 uint8_t*, int32_t*, int64_t*);
 typedef struct {
@@ -679,12 +691,18 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     memset(&job, 0, sizeof(job));
     pthread_t th;
     int started = 0;
+    const char* tr_env = getenv("OVL_TRACE_STREAM");
+    const int trace = tr_env && atoi(tr_env) != 0;
+    const double t0 = trace ? now_ms() : 0.0;
+    double t_setup = 0.0, t_replay = -1.0, t_built = 0.0;
+    int64_t k_at_replay = 0;
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
     PyObject **rows = NULL, **dptr = NULL, **pin = NULL;
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t* din = NULL;
     int64_t* rread = NULL;
-    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL;
+    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL;
+    uint8_t* spec = NULL;
     if (!ints) { PyErr_NoMemory(); goto done; }
     if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end") ||
         take(ooff, &boff, 8, "off") || take(oh, &bh, 4, "heads") || take(ow, &bw, 8, "weights"))
@@ -767,85 +785,139 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             goto done;
         }
         started = 1;
+        if (trace) t_setup = now_ms() - t0;
         /* successors of each node as its out-edges become final (row order: kept pairs with a == its read in
-           list order, then the copies of b); predecessors of each node once every tail of its in-edges is */
-        int64_t k_done = 0, n_pred = 0;
-        int64_t* ready = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+           list order, then the copies of b); predecessors of each node once every tail of its in-edges is.
+           Speculation: while the replay runs and no node is newly final, this thread builds the whole successor
+           row (removed edges included) of the next node in node order that is not final yet; when that node
+           becomes final, its removed edges are deleted from the row (PyDict_DelItem keeps the order of the
+           others, as DiGraph.remove_edge does).  A node's row is final at the end of the replay for ~60 % of the
+           target point's nodes, which without speculation all wait for it. */
+        int64_t k_done = 0, n_pred = 0, spec_next = 0, n_spec = 0, n_pruned = 0;
+        /* OVL_STREAM_SPEC (tests): 0 no speculation, 2 every node's row speculatively first (each one then
+           pruned), else (1) in idle time */
+        const char* spec_env = getenv("OVL_STREAM_SPEC");
+        const int spec_mode = spec_env ? atoi(spec_env) : 1;
+        ready = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        spec = (uint8_t*)PyMem_Calloc((size_t)(N ? N : 1), 1);
         int64_t n_ready = 0;
-        if (!ready) { PyErr_NoMemory(); goto done; }
+        if (!ready || !spec) { PyErr_NoMemory(); goto done; }
         for (int64_t v = 0; v < N; ++v)
             if (pending[v] == 0) ready[n_ready++] = v;
         for (;;) {
             const int64_t avail = __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE);
-            if (avail > k_done) {
-                for (; k_done < avail; ++k_done) {
-                    const int64_t u = job.final_nodes[k_done];
-                    const Py_ssize_t r = rread[u];
-                    int64_t live = 0;
-                    for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                        const int64_t p = L.plist[g];
-                        const int64_t e0 = L.off[u] + L.pstart[p];
-                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb) live += job.alive[e0 + cb];
-                    }
-                    PyObject* sd = _PyDict_NewPresized(live);
-                    if (!sd) goto done;
-                    rows[u] = sd;
-                    for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                        const int64_t p = L.plist[g];
-                        const int64_t e0 = L.off[u] + L.pstart[p];
-                        const int64_t vb = L.first[b[p]];
-                        PyObject *wv = NULL, *ev = NULL;
-                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                            if (!job.alive[e0 + cb]) continue;
-                            if (!wv) {
-                                wv = int_of(ints, sc[p]);
-                                ev = int_of(ints, en[p]);
-                                if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
-                            }
-                            PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
-                            const int bad = !d || PyDict_SetItem(sd, PyList_GET_ITEM(names, vb + cb), d);
-                            Py_XDECREF(d);
-                            if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
-                            dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
-                            ++din[vb + cb];
-                        }
-                        Py_XDECREF(wv);
-                        Py_XDECREF(ev);
-                        /* u's edge to every copy of b is final now */
-                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
-                            if (--pending[vb + cb] == 0) ready[n_ready++] = vb + cb;
-                    }
-                    /* predecessors whose in-edges are all final */
-                    while (n_ready > 0) {
-                        const int64_t v = ready[--n_ready];
-                        const Py_ssize_t rv = rread[v];
-                        const int64_t cv = v - L.first[rv];
-                        PyObject* pd = _PyDict_NewPresized(din[v]);
-                        if (!pd) { PyMem_Free(ready); goto done; }
-                        pin[v] = pd;
-                        for (int64_t g = bgoff[rv]; g < bgoff[rv + 1]; ++g) {
-                            const int64_t q = blist[g];
-                            for (int64_t t = L.first[a[q]]; t < L.first[a[q] + 1]; ++t) {
-                                PyObject* d = dptr[L.off[t] + L.pstart[q] + cv];
-                                if (d && PyDict_SetItem(pd, PyList_GET_ITEM(names, t), d)) { PyMem_Free(ready); goto done; }
-                            }
-                        }
-                        ++n_pred;
-                    }
+            int64_t u = -1;
+            int speculative = 0;
+            while (spec_mode == 2 && spec_next < N && rows[spec_next]) ++spec_next;
+            if (spec_mode == 2 && spec_next < N) {
+                u = spec_next++;
+                speculative = 1;
+            } else if (avail > k_done) {
+                u = job.final_nodes[k_done++];
+            } else if (__atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
+                if (trace && t_replay < 0.0) {
+                    t_replay = now_ms() - t0;
+                    k_at_replay = k_done;
                 }
-                continue;
-            }
-            if (__atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
                 if (__atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE) > k_done) continue;
                 break;
+            } else {
+                while (spec_next < N && rows[spec_next]) ++spec_next;
+                if (spec_mode == 0 || spec_next >= N) {
+                    Py_BEGIN_ALLOW_THREADS
+                    sched_yield();
+                    Py_END_ALLOW_THREADS
+                    continue;
+                }
+                u = spec_next++;
+                speculative = 1;
             }
-            Py_BEGIN_ALLOW_THREADS
-            sched_yield();
-            Py_END_ALLOW_THREADS
+            const Py_ssize_t r = rread[u];
+            if (!rows[u]) {
+                /* build the row: the live edges of a final node, every edge of a speculative one */
+                int64_t cnt = 0;
+                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                    const int64_t p = L.plist[g];
+                    const int64_t e0 = L.off[u] + L.pstart[p];
+                    if (speculative) cnt += counts[b[p]];
+                    else
+                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb) cnt += job.alive[e0 + cb];
+                }
+                PyObject* sd = _PyDict_NewPresized(cnt);
+                if (!sd) goto done;
+                rows[u] = sd;
+                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                    const int64_t p = L.plist[g];
+                    const int64_t e0 = L.off[u] + L.pstart[p];
+                    const int64_t vb = L.first[b[p]];
+                    PyObject *wv = NULL, *ev = NULL;
+                    for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
+                        if (!speculative && !job.alive[e0 + cb]) continue;
+                        if (!wv) {
+                            wv = int_of(ints, sc[p]);
+                            ev = int_of(ints, en[p]);
+                            if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
+                        }
+                        PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
+                        const int bad = !d || PyDict_SetItem(sd, PyList_GET_ITEM(names, vb + cb), d);
+                        Py_XDECREF(d);
+                        if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
+                        dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
+                    }
+                    Py_XDECREF(wv);
+                    Py_XDECREF(ev);
+                }
+                if (speculative) {
+                    spec[u] = 1;
+                    ++n_spec;
+                    continue;
+                }
+            } else {
+                /* a speculative row, final now: delete its removed edges */
+                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                    const int64_t p = L.plist[g];
+                    const int64_t e0 = L.off[u] + L.pstart[p];
+                    const int64_t vb = L.first[b[p]];
+                    for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
+                        if (!job.alive[e0 + cb]) {
+                            dptr[e0 + cb] = NULL;
+                            if (PyDict_DelItem(rows[u], PyList_GET_ITEM(names, vb + cb))) goto done;
+                            ++n_pruned;
+                        }
+                }
+            }
+            /* u's edges are final: count the live ones into their heads, and its edge to every copy of b is
+               one in-edge fewer for those heads to wait on */
+            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                const int64_t p = L.plist[g];
+                const int64_t e0 = L.off[u] + L.pstart[p];
+                const int64_t vb = L.first[b[p]];
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
+                    din[vb + cb] += job.alive[e0 + cb];
+                    if (--pending[vb + cb] == 0) ready[n_ready++] = vb + cb;
+                }
+            }
+            /* predecessors whose in-edges are all final */
+            while (n_ready > 0) {
+                const int64_t v = ready[--n_ready];
+                const Py_ssize_t rv = rread[v];
+                const int64_t cv = v - L.first[rv];
+                PyObject* pd = _PyDict_NewPresized(din[v]);
+                if (!pd) goto done;
+                pin[v] = pd;
+                for (int64_t g = bgoff[rv]; g < bgoff[rv + 1]; ++g) {
+                    const int64_t q = blist[g];
+                    for (int64_t t = L.first[a[q]]; t < L.first[a[q] + 1]; ++t) {
+                        PyObject* d = dptr[L.off[t] + L.pstart[q] + cv];
+                        if (d && PyDict_SetItem(pd, PyList_GET_ITEM(names, t), d)) goto done;
+                    }
+                }
+                ++n_pred;
+            }
         }
-        PyMem_Free(ready);
         pthread_join(th, NULL);
         started = 0;
+        if (trace) t_built = now_ms() - t0;
         if (job.rc != 0 || k_done != N || n_pred != N) {
             PyErr_Format(PyExc_RuntimeError, "ovl_remove_cycles_stream failed (rc %d, %lld of %lld nodes final, "
                          "%lld predecessor dicts)", job.rc, (long long)k_done, (long long)N, (long long)n_pred);
@@ -866,6 +938,10 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         PyObject* rem = PyBytes_FromStringAndSize((const char*)job.removed, (Py_ssize_t)(8 * job.n_removed));
         if (!rem) goto done;
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
+        if (trace)
+            fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% final) b=%.1f t=%.1f spec=%lld pruned=%lld\n", t_setup,
+                    t_replay, N ? 100.0 * (double)k_at_replay / (double)N : 100.0, t_built, now_ms() - t0,
+                    (long long)n_spec, (long long)n_pruned);
     }
 done:
     if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */
@@ -898,6 +974,8 @@ done:
     PyMem_Free(bgoff);
     PyMem_Free(blist);
     PyMem_Free(pending);
+    PyMem_Free(ready);
+    PyMem_Free(spec);
     PyMem_RawFree(job.removed);
     PyMem_RawFree(job.alive);
     PyMem_RawFree(job.final_nodes);
