@@ -16,3 +16,5 @@ SHARD_AB_SETTINGS="noramp=OVL_PACK_RAMP:0;ramp=;noramp_p64=OVL_PACK_RAMP:0,OVL_E
 echo "new ok"
 SHARD_AB_SETTINGS="noramp=OVL_PACK_RAMP:0;ramp=;pm64k=OVL_PACK_MIN:65536,OVL_PACK_RAMP:0" OVL_TRACE_PIPE=1 timeout -k 10 200 python -u tools/shard_step_ab.py 1 3 > $OUT/trace.json 2> $OUT/trace.err || { echo "trace failed"; tail -30 $OUT/trace.err; exit 1; }
 echo "trace ok"
+OVL_TRACE_STREAM=1 timeout -k 10 400 python -u tools/replay_ab.py 5 > $OUT/replay_ab.json 2> $OUT/replay_ab.err || { echo "replay ab failed"; tail -30 $OUT/replay_ab.err; exit 1; }
+echo "replay ab ok"
