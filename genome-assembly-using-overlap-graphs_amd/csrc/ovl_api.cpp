@@ -1083,7 +1083,11 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
     // chunk scores, and read by the scoring launch as they lie -- no decode launch.  Needs a-major tiles (a
     // within 255 of its tile's first, every a in range; the parts are cut at multiples of 64) and a
     // throughput-mode uniform launch; else the decode below.
-    if (wd == 2 && d->k.pairs_ix && C.plan->kernel == OVL_KERNEL_UNGAPPED && !C.plan->key64 && ix_launch(d, n)) {
+    // (OVL_TRACE_PIPE: 'x' marks a chunk that cannot be read in place, with the first failed condition)
+    const int ix_why = wd != 2 ? 1 : !d->k.pairs_ix ? 2 : C.plan->kernel != OVL_KERNEL_UNGAPPED ? 3
+                       : C.plan->key64 ? 4 : !ix_launch(d, n) ? 5 : 0;
+    if (g_trace && ix_why) g_trace->mark('x', ix_why);
+    if (ix_why == 0) {
         uint8_t* d8 = reinterpret_cast<uint8_t*>(ha);
         int32_t* tb = reinterpret_cast<int32_t*>(ha + (((size_t)n + 15) & ~size_t(15)));
         std::vector<uint8_t> bad(parts.size(), 0);
@@ -1095,6 +1099,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
             },
             run_pre);
         if (pre_rc != OVL_OK) return pre_rc;
+        if (g_trace && std::find(bad.begin(), bad.end(), 1) != bad.end()) g_trace->mark('x', 6);
         if (std::find(bad.begin(), bad.end(), 1) == bad.end()) {
             J.ixk[(size_t)k] = 1;  // (issue_chunk copies the chunk into HBM and launches on it)
             if (g_trace) g_trace->mark('e', k);

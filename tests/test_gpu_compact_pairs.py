@@ -195,7 +195,10 @@ def test_ix_in_place_vs_decode(oracle_mod, target, pinned):
             s, en = ix.score(a, b)
             np.testing.assert_array_equal(s, ref_s)
             np.testing.assert_array_equal(en, ref_e)
-            assert ix.last_pair_list() == {"in_place_pairs": n, "decoded_pairs": 0}
+            got = ix.last_pair_list()
+            assert got == {"in_place_pairs": n, "decoded_pairs": 0}, (got, ix.plan(), ix.info(), ix.last_transfer(),
+                                                                      {k: v for k, v in os.environ.items()
+                                                                       if k.startswith("OVL")})
         s, en = dec.score(a, b)
         np.testing.assert_array_equal(s, ref_s)
         np.testing.assert_array_equal(en, ref_e)
