@@ -86,15 +86,14 @@ struct Knobs {
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
     int32_t pack = 1;             // OVL_PACK=0: host-array results cross the link as int32 pairs even when the
                                   // packed form (2 bytes per pair) holds (tests)
-    int64_t pack_min = 1 << 18;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
+    int64_t pack_min = 1 << 16;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
+                                  // (64 K: a 250 K-pair shard -- N = 8 at the target point -- 0.057 -> 0.054 ms)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
     int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
                                   // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
                                   // instead of uniform_kernel reading b16 + tile deltas in place (tests)
-    int32_t pack_ramp = 1;        // OVL_PACK_RAMP=0 (A/B, round 4): equal packed chunks instead of a ramp
-    int64_t expand_part = 1 << 14;// OVL_EXPAND_PART (A/B, round 4): pairs per host-pool part of an expansion
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -112,8 +111,10 @@ constexpr int64_t kBlocksPerCu = 32;
 constexpr int32_t kBandLane2Min = 64;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
-// packed calls: the first chunk of a ramp (setup_job), then x 1.5 per chunk up to the chunk size
-constexpr int64_t kRampFirst = int64_t(3) << 16;
+// host expansion of packed results: pairs per pool part at least (finer parts than 64 K: the expansion of a
+// 250 K-pair shard 22.7 -> 9.4 us, the N = 4 step 0.085 -> 0.075 ms; tools/pool_probe.cpp,
+// profiles/r04_pool_ab_*.json)
+constexpr size_t kExpandPart = size_t(1) << 14;
 
 }  // namespace
 
@@ -688,8 +689,7 @@ Knobs read_knobs() {
         k.pack_adapt = 0;  // a fixed share
     }
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PACK_RAMP")) k.pack_ramp = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_EXPAND_PART")) k.expand_part = std::max(64LL, atoll(e));
+
     if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
@@ -915,8 +915,7 @@ int setup_job(const Call& C, Job& J) {
     HIPCHK(d, hipSetDevice(d->device));
     const bool need_in = C.h_a && !C.in_pinned && !C.compact, need_out = !C.out_pinned || C.pack;
     J.chunk = pick_chunk(d, n, need_in || need_out, C.pack);
-    // packed calls: the packed share in chunks of <= J.chunk (a ramp, or equal), then (pinned arrays) the direct
-    // share
+    // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
     if (C.pack) {
         double& share = C.compact ? d->pack_pct_h : d->pack_pct;
@@ -924,24 +923,13 @@ int setup_job(const Call& C, Job& J) {
         const int64_t pct = d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct;
         packed = C.out_pinned ? (n - n * pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
-        if (d->k.pack_ramp && d->k.pipe_chunk == 0 && packed >= 2 * kRampFirst && J.chunk >= kRampFirst) {
-            // a ramp: the host starts expanding after a short first kernel, and each next chunk's kernel
-            // (~48 us per M pairs at the target point) ends before the host has expanded the one before it
-            // (~68 us per M pairs), so the host never waits after the first
-            int64_t c = kRampFirst;
-            for (int64_t o = 0; o < packed;) {
-                int64_t sz = std::min(c, packed - o);
-                if (packed - o - sz < c / 2) sz = packed - o;  // no short tail chunk
-                o += sz;
-                J.cb.push_back(o);
-                c = std::min(J.chunk, ((c * 3 / 2) + 63) & ~int64_t(63));
-            }
-        } else {
-            const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
-            const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
-            for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
-            if (packed > 0) J.cb.push_back(packed);
-        }
+        // (a ramp of growing chunks -- 196 K, x 1.5 each -- to start the host's expansion sooner measured slower:
+        // 0.208 against 0.145 ms at the target point, each extra chunk costing an issue and a later direct
+        // chunk; profiles/r04_pool_ab_*.json)
+        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
+        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
+        if (packed > 0) J.cb.push_back(packed);
         J.n_packed = (int64_t)J.cb.size() - 1;
     }
     for (int64_t o = packed; o < n;) {
@@ -1259,7 +1247,7 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
     if (C.pack) {
         host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
-                    ss + d->st_cap, C.match, C.mismatch, true, (size_t)n, (size_t)d->k.expand_part);
+                    ss + d->st_cap, C.match, C.mismatch, true, (size_t)n, kExpandPart);
         return OVL_OK;
     }
     host_copy(C.out_s + (g - C.out_base), ss, sizeof(int32_t) * (size_t)n);

@@ -627,6 +627,119 @@ done:
     return out;
 }
 
+/* Out-edges that no removal can touch: remove_cycles_from_graph removes an edge only as the weakest of a cycle it
+   lies on, so a node in a strongly connected component of its own (and without a live self-loop) never loses an
+   out-edge again -- removals only delete edges, so components only split.  That holds for far more nodes, and far
+   sooner, than the replay's own final set (nodes that can reach no cycle, or whose start's walk is over: at the
+   target point 60 % of the nodes only at the end).  The helper recomputes the components of the live graph (Tarjan,
+   iterative) pass after pass while the replay runs and publishes every node newly alone in its component.  It reads
+   `alive` while the replay clears entries, so a pass sees a superset of the live edges; the components of a
+   supergraph contain the true ones, so a node alone in a pass's graph is alone in the true graph too.  Edges into
+   published nodes are skipped in later passes (such a node is on no cycle). */
+typedef struct {
+    const int64_t* off;
+    const int32_t* heads;
+    const uint8_t* alive;
+    int32_t n;
+    const int* stop;       /* the replay's finished flag */
+    int* gate;             /* set after the first pass (else already set) */
+    int32_t* nodes;        /* published nodes [0, n_pub) (release-ordered count) */
+    int64_t n_pub;
+    int passes;
+    int ok;
+} SccJob;
+
+static void* scc_main(void* arg) {
+    SccJob* j = (SccJob*)arg;
+    const int32_t N = j->n;
+    int32_t* index = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    int32_t* low = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    int32_t* stk = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    int32_t* cv = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));  /* call stack: node */
+    int64_t* cp = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N ? N : 1));  /* call stack: next edge */
+    uint8_t* on = (uint8_t*)malloc((size_t)(N ? N : 1));
+    uint8_t* alone = (uint8_t*)calloc((size_t)(N ? N : 1), 1);
+    if (!index || !low || !stk || !cv || !cp || !on || !alone) goto out;
+    j->ok = 1;
+    while (!__atomic_load_n(j->stop, __ATOMIC_ACQUIRE)) {
+        for (int32_t v = 0; v < N; ++v) index[v] = -1;
+        memset(on, 0, (size_t)N);
+        int32_t idx = 0, sp = 0;
+        int64_t pub = j->n_pub;
+        const int64_t pub0 = pub;
+        for (int32_t r = 0; r < N && !__atomic_load_n(j->stop, __ATOMIC_RELAXED); ++r) {
+            if (index[r] >= 0 || alone[r]) continue;
+            int32_t depth = 0;
+            cv[0] = r;
+            cp[0] = j->off[r];
+            index[r] = low[r] = idx++;
+            stk[sp++] = r;
+            on[r] = 1;
+            while (depth >= 0) {
+                const int32_t v = cv[depth];
+                const int64_t end = j->off[v + 1];
+                int64_t e = cp[depth];
+                int descended = 0;
+                for (; e < end; ++e) {
+                    if (!__atomic_load_n(&j->alive[e], __ATOMIC_ACQUIRE)) continue;
+                    const int32_t w = j->heads[e];
+                    if (alone[w]) continue;
+                    if (index[w] < 0) {
+                        cp[depth] = e + 1;
+                        ++depth;
+                        cv[depth] = w;
+                        cp[depth] = j->off[w];
+                        index[w] = low[w] = idx++;
+                        stk[sp++] = w;
+                        on[w] = 1;
+                        descended = 1;
+                        break;
+                    }
+                    if (on[w] && index[w] < low[v]) low[v] = index[w];
+                }
+                if (descended) continue;
+                /* v is done: the root of a component? */
+                if (low[v] == index[v]) {
+                    if (stk[sp - 1] == v) {
+                        /* a component of one: alone unless a live self-loop */
+                        int loop = 0;
+                        for (int64_t f = j->off[v]; f < end && !loop; ++f)
+                            loop = j->heads[f] == v && __atomic_load_n(&j->alive[f], __ATOMIC_ACQUIRE);
+                        if (!loop) {
+                            alone[v] = 1;
+                            j->nodes[pub++] = v;
+                            __atomic_store_n(&j->n_pub, pub, __ATOMIC_RELEASE);
+                        }
+                    }
+                    int32_t x;
+                    do {
+                        x = stk[--sp];
+                        on[x] = 0;
+                    } while (x != v);
+                }
+                --depth;
+                if (depth >= 0 && low[v] < low[cv[depth]]) low[cv[depth]] = low[v];
+            }
+        }
+        ++j->passes;
+        __atomic_store_n(j->gate, 1, __ATOMIC_RELEASE);
+        if (j->n_pub == pub0) {  /* nothing new: let the replay remove more before the next pass */
+            struct timespec ts = {0, 300000};
+            nanosleep(&ts, NULL);
+        }
+    }
+out:
+    __atomic_store_n(j->gate, 1, __ATOMIC_RELEASE);
+    free(index);
+    free(low);
+    free(stk);
+    free(cv);
+    free(cp);
+    free(on);
+    free(alone);
+    return NULL;
+}
+
 /* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
  *     -> (node, succ, pred, removed, n_removed)
  * remove_cycles_from_graph on a graph that is still columns, with the replay and the dicts overlapped: the replay
@@ -638,8 +751,8 @@ done:
  * node-ordered top-level dicts.  The result is build_overlap's for the alive mask of the replay; removed holds
  * the replay's removed CSR indices (int64) in removal order. */
 /* OVL_TRACE_STREAM=1 (diagnostics): one stderr line per build_overlap_stream with the millisecond offsets of its
-   phases (s setup done, r replay finished as seen here, with the share of nodes final by then, b dicts built,
-   t top-level dicts) */
+   phases (s setup done, r replay finished as seen here, with the share of the nodes whose rows were built by
+   then, b dicts built, t top-level dicts), the replay thread's own time and the CPUs both threads ran on */
 static double now_ms(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -661,11 +774,62 @@ typedef struct {
     int64_t n_final;
     int rc;
     int finished;
+    int pin;        /* OVL_STREAM_PIN (A/B): 0 none, 1 the caller's NUMA node less the caller's CPU, 2 its first CPU */
+    int gate;       /* the replay starts once this is non-zero (OVL_STREAM_SCC=2: after the helper's first pass) */
+    int cpu_main;   /* the calling thread's CPU when the replay started */
+    int cpu_start, cpu_end;
+    double ms;      /* the replay's own duration */
 } ReplayJob;
+
+/* CPUs of the NUMA node holding `cpu` (from sysfs), into `set`; 0 if not found */
+static int node_cpus(int cpu, cpu_set_t* set) {
+    char path[96], buf[4096];
+    for (int node = 0; node < 64; ++node) {
+        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+        FILE* f = fopen(path, "r");
+        if (!f) continue;
+        const size_t got = fread(buf, 1, sizeof(buf) - 1, f);
+        fclose(f);
+        buf[got] = 0;
+        CPU_ZERO(set);
+        int found = 0;
+        for (char* q = buf; *q && *q != '\n';) {
+            char* e;
+            long lo = strtol(q, &e, 10), hi = lo;
+            if (e == q) break;
+            if (*e == '-') hi = strtol(e + 1, &e, 10);
+            for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c) {
+                CPU_SET((int)c, set);
+                if (c == cpu) found = 1;
+            }
+            q = *e == ',' ? e + 1 : e;
+        }
+        if (found) return 1;
+    }
+    return 0;
+}
 
 static void* replay_main(void* arg) {
     ReplayJob* j = (ReplayJob*)arg;
+    if (j->pin == 1 && j->cpu_main >= 0) {
+        cpu_set_t node, mine, use;
+        if (node_cpus(j->cpu_main, &node) && sched_getaffinity(0, sizeof(mine), &mine) == 0) {
+            CPU_AND(&use, &node, &mine);
+            CPU_CLR(j->cpu_main, &use);
+            if (CPU_COUNT(&use) > 0) sched_setaffinity(0, sizeof(use), &use);
+        }
+    } else if (j->pin == 2) {
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(sched_getcpu(), &one);
+        sched_setaffinity(0, sizeof(one), &one);
+    }
+    while (!__atomic_load_n(&j->gate, __ATOMIC_ACQUIRE)) sched_yield();
+    j->cpu_start = sched_getcpu();
+    const double t0 = now_ms();
     j->rc = j->fn(j->off, j->heads, j->w, j->n, j->removed, &j->n_removed, j->alive, j->final_nodes, &j->n_final);
+    j->ms = now_ms() - t0;
+    j->cpu_end = sched_getcpu();
     __atomic_store_n(&j->finished, 1, __ATOMIC_RELEASE);
     return NULL;
 }
@@ -689,8 +853,14 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     memset(&L, 0, sizeof(L));
     ReplayJob job;
     memset(&job, 0, sizeof(job));
-    pthread_t th;
-    int started = 0;
+    pthread_t th, scc_th;
+    int started = 0, scc_started = 0;
+    SccJob scc;
+    memset(&scc, 0, sizeof(scc));
+    /* OVL_STREAM_SCC (tests, A/B): 0 rows only as the replay publishes them (no component helper); 2 the replay
+       waits for the helper's first pass (every node alone in the whole graph's components goes first) */
+    const char* scc_env = getenv("OVL_STREAM_SCC");
+    const int scc_on = scc_env ? atoi(scc_env) : 1;
     const char* tr_env = getenv("OVL_TRACE_STREAM");
     const int trace = tr_env && atoi(tr_env) != 0;
     const double t0 = trace ? now_ms() : 0.0;
@@ -702,7 +872,6 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     int64_t* din = NULL;
     int64_t* rread = NULL;
     int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL;
-    uint8_t* spec = NULL;
     if (!ints) { PyErr_NoMemory(); goto done; }
     if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end") ||
         take(ooff, &boff, 8, "off") || take(oh, &bh, 4, "heads") || take(ow, &bw, 8, "weights"))
@@ -748,6 +917,9 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             PyErr_NoMemory();
             goto done;
         }
+        /* all ones before either thread starts (the replay sets it too, but on its own thread, where the component
+           helper could read it first) */
+        memset(job.alive, 1, (size_t)E);
         for (Py_ssize_t r = 0; r < L.R; ++r)
             for (int64_t u = L.first[r]; u < L.first[r + 1]; ++u) rread[u] = r;
         for (Py_ssize_t p = 0; p < L.P; ++p)
@@ -780,6 +952,12 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         }
         Py_ssize_t iw, ie;
         attr_slots(tmpl, kw, ke, &iw, &ie);
+        {
+            const char* pin_env = getenv("OVL_STREAM_PIN");
+            job.pin = pin_env ? atoi(pin_env) : 0;
+            job.cpu_main = sched_getcpu();
+            job.gate = scc_on != 2;
+        }
         if (pthread_create(&th, NULL, replay_main, &job) != 0) {
             PyErr_SetString(PyExc_RuntimeError, "cannot start the replay thread");
             goto done;
@@ -787,115 +965,86 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         started = 1;
         if (trace) t_setup = now_ms() - t0;
         /* successors of each node as its out-edges become final (row order: kept pairs with a == its read in
-           list order, then the copies of b); predecessors of each node once every tail of its in-edges is.
-           Speculation: while the replay runs and no node is newly final, this thread builds the whole successor
-           row (removed edges included) of the next node in node order that is not final yet; when that node
-           becomes final, its removed edges are deleted from the row (PyDict_DelItem keeps the order of the
-           others, as DiGraph.remove_edge does).  A node's row is final at the end of the replay for ~60 % of the
-           target point's nodes, which without speculation all wait for it. */
-        int64_t k_done = 0, n_pred = 0, spec_next = 0, n_spec = 0, n_pruned = 0;
-        /* OVL_STREAM_SPEC (tests): 0 no speculation, 2 every node's row speculatively first (each one then
-           pruned), else (1) in idle time */
-        const char* spec_env = getenv("OVL_STREAM_SPEC");
-        const int spec_mode = spec_env ? atoi(spec_env) : 1;
+           list order, then the copies of b) -- published by the replay (settled or explored nodes) or by the
+           component helper (scc_main), whichever comes first; predecessors of each node once every tail of its
+           in-edges is */
+        if (scc_on) {
+            scc.off = job.off;
+            scc.heads = job.heads;
+            scc.alive = job.alive;
+            scc.n = (int32_t)N;
+            scc.stop = &job.finished;
+            scc.gate = &job.gate;
+            scc.nodes = (int32_t*)PyMem_RawMalloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+            if (!scc.nodes) { PyErr_NoMemory(); goto done; }
+            if (pthread_create(&scc_th, NULL, scc_main, &scc) != 0) {
+                PyErr_SetString(PyExc_RuntimeError, "cannot start the component thread");
+                goto done;
+            }
+            scc_started = 1;
+        }
+        int64_t k_done = 0, k_scc = 0, n_rows = 0, n_pred = 0, n_from_scc = 0;
         ready = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
-        spec = (uint8_t*)PyMem_Calloc((size_t)(N ? N : 1), 1);
         int64_t n_ready = 0;
-        if (!ready || !spec) { PyErr_NoMemory(); goto done; }
+        if (!ready) { PyErr_NoMemory(); goto done; }
         for (int64_t v = 0; v < N; ++v)
             if (pending[v] == 0) ready[n_ready++] = v;
         for (;;) {
-            const int64_t avail = __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE);
+            if (trace && t_replay < 0.0 && __atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
+                t_replay = now_ms() - t0;
+                k_at_replay = n_rows;
+            }
             int64_t u = -1;
-            int speculative = 0;
-            while (spec_mode == 2 && spec_next < N && rows[spec_next]) ++spec_next;
-            if (spec_mode == 2 && spec_next < N) {
-                u = spec_next++;
-                speculative = 1;
-            } else if (avail > k_done) {
+            if (k_done < __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE)) {
                 u = job.final_nodes[k_done++];
+            } else if (scc_started && k_scc < __atomic_load_n(&scc.n_pub, __ATOMIC_ACQUIRE)) {
+                u = scc.nodes[k_scc++];
+                if (!rows[u]) ++n_from_scc;
             } else if (__atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
-                if (trace && t_replay < 0.0) {
-                    t_replay = now_ms() - t0;
-                    k_at_replay = k_done;
-                }
                 if (__atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE) > k_done) continue;
                 break;
             } else {
-                while (spec_next < N && rows[spec_next]) ++spec_next;
-                if (spec_mode == 0 || spec_next >= N) {
-                    Py_BEGIN_ALLOW_THREADS
-                    sched_yield();
-                    Py_END_ALLOW_THREADS
-                    continue;
-                }
-                u = spec_next++;
-                speculative = 1;
+                Py_BEGIN_ALLOW_THREADS
+                sched_yield();
+                Py_END_ALLOW_THREADS
+                continue;
             }
+            if (rows[u]) continue;  /* (published by both) */
             const Py_ssize_t r = rread[u];
-            if (!rows[u]) {
-                /* build the row: the live edges of a final node, every edge of a speculative one */
-                int64_t cnt = 0;
-                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                    const int64_t p = L.plist[g];
-                    const int64_t e0 = L.off[u] + L.pstart[p];
-                    if (speculative) cnt += counts[b[p]];
-                    else
-                        for (int32_t cb = 0; cb < counts[b[p]]; ++cb) cnt += job.alive[e0 + cb];
-                }
-                PyObject* sd = _PyDict_NewPresized(cnt);
-                if (!sd) goto done;
-                rows[u] = sd;
-                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                    const int64_t p = L.plist[g];
-                    const int64_t e0 = L.off[u] + L.pstart[p];
-                    const int64_t vb = L.first[b[p]];
-                    PyObject *wv = NULL, *ev = NULL;
-                    for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                        if (!speculative && !job.alive[e0 + cb]) continue;
-                        if (!wv) {
-                            wv = int_of(ints, sc[p]);
-                            ev = int_of(ints, en[p]);
-                            if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
-                        }
-                        PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
-                        const int bad = !d || PyDict_SetItem(sd, PyList_GET_ITEM(names, vb + cb), d);
-                        Py_XDECREF(d);
-                        if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
-                        dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
-                    }
-                    Py_XDECREF(wv);
-                    Py_XDECREF(ev);
-                }
-                if (speculative) {
-                    spec[u] = 1;
-                    ++n_spec;
-                    continue;
-                }
-            } else {
-                /* a speculative row, final now: delete its removed edges */
-                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                    const int64_t p = L.plist[g];
-                    const int64_t e0 = L.off[u] + L.pstart[p];
-                    const int64_t vb = L.first[b[p]];
-                    for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
-                        if (!job.alive[e0 + cb]) {
-                            dptr[e0 + cb] = NULL;
-                            if (PyDict_DelItem(rows[u], PyList_GET_ITEM(names, vb + cb))) goto done;
-                            ++n_pruned;
-                        }
-                }
+            int64_t live = 0;
+            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                const int64_t p = L.plist[g];
+                const int64_t e0 = L.off[u] + L.pstart[p];
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) live += job.alive[e0 + cb];
             }
-            /* u's edges are final: count the live ones into their heads, and its edge to every copy of b is
-               one in-edge fewer for those heads to wait on */
+            PyObject* sd = _PyDict_NewPresized(live);
+            if (!sd) goto done;
+            rows[u] = sd;
+            ++n_rows;
             for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
                 const int64_t p = L.plist[g];
                 const int64_t e0 = L.off[u] + L.pstart[p];
                 const int64_t vb = L.first[b[p]];
+                PyObject *wv = NULL, *ev = NULL;
                 for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                    din[vb + cb] += job.alive[e0 + cb];
-                    if (--pending[vb + cb] == 0) ready[n_ready++] = vb + cb;
+                    if (!job.alive[e0 + cb]) continue;
+                    if (!wv) {
+                        wv = int_of(ints, sc[p]);
+                        ev = int_of(ints, en[p]);
+                        if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
+                    }
+                    PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
+                    const int bad = !d || PyDict_SetItem(sd, PyList_GET_ITEM(names, vb + cb), d);
+                    Py_XDECREF(d);
+                    if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
+                    dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
+                    ++din[vb + cb];
                 }
+                Py_XDECREF(wv);
+                Py_XDECREF(ev);
+                /* u's edge to every copy of b is final now */
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
+                    if (--pending[vb + cb] == 0) ready[n_ready++] = vb + cb;
             }
             /* predecessors whose in-edges are all final */
             while (n_ready > 0) {
@@ -917,8 +1066,12 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         }
         pthread_join(th, NULL);
         started = 0;
+        if (scc_started) {
+            pthread_join(scc_th, NULL);
+            scc_started = 0;
+        }
         if (trace) t_built = now_ms() - t0;
-        if (job.rc != 0 || k_done != N || n_pred != N) {
+        if (job.rc != 0 || k_done != N || n_rows != N || n_pred != N) {
             PyErr_Format(PyExc_RuntimeError, "ovl_remove_cycles_stream failed (rc %d, %lld of %lld nodes final, "
                          "%lld predecessor dicts)", job.rc, (long long)k_done, (long long)N, (long long)n_pred);
             goto done;
@@ -939,14 +1092,21 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         if (!rem) goto done;
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
         if (trace)
-            fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% final) b=%.1f t=%.1f spec=%lld pruned=%lld\n", t_setup,
-                    t_replay, N ? 100.0 * (double)k_at_replay / (double)N : 100.0, t_built, now_ms() - t0,
-                    (long long)n_spec, (long long)n_pruned);
+            fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows) b=%.1f t=%.1f scc=%d passes=%d first=%lld "
+                    "replay=%.1f pin=%d cpus main %d/%d replay %d/%d\n", t_setup, t_replay,
+                    N ? 100.0 * (double)k_at_replay / (double)N : 100.0, t_built, now_ms() - t0, scc_on, scc.passes,
+                    (long long)n_from_scc, job.ms, job.pin, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end);
     }
 done:
     if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */
+        __atomic_store_n(&job.gate, 1, __ATOMIC_RELEASE);  /* (if it still waits for the helper's first pass) */
         Py_BEGIN_ALLOW_THREADS
         pthread_join(th, NULL);
+        Py_END_ALLOW_THREADS
+    }
+    if (scc_started) {  /* (it stops once the replay has finished) */
+        Py_BEGIN_ALLOW_THREADS
+        pthread_join(scc_th, NULL);
         Py_END_ALLOW_THREADS
     }
     layout_free(&L);
@@ -975,7 +1135,7 @@ done:
     PyMem_Free(blist);
     PyMem_Free(pending);
     PyMem_Free(ready);
-    PyMem_Free(spec);
+    PyMem_RawFree(scc.nodes);
     PyMem_RawFree(job.removed);
     PyMem_RawFree(job.alive);
     PyMem_RawFree(job.final_nodes);

@@ -17,6 +17,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
 
 
+@pytest.fixture(autouse=True)
+def _no_knob_leaks():
+    """Every test leaves the library's environment knobs (OVL_*) as it found them: a knob left set changes what
+    the next tests' contexts do (a pipeline chunk size once turned the in-place pair-list path off for the rest
+    of the session).  monkeypatch's own restore runs before this check."""
+    before = {k: v for k, v in os.environ.items() if k.startswith("OVL_")}
+    yield
+    after = {k: v for k, v in os.environ.items() if k.startswith("OVL_")}
+    assert after == before, f"OVL_* environment changed by this test: {before} -> {after}"
+
+
 def load_golden(name):
     with open(os.path.join(GOLDEN, name), "r", encoding="utf-8") as fh:
         return json.load(fh)

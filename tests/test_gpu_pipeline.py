@@ -367,10 +367,14 @@ def test_contexts_on_concurrent_host_threads(oracle_mod, cfg2, cfg2_ref):
     reads, a, b = cfg2
     n = a.shape[0]
     errors, results = [], {}
+    # (engines made here, one at a time: _engine_env sets and restores os.environ, which threads would race on
+    # and could leave set for later tests)
+    engines = [_engine_env({"OVL_PIPE_CHUNK": str(9000 + 1000 * t)}) for t in range(4)]
+    assert "OVL_PIPE_CHUNK" not in os.environ
 
     def work(t):
         try:
-            eng = _engine_env({"OVL_PIPE_CHUNK": str(9000 + 1000 * t)})
+            eng = engines[t]
             try:
                 eng.set_reads(reads)
                 for rep in range(5):

@@ -141,14 +141,15 @@ def test_csr_from_columns_matches_graph_csr():
 
 
 @pytest.mark.parametrize("ms", [None, 3])
-@pytest.mark.parametrize("spec", ["1", "0", "2"])
-def test_streamed_removal_equals_serial(monkeypatch, ms, spec):
+@pytest.mark.parametrize("scc", ["1", "0", "2"])
+def test_streamed_removal_equals_serial(monkeypatch, ms, scc):
     """Cycle removal on a lazy graph with the replay and the survivors' dicts overlapped (ovl_remove_cycles_stream
     publishing final nodes to build_overlap_stream) leaves the graph the replay-then-dicts path leaves, every
-    view and shared attribute dict included; so does a graph with no cycle and one with no edge.  OVL_STREAM_SPEC:
-    rows built speculatively in idle time (1, the default), never (0), or every row speculatively first, each
-    then pruned of its removed edges (2)."""
-    monkeypatch.setenv("OVL_STREAM_SPEC", spec)
+    view and shared attribute dict included; so does a graph with no cycle and one with no edge.  OVL_STREAM_SCC:
+    rows also built as soon as the component helper finds their node alone in its strongly connected component
+    (1, the default), only as the replay publishes them (0), or with the replay held until the helper's first pass
+    has published every node alone in the whole graph's components (2)."""
+    monkeypatch.setenv("OVL_STREAM_SCC", scc)
     cases = [_case(s, n_reads=500) for s in (11, 12)] + [_case(13, n_reads=60, alphabet="A")]
     for d, c, a, b, sc, en in cases:
         E = og.OverlapEdges(d, c, a, b, sc, en, min_score=ms)

@@ -73,12 +73,12 @@ def main():
             gc.collect()
     # the whole lazy-graph removal (what end_to_end times): replay then survivors' dicts, or both overlapped
     og._digraph_mod = None  # (the tree's own build)
-    modes = ("serial", "stream_nospec", "stream")  # stream: speculative rows in idle time (OVL_STREAM_SPEC)
+    modes = ("serial", "stream_noscc", "stream")  # stream: with the component helper (OVL_STREAM_SCC)
     res["remove_cycles_s"] = {m: [] for m in modes}
     for _ in range(rounds):
         for mode in modes:
             og._STREAM_OFF = mode == "serial"
-            os.environ["OVL_STREAM_SPEC"] = "0" if mode == "stream_nospec" else "1"
+            os.environ["OVL_STREAM_SCC"] = "0" if mode == "stream_noscc" else "1"
             G = edges.to_digraph()
             t0 = time.perf_counter()
             og.remove_cycles_from_graph(G)
