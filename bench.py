@@ -763,7 +763,8 @@ def abi_one_shot(w, reps: int = 10):
     res = {"reads_bytes": int(enc[0].nbytes), "pairs": w.n_pairs}
     ref = (np.array(w.out[0]), np.array(w.out[1]))
     for label, (x, y) in (("pinned_pair_list", (pa, pb)), ("pageable_pair_list", (ga, gb))):
-        w.eng.score_pairs(w.reads, x, y, out=out, encoded=enc)
+        for _ in range(40):  # (the direct share of compact-list calls settles within ~30 calls, pack_share)
+            w.eng.score_pairs(w.reads, x, y, out=out, encoded=enc)
         t0 = time.perf_counter()
         for _ in range(reps):
             w.eng.score_pairs(w.reads, x, y, out=out, encoded=enc)
@@ -777,7 +778,8 @@ def abi_one_shot(w, reps: int = 10):
     buf2 = enc[0].copy()
     buf2[0] = ord("C") if buf2[0] != ord("C") else ord("A")
     enc2 = (buf2, enc[1])
-    w.eng.score_pairs(w.reads, pa, pb, out=out, encoded=enc2)
+    for i in range(10):
+        w.eng.score_pairs(w.reads, pa, pb, out=out, encoded=enc if i % 2 == 0 else enc2)
     t0 = time.perf_counter()
     for i in range(reps):
         w.eng.score_pairs(w.reads, pa, pb, out=out, encoded=enc if i % 2 == 0 else enc2)
@@ -792,8 +794,10 @@ def abi_one_shot(w, reps: int = 10):
         w.eng.set_reads(w.reads, enc)
     res["set_reads_ms"] = (time.perf_counter() - t0) / reps * 1e3
     w.eng.enumerate_candidates(w.cfg["k"])  # the resident list again (set_reads dropped it)
-    res["what"] = ("ovl_score_pairs(seqs, offsets, n_reads, a_idx, b_idx, ...) per call: reads uploaded and packed "
-                   "every call, pair list read from host memory, (score, end) into pinned host arrays")
+    res["what"] = ("ovl_score_pairs(seqs, offsets, n_reads, a_idx, b_idx, ...) per call: the reads handed over every "
+                   "call (raw bytes + offsets) -- compared byte for byte with the resident set, uploaded and packed "
+                   "when they differ (pinned_pair_list_new_reads: every call) --, the pair list read from host "
+                   "memory, (score, end) into pinned host arrays; steady state after 40 calls")
     return res
 
 
