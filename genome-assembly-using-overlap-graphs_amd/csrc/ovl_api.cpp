@@ -184,7 +184,9 @@ struct Dev {
     uint32_t* cur_flag = nullptr;    // the flag the next launches write: err_flag (device calls) or h_flag_dev
     int32_t out_mode = 0;            // result sink of the next ungapped launches (OvlUngappedArgs::host_out):
                                      // 0 HBM, 1 host-mapped int32 arrays, 2 host-mapped packed uint16
-    std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk
+    std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk (recorded on the stream around the launch)
+    std::vector<hipEvent_t> k_ev;  // timing: the same recorded by an ungapped launch itself (kernel start / end)
+    hipEvent_t kev_start = nullptr, kev_stop = nullptr;  // the next ungapped launch records these (then cleared)
     // compact host pair lists (encode_chunk): pinned encoding buffer (8 bytes per pair + slack), its device
     // address, a decode event per chunk, and the encoded bytes of the last call
     char* cp_host = nullptr;
@@ -523,6 +525,9 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         // uniform_kernel scores the other pairs through its LDS side ring
         g.lw = c->planes == 2 ? c->lmax : 0;
         g.full = as<uint32_t>(c->full);
+        // (timing: this launch records the chunk's kernel events itself, once; issue_chunk checks they were taken)
+        g.ev_start = c->kev_start;
+        g.ev_stop = c->kev_stop;
         g.match = match;
         g.mismatch = mismatch;
         g.out_score = d_score;
@@ -553,6 +558,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
             }
         }
         HIPCHK(c, ovl_launch_ungapped(&g, s));
+        if (g.ev_start && g.lw > 0) c->kev_start = c->kev_stop = nullptr;  // (uniform_kernel recorded them)
     } else {
         OvlDpArgs g{};
         g.codes = as<uint8_t>(c->codes);
@@ -751,6 +757,8 @@ void destroy_dev(Dev* d) {
         if (d->ev_k[i]) (void)hipEventDestroy(d->ev_k[i]);
     for (hipEvent_t e : d->t_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d->k_ev)
+        if (e) (void)hipEventDestroy(e);
     if (d->scratch_evt) (void)hipEventDestroy(d->scratch_evt);
     if (d->ev_last) (void)hipEventDestroy(d->ev_last);
     for (hipStream_t s : {d->stream, d->s_in})
@@ -901,6 +909,7 @@ struct Job {
     int32_t* d_score = nullptr;  // device results (local indexing)
     int32_t* d_end = nullptr;
     std::vector<uint8_t> ixk;    // C.compact: chunk k's list is read in place by uniform_kernel (encode_chunk)
+    std::vector<uint8_t> kexact; // timing: chunk k's kernel recorded its own start / end (k_ev)
 };
 
 // Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
@@ -994,8 +1003,11 @@ int setup_job(const Call& C, Job& J) {
             hipEvent_t ev;
             HIPCHK(d, hipEventCreate(&ev));
             d->t_ev.push_back(ev);
+            HIPCHK(d, hipEventCreate(&ev));
+            d->k_ev.push_back(ev);
         }
     }
+    if (C.timing) J.kexact.assign((size_t)J.nchunks, 0);
     return OVL_OK;
 }
 
@@ -1215,8 +1227,16 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     int32_t* os = staged_out ? d->st_out_dev + so : J.d_score + off;
     int32_t* oe = staged_out ? d->st_out_dev + so + d->st_cap : J.d_end + off;
     d->out_mode = C.pack && k < J.n_packed ? 2 : 1;
-    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
+    if (C.timing) {
+        HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
+        if (C.plan->kernel == OVL_KERNEL_UNGAPPED) {  // (a chunk of one ungapped launch: time the kernel itself)
+            d->kev_start = d->k_ev[2 * k];
+            d->kev_stop = d->k_ev[2 * k + 1];
+        }
+    }
     int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
+    if (C.timing) J.kexact[(size_t)k] = d->kev_start == nullptr && C.plan->kernel == OVL_KERNEL_UNGAPPED;
+    d->kev_start = d->kev_stop = nullptr;
     d->ix_b16 = nullptr;
     d->ix_d8 = nullptr;
     d->ix_base = nullptr;
@@ -1364,7 +1384,9 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
             double s = 0.0;
             for (int64_t k = 0; k < J.nchunks; ++k) {
                 float ms = 0.f;
-                if (hipEventElapsedTime(&ms, d->t_ev[2 * k], d->t_ev[2 * k + 1]) == hipSuccess) s += ms;
+                const bool exact = k < (int64_t)J.kexact.size() && J.kexact[(size_t)k];
+                const hipEvent_t* ev = exact ? &d->k_ev[2 * (size_t)k] : &d->t_ev[2 * (size_t)k];
+                if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) s += ms;
                 // the chunk's result sink (issue_chunk): packed staging, or int32 into host memory
                 const int32_t sink = C.pack && k < J.n_packed ? 2 : 1;
                 c->t_launches.push_back({d->device, sink, J.cb[(size_t)k + 1] - J.cb[(size_t)k], (double)ms});

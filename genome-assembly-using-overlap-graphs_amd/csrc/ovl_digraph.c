@@ -740,6 +740,55 @@ out:
     return NULL;
 }
 
+/* A node's predecessor dict, built as a prefix of its in-edges in insertion order (kept pairs with b == its read in
+   list order, then the copies of a): the cursor (pg, pt: pair group and tail copy) advances while the next in-edge's
+   tail has its row built (that tail's out-edges are final, so the edge's fate is known), inserting the live ones. */
+typedef struct {
+    const Layout* L;
+    const int32_t* a;
+    const int64_t* blist;
+    const int64_t* bgoff;
+    const int64_t* rread;
+    const int64_t* indeg;   /* in-edges of the node, live or not (the dict's presize) */
+    PyObject* const* rows;
+    PyObject* const* dptr;
+    PyObject* names;
+    PyObject** pin;
+    int64_t* pg;            /* -1: complete */
+    int64_t* pt;
+    int64_t n_pred;
+} PredCtx;
+
+static int pred_advance(PredCtx* X, int64_t v) {
+    int64_t g = X->pg[v];
+    if (g < 0) return 0;
+    const Py_ssize_t rv = (Py_ssize_t)X->rread[v];
+    const int64_t gend = X->bgoff[rv + 1];
+    const int64_t cv = v - X->L->first[rv];
+    int64_t t = X->pt[v];
+    while (g < gend) {
+        const int64_t q = X->blist[g];
+        const int64_t tend = X->L->first[X->a[q] + 1];
+        for (; t < tend; ++t) {
+            if (!X->rows[t]) {
+                X->pg[v] = g;
+                X->pt[v] = t;
+                return 0;
+            }
+            PyObject* d = X->dptr[X->L->off[t] + X->L->pstart[q] + cv];
+            if (d) {
+                if (!X->pin[v] && !(X->pin[v] = _PyDict_NewPresized(X->indeg[v]))) return -1;
+                if (PyDict_SetItem(X->pin[v], PyList_GET_ITEM(X->names, t), d)) return -1;
+            }
+        }
+        if (++g < gend) t = X->L->first[X->a[X->blist[g]]];
+    }
+    if (!X->pin[v] && !(X->pin[v] = PyDict_New())) return -1;
+    X->pg[v] = -1;
+    ++X->n_pred;
+    return 0;
+}
+
 /* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
  *     -> (node, succ, pred, removed, n_removed)
  * remove_cycles_from_graph on a graph that is still columns, with the replay and the dicts overlapped: the replay
@@ -869,9 +918,8 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
     PyObject **rows = NULL, **dptr = NULL, **pin = NULL;
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
-    int64_t* din = NULL;
     int64_t* rread = NULL;
-    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL;
+    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL, *pg = NULL, *pt = NULL;
     if (!ints) { PyErr_NoMemory(); goto done; }
     if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end") ||
         take(ooff, &boff, 8, "off") || take(oh, &bh, 4, "heads") || take(ow, &bw, 8, "weights"))
@@ -906,13 +954,12 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         rows = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
         pin = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
         dptr = (PyObject**)PyMem_Calloc((size_t)(E ? E : 1), sizeof(PyObject*));
-        din = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
         rread = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
         /* in-edges in insertion order: the kept pairs grouped by b (list order within a group) */
         bgoff = (int64_t*)PyMem_Calloc((size_t)L.R + 1, sizeof(int64_t));
         blist = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(L.P ? L.P : 1));
         pending = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
-        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !din || !rread || !bgoff ||
+        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !rread || !bgoff ||
             !blist || !pending) {
             PyErr_NoMemory();
             goto done;
@@ -933,7 +980,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                 if (!keep || keep[p]) blist[fill[b[p]]++] = p;
             PyMem_Free(fill);
         }
-        /* a node's in-edges whose tail is not final yet (every copy of one read has the same in-edges) */
+        /* a node's in-edges, live or not (every copy of one read has the same in-edges) */
         for (Py_ssize_t r = 0; r < L.R; ++r) {
             int64_t k = 0;
             for (int64_t g = bgoff[r]; g < bgoff[r + 1]; ++g) k += L.first[a[blist[g]] + 1] - L.first[a[blist[g]]];
@@ -983,12 +1030,17 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             }
             scc_started = 1;
         }
-        int64_t k_done = 0, k_scc = 0, n_rows = 0, n_pred = 0, n_from_scc = 0;
-        ready = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
-        int64_t n_ready = 0;
-        if (!ready) { PyErr_NoMemory(); goto done; }
-        for (int64_t v = 0; v < N; ++v)
-            if (pending[v] == 0) ready[n_ready++] = v;
+        int64_t k_done = 0, k_scc = 0, n_rows = 0, n_from_scc = 0;
+        pg = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        pt = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        if (!pg || !pt) { PyErr_NoMemory(); goto done; }
+        PredCtx X = {&L, a, blist, bgoff, rread, pending, rows, dptr, names, pin, pg, pt, 0};
+        for (int64_t v = 0; v < N; ++v) {
+            const Py_ssize_t rv = (Py_ssize_t)rread[v];
+            pg[v] = bgoff[rv];
+            pt[v] = bgoff[rv] < bgoff[rv + 1] ? L.first[a[blist[bgoff[rv]]]] : 0;
+            if (pred_advance(&X, v)) goto done;  /* (completes the nodes without in-edges) */
+        }
         for (;;) {
             if (trace && t_replay < 0.0 && __atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
                 t_replay = now_ms() - t0;
@@ -1038,32 +1090,19 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                     Py_XDECREF(d);
                     if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
                     dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
-                    ++din[vb + cb];
                 }
                 Py_XDECREF(wv);
                 Py_XDECREF(ev);
-                /* u's edge to every copy of b is final now */
-                for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
-                    if (--pending[vb + cb] == 0) ready[n_ready++] = vb + cb;
             }
-            /* predecessors whose in-edges are all final */
-            while (n_ready > 0) {
-                const int64_t v = ready[--n_ready];
-                const Py_ssize_t rv = rread[v];
-                const int64_t cv = v - L.first[rv];
-                PyObject* pd = _PyDict_NewPresized(din[v]);
-                if (!pd) goto done;
-                pin[v] = pd;
-                for (int64_t g = bgoff[rv]; g < bgoff[rv + 1]; ++g) {
-                    const int64_t q = blist[g];
-                    for (int64_t t = L.first[a[q]]; t < L.first[a[q] + 1]; ++t) {
-                        PyObject* d = dptr[L.off[t] + L.pstart[q] + cv];
-                        if (d && PyDict_SetItem(pd, PyList_GET_ITEM(names, t), d)) goto done;
-                    }
-                }
-                ++n_pred;
+            /* u's out-edges are final: its heads' predecessor dicts may advance past it */
+            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                const int64_t p = L.plist[g];
+                const int64_t vb = L.first[b[p]];
+                for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
+                    if (pred_advance(&X, vb + cb)) goto done;
             }
         }
+        const int64_t n_pred = X.n_pred;
         pthread_join(th, NULL);
         started = 0;
         if (scc_started) {
@@ -1129,12 +1168,13 @@ done:
         PyMem_Free(pin);
     }
     PyMem_Free(dptr);
-    PyMem_Free(din);
     PyMem_Free(rread);
     PyMem_Free(bgoff);
     PyMem_Free(blist);
     PyMem_Free(pending);
     PyMem_Free(ready);
+    PyMem_Free(pg);
+    PyMem_Free(pt);
     PyMem_RawFree(scc.nodes);
     PyMem_RawFree(job.removed);
     PyMem_RawFree(job.alive);

@@ -41,6 +41,8 @@ struct OvlUngappedArgs {
     int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
                          // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
                          // out_score as uint16, the score of the few pairs that need it in out_end
+    hipEvent_t ev_start; // non-null (timing): uniform_kernel's launch records these at the kernel's own start and
+    hipEvent_t ev_stop;  // end (hipExtLaunchKernelGGL), without the dispatch wait that stream events include
 };
 
 // kernels of the band knob (ovl_launch_dp); OVL_BAND_FORM env picks one for tests

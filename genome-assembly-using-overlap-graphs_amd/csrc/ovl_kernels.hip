@@ -29,6 +29,8 @@
 
 #include <type_traits>
 
+#include <hip/hip_ext.h>
+
 #include "ovl_kernels.h"
 
 // uniform sweep: two shifts from one shifted row (sweep_uniform, keys_s2 / keys_t2); 0: one shifted row per shift
@@ -1589,6 +1591,13 @@ extern "C" hipError_t ovl_launch_pack(int planes, const uint8_t* codes, const in
 
 template <int W, int KM, bool LAT, int OM, bool IX = false>
 static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStream_t stream) {
+    if (g.ev_start) {
+        hipExtLaunchKernelGGL(uniform_kernel<W, KM, LAT, OM, IX>, dim3(blocks), dim3(256), 0, stream, g.ev_start,
+                              g.ev_stop, 0, g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full,
+                              g.match, g.mismatch, g.out_score, g.out_end, g.err_flag, g.heavy_ids, g.tile_flags,
+                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
+        return;
+    }
     uniform_kernel<W, KM, LAT, OM, IX><<<blocks, 256, 0, stream>>>(
         g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full, g.match, g.mismatch, g.out_score,
         g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
