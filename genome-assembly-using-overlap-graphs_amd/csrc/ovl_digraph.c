@@ -742,7 +742,7 @@ out:
 
 /* A node's predecessor dict, built as a prefix of its in-edges in insertion order (kept pairs with b == its read in
    list order, then the copies of a): the cursor (pg, pt: pair group and tail copy) advances while the next in-edge's
-   tail has its row built (that tail's out-edges are final, so the edge's fate is known), inserting the live ones. */
+   fate is known (its tail's successor row has passed it: dec), inserting the live ones. */
 typedef struct {
     const Layout* L;
     const int32_t* a;
@@ -750,7 +750,7 @@ typedef struct {
     const int64_t* bgoff;
     const int64_t* rread;
     const int64_t* indeg;   /* in-edges of the node, live or not (the dict's presize) */
-    PyObject* const* rows;
+    const uint8_t* dec;     /* per edge: its fate is known (its tail's row has passed it) */
     PyObject* const* dptr;
     PyObject* names;
     PyObject** pin;
@@ -770,12 +770,13 @@ static int pred_advance(PredCtx* X, int64_t v) {
         const int64_t q = X->blist[g];
         const int64_t tend = X->L->first[X->a[q] + 1];
         for (; t < tend; ++t) {
-            if (!X->rows[t]) {
+            const int64_t e = X->L->off[t] + X->L->pstart[q] + cv;
+            if (!X->dec[e]) {
                 X->pg[v] = g;
                 X->pt[v] = t;
                 return 0;
             }
-            PyObject* d = X->dptr[X->L->off[t] + X->L->pstart[q] + cv];
+            PyObject* d = X->dptr[e];
             if (d) {
                 if (!X->pin[v] && !(X->pin[v] = _PyDict_NewPresized(X->indeg[v]))) return -1;
                 if (PyDict_SetItem(X->pin[v], PyList_GET_ITEM(X->names, t), d)) return -1;
@@ -787,6 +788,82 @@ static int pred_advance(PredCtx* X, int64_t v) {
     X->pg[v] = -1;
     ++X->n_pred;
     return 0;
+}
+
+/* A node's successor dict, built the same way as a prefix of its out-edges in row order (kept pairs with a == its
+   read in list order, then the copies of b): an out-edge's fate is known once it is removed (alive 0: removals are
+   final), once its head is on no cycle (published by the replay or the component helper: no cycle can hold the
+   edge, so it is never removed), or once the tail itself is published (all its out-edges final).  Each edge passed
+   is marked decided and lets its head's predecessor dict advance. */
+typedef struct {
+    PredCtx* P;
+    const int32_t* counts;
+    const int32_t* b;
+    const int32_t* sc;
+    const int32_t* en;
+    const uint8_t* alive;
+    const uint8_t* pub;     /* per node: published (on no cycle) */
+    const int64_t* outdeg;  /* out-edges of the node, live or not (the dict's presize) */
+    PyObject** rows;
+    PyObject** dptr;
+    uint8_t* dec;
+    int64_t* rg;            /* row cursor: pair group (-1: complete) */
+    int32_t* rc;            /*             copy of b */
+    PyObject** ints;
+    PyObject *tmpl, *kw, *ke;
+    Py_ssize_t iw, ie;
+    int64_t n_rows;         /* complete rows */
+    int64_t n_dec;          /* decided edges */
+    int64_t n_ins;          /* live edges inserted */
+} RowCtx;
+
+/* advance u's row; `all`: u is published (every edge decided).  1 if it moved, 0 if not, -1 on error */
+static int row_advance(RowCtx* R, int64_t u, int all) {
+    int64_t g = R->rg[u];
+    if (g < 0) return 0;
+    const Layout* L = R->P->L;
+    const Py_ssize_t r = (Py_ssize_t)R->P->rread[u];
+    const int64_t gend = L->goff[r + 1];
+    int32_t cb = R->rc[u];
+    int moved = 0;
+    while (g < gend) {
+        const int64_t p = L->plist[g];
+        const int64_t e0 = L->off[u] + L->pstart[p];
+        const int64_t vb = L->first[R->b[p]];
+        const int32_t nb = R->counts[R->b[p]];
+        for (; cb < nb; ++cb) {
+            const int64_t e = e0 + cb;
+            const int live = __atomic_load_n(&R->alive[e], __ATOMIC_ACQUIRE);
+            if (live && !all && !R->pub[vb + cb]) {
+                R->rg[u] = g;
+                R->rc[u] = cb;
+                return moved;
+            }
+            if (live) {
+                if (!R->rows[u] && !(R->rows[u] = _PyDict_NewPresized(R->outdeg[u]))) return -1;
+                PyObject* wv = int_of(R->ints, R->sc[p]);
+                PyObject* ev = int_of(R->ints, R->en[p]);
+                PyObject* d = wv && ev ? new_attr(R->tmpl, R->kw, R->ke, R->iw, R->ie, wv, ev) : NULL;
+                Py_XDECREF(wv);
+                Py_XDECREF(ev);
+                const int bad = !d || PyDict_SetItem(R->rows[u], PyList_GET_ITEM(R->P->names, vb + cb), d);
+                Py_XDECREF(d);
+                if (bad) return -1;
+                R->dptr[e] = d; /* borrowed: the successor dict holds it */
+                ++R->n_ins;
+            }
+            R->dec[e] = 1;
+            ++R->n_dec;
+            moved = 1;
+            if (pred_advance(R->P, vb + cb)) return -1;
+        }
+        ++g;
+        cb = 0;
+    }
+    if (!R->rows[u] && !(R->rows[u] = PyDict_New())) return -1;
+    R->rg[u] = -1;
+    ++R->n_rows;
+    return 1;
 }
 
 /* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
@@ -914,12 +991,15 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     const int trace = tr_env && atoi(tr_env) != 0;
     const double t0 = trace ? now_ms() : 0.0;
     double t_setup = 0.0, t_replay = -1.0, t_built = 0.0;
-    int64_t k_at_replay = 0;
+    int64_t k_at_replay = 0, dec_at_replay = 0, ins_at_replay = 0;
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
     PyObject **rows = NULL, **dptr = NULL, **pin = NULL;
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t* rread = NULL;
-    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL, *pg = NULL, *pt = NULL;
+    int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL, *pg = NULL, *pt = NULL, *rg = NULL;
+    int64_t *outdeg = NULL, *openl = NULL;
+    int32_t* rc = NULL;
+    uint8_t *pubd = NULL, *dec = NULL;
     if (!ints) { PyErr_NoMemory(); goto done; }
     if (cols_take(&C, oc, oa, ob, ok) || take(os, &bs, 4, "score") || take(oe, &be, 4, "end") ||
         take(ooff, &boff, 8, "off") || take(oh, &bh, 4, "heads") || take(ow, &bw, 8, "weights"))
@@ -1030,78 +1110,80 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             }
             scc_started = 1;
         }
-        int64_t k_done = 0, k_scc = 0, n_rows = 0, n_from_scc = 0;
+        int64_t k_done = 0, k_scc = 0, n_pub = 0, n_from_scc = 0, n_sweeps = 0;
         pg = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
         pt = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
-        if (!pg || !pt) { PyErr_NoMemory(); goto done; }
-        PredCtx X = {&L, a, blist, bgoff, rread, pending, rows, dptr, names, pin, pg, pt, 0};
+        rg = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        rc = (int32_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int32_t));
+        outdeg = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
+        pubd = (uint8_t*)PyMem_Calloc((size_t)(N ? N : 1), 1);
+        dec = (uint8_t*)PyMem_Calloc((size_t)(E ? E : 1), 1);
+        openl = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
+        if (!pg || !pt || !rg || !rc || !outdeg || !pubd || !dec || !openl) { PyErr_NoMemory(); goto done; }
+        PredCtx X = {&L, a, blist, bgoff, rread, pending, dec, dptr, names, pin, pg, pt, 0};
         for (int64_t v = 0; v < N; ++v) {
             const Py_ssize_t rv = (Py_ssize_t)rread[v];
             pg[v] = bgoff[rv];
             pt[v] = bgoff[rv] < bgoff[rv + 1] ? L.first[a[blist[bgoff[rv]]]] : 0;
-            if (pred_advance(&X, v)) goto done;  /* (completes the nodes without in-edges) */
+            rg[v] = L.goff[rv];
+            for (int64_t g = L.goff[rv]; g < L.goff[rv + 1]; ++g) outdeg[v] += counts[b[L.plist[g]]];
+            openl[v] = v;
         }
+        int64_t n_open = N;
+        RowCtx R = {&X, counts, b, sc, en, job.alive, pubd, outdeg, rows, dptr, dec, rg, rc, ints, tmpl, kw, ke, iw, ie,
+                    0, 0, 0};
+        for (int64_t v = 0; v < N; ++v)
+            if (pred_advance(&X, v)) goto done;  /* (completes the nodes without in-edges) */
         for (;;) {
             if (trace && t_replay < 0.0 && __atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
                 t_replay = now_ms() - t0;
-                k_at_replay = n_rows;
+                k_at_replay = R.n_rows;
+                dec_at_replay = R.n_dec;
+                ins_at_replay = R.n_ins;
             }
             int64_t u = -1;
             if (k_done < __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE)) {
                 u = job.final_nodes[k_done++];
             } else if (scc_started && k_scc < __atomic_load_n(&scc.n_pub, __ATOMIC_ACQUIRE)) {
                 u = scc.nodes[k_scc++];
-                if (!rows[u]) ++n_from_scc;
-            } else if (__atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
+                if (!pubd[u]) ++n_from_scc;
+            }
+            if (u >= 0) {
+                if (pubd[u]) continue;  /* (published by both) */
+                pubd[u] = 1;
+                ++n_pub;
+                if (row_advance(&R, u, 1) < 0) goto done;
+                continue;
+            }
+            if (__atomic_load_n(&job.finished, __ATOMIC_ACQUIRE)) {
                 if (__atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE) > k_done) continue;
                 break;
-            } else {
+            }
+            /* nothing newly published: advance the openl rows as far as their heads allow */
+            int moved = 0;
+            int64_t keep_n = 0;
+            for (int64_t i = 0; i < n_open; ++i) {
+                const int64_t x = openl[i];
+                if (rg[x] < 0) continue;
+                const int m = row_advance(&R, x, 0);
+                if (m < 0) goto done;
+                moved |= m;
+                if (rg[x] >= 0) openl[keep_n++] = x;
+                if ((i & 255) == 255 && k_done < __atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE)) {
+                    /* (newly published nodes first: keep the rest of the list for the next sweep) */
+                    for (int64_t j = i + 1; j < n_open; ++j) openl[keep_n++] = openl[j];
+                    break;
+                }
+            }
+            n_open = keep_n;
+            ++n_sweeps;
+            if (!moved) {
                 Py_BEGIN_ALLOW_THREADS
                 sched_yield();
                 Py_END_ALLOW_THREADS
-                continue;
-            }
-            if (rows[u]) continue;  /* (published by both) */
-            const Py_ssize_t r = rread[u];
-            int64_t live = 0;
-            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                const int64_t p = L.plist[g];
-                const int64_t e0 = L.off[u] + L.pstart[p];
-                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) live += job.alive[e0 + cb];
-            }
-            PyObject* sd = _PyDict_NewPresized(live);
-            if (!sd) goto done;
-            rows[u] = sd;
-            ++n_rows;
-            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                const int64_t p = L.plist[g];
-                const int64_t e0 = L.off[u] + L.pstart[p];
-                const int64_t vb = L.first[b[p]];
-                PyObject *wv = NULL, *ev = NULL;
-                for (int32_t cb = 0; cb < counts[b[p]]; ++cb) {
-                    if (!job.alive[e0 + cb]) continue;
-                    if (!wv) {
-                        wv = int_of(ints, sc[p]);
-                        ev = int_of(ints, en[p]);
-                        if (!wv || !ev) { Py_XDECREF(wv); Py_XDECREF(ev); goto done; }
-                    }
-                    PyObject* d = new_attr(tmpl, kw, ke, iw, ie, wv, ev);
-                    const int bad = !d || PyDict_SetItem(sd, PyList_GET_ITEM(names, vb + cb), d);
-                    Py_XDECREF(d);
-                    if (bad) { Py_DECREF(wv); Py_DECREF(ev); goto done; }
-                    dptr[e0 + cb] = d; /* borrowed: the successor dict holds it */
-                }
-                Py_XDECREF(wv);
-                Py_XDECREF(ev);
-            }
-            /* u's out-edges are final: its heads' predecessor dicts may advance past it */
-            for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
-                const int64_t p = L.plist[g];
-                const int64_t vb = L.first[b[p]];
-                for (int32_t cb = 0; cb < counts[b[p]]; ++cb)
-                    if (pred_advance(&X, vb + cb)) goto done;
             }
         }
+        const int64_t n_rows = R.n_rows;
         const int64_t n_pred = X.n_pred;
         pthread_join(th, NULL);
         started = 0;
@@ -1131,9 +1213,11 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         if (!rem) goto done;
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
         if (trace)
-            fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows) b=%.1f t=%.1f scc=%d passes=%d first=%lld "
+            fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows, %.0f%% edges, %lld inserted) b=%.1f t=%.1f sweeps=%lld scc=%d passes=%d first=%lld "
                     "replay=%.1f pin=%d cpus main %d/%d replay %d/%d\n", t_setup, t_replay,
-                    N ? 100.0 * (double)k_at_replay / (double)N : 100.0, t_built, now_ms() - t0, scc_on, scc.passes,
+                    N ? 100.0 * (double)k_at_replay / (double)N : 100.0,
+                    E ? 100.0 * (double)dec_at_replay / (double)E : 100.0, (long long)ins_at_replay, t_built, now_ms() - t0, (long long)n_sweeps,
+                    scc_on, scc.passes,
                     (long long)n_from_scc, job.ms, job.pin, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end);
     }
 done:
@@ -1175,6 +1259,12 @@ done:
     PyMem_Free(ready);
     PyMem_Free(pg);
     PyMem_Free(pt);
+    PyMem_Free(rg);
+    PyMem_Free(rc);
+    PyMem_Free(outdeg);
+    PyMem_Free(pubd);
+    PyMem_Free(dec);
+    PyMem_Free(openl);
     PyMem_RawFree(scc.nodes);
     PyMem_RawFree(job.removed);
     PyMem_RawFree(job.alive);
