@@ -900,56 +900,14 @@ typedef struct {
     int64_t n_final;
     int rc;
     int finished;
-    int pin;        /* OVL_STREAM_PIN (A/B): 0 none, 1 the caller's NUMA node less the caller's CPU, 2 its first CPU */
     int gate;       /* the replay starts once this is non-zero (OVL_STREAM_SCC=2: after the helper's first pass) */
     int cpu_main;   /* the calling thread's CPU when the replay started */
     int cpu_start, cpu_end;
     double ms;      /* the replay's own duration */
 } ReplayJob;
 
-/* CPUs of the NUMA node holding `cpu` (from sysfs), into `set`; 0 if not found */
-static int node_cpus(int cpu, cpu_set_t* set) {
-    char path[96], buf[4096];
-    for (int node = 0; node < 64; ++node) {
-        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
-        FILE* f = fopen(path, "r");
-        if (!f) continue;
-        const size_t got = fread(buf, 1, sizeof(buf) - 1, f);
-        fclose(f);
-        buf[got] = 0;
-        CPU_ZERO(set);
-        int found = 0;
-        for (char* q = buf; *q && *q != '\n';) {
-            char* e;
-            long lo = strtol(q, &e, 10), hi = lo;
-            if (e == q) break;
-            if (*e == '-') hi = strtol(e + 1, &e, 10);
-            for (long c = lo; c <= hi && c < CPU_SETSIZE; ++c) {
-                CPU_SET((int)c, set);
-                if (c == cpu) found = 1;
-            }
-            q = *e == ',' ? e + 1 : e;
-        }
-        if (found) return 1;
-    }
-    return 0;
-}
-
 static void* replay_main(void* arg) {
     ReplayJob* j = (ReplayJob*)arg;
-    if (j->pin == 1 && j->cpu_main >= 0) {
-        cpu_set_t node, mine, use;
-        if (node_cpus(j->cpu_main, &node) && sched_getaffinity(0, sizeof(mine), &mine) == 0) {
-            CPU_AND(&use, &node, &mine);
-            CPU_CLR(j->cpu_main, &use);
-            if (CPU_COUNT(&use) > 0) sched_setaffinity(0, sizeof(use), &use);
-        }
-    } else if (j->pin == 2) {
-        cpu_set_t one;
-        CPU_ZERO(&one);
-        CPU_SET(sched_getcpu(), &one);
-        sched_setaffinity(0, sizeof(one), &one);
-    }
     while (!__atomic_load_n(&j->gate, __ATOMIC_ACQUIRE)) sched_yield();
     j->cpu_start = sched_getcpu();
     const double t0 = now_ms();
@@ -1080,8 +1038,6 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         Py_ssize_t iw, ie;
         attr_slots(tmpl, kw, ke, &iw, &ie);
         {
-            const char* pin_env = getenv("OVL_STREAM_PIN");
-            job.pin = pin_env ? atoi(pin_env) : 0;
             job.cpu_main = sched_getcpu();
             job.gate = scc_on != 2;
         }
@@ -1214,11 +1170,11 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
         if (trace)
             fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows, %.0f%% edges, %lld inserted) b=%.1f t=%.1f sweeps=%lld scc=%d passes=%d first=%lld "
-                    "replay=%.1f pin=%d cpus main %d/%d replay %d/%d\n", t_setup, t_replay,
+                    "replay=%.1f cpus main %d/%d replay %d/%d\n", t_setup, t_replay,
                     N ? 100.0 * (double)k_at_replay / (double)N : 100.0,
                     E ? 100.0 * (double)dec_at_replay / (double)E : 100.0, (long long)ins_at_replay, t_built, now_ms() - t0, (long long)n_sweeps,
                     scc_on, scc.passes,
-                    (long long)n_from_scc, job.ms, job.pin, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end);
+                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end);
     }
 done:
     if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */

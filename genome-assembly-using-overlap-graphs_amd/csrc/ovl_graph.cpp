@@ -37,12 +37,47 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <vector>
 
 #include "ovl.h"
 
 namespace {
+
+// An array of n trivially-constructible T in anonymous memory aligned to 2 MB and marked for transparent huge
+// pages (madvise; a no-op where THP is off): the replay's edge records are read at random, 45-60 MB at the target
+// point, so with 4 KB pages nearly every yield is a TLB miss as well as a cache miss.  Falls back to the heap.
+template <typename T>
+class HugeArray {
+  public:
+    explicit HugeArray(size_t n) : n_(n) {
+        const size_t align = size_t(2) << 20;
+        bytes_ = ((n * sizeof(T) + align - 1) / align + 1) * align;
+        void* m = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) {
+            heap_.resize(n);
+            p_ = heap_.data();
+            return;
+        }
+        base_ = m;
+        p_ = reinterpret_cast<T*>((reinterpret_cast<uintptr_t>(m) + align - 1) & ~(uintptr_t)(align - 1));
+        (void)madvise(p_, n * sizeof(T), MADV_HUGEPAGE);
+    }
+    ~HugeArray() {
+        if (base_) munmap(base_, bytes_);
+    }
+    HugeArray(const HugeArray&) = delete;
+    HugeArray& operator=(const HugeArray&) = delete;
+    T* data() { return p_; }
+    T& operator[](size_t i) { return p_[i]; }
+
+  private:
+    size_t n_, bytes_ = 0;
+    void* base_ = nullptr;
+    T* p_ = nullptr;
+    std::vector<T> heap_;
+};
 
 // One undo-log record per iterator advance of `node` (its old position).  A yield that reaches a node for the
 // first time also carries that node (`first`; -1 otherwise): its first visit and 'seen' insertion happen at
@@ -155,7 +190,7 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
         int32_t skip;
         WT w;
     };
-    std::vector<Edge> ed((size_t)n_edges + 1);
+    HugeArray<Edge> ed((size_t)n_edges + 1);
     for (int64_t e = 0; e < n_edges; ++e) ed[(size_t)e] = {head[e], 0, (WT)weight[e]};
     ed[(size_t)n_edges] = {0, 0, 0};
     std::vector<uint8_t> alive_own(alive_out ? 0 : (size_t)n_edges, 1), done(n_nodes, 0);  // done = explored |
