@@ -1093,6 +1093,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-extra", action="store_true", help="skip the extra configs and stages")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="N > 1: leave the ranks' CPU affinity alone (default: each rank on its GPU's NUMA node)")
+    ap.add_argument("--numa-bind", action="store_true", help=argparse.SUPPRESS)  # (A/B: bind at N = 1 too)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of all-core CPU-baseline work")
     ap.add_argument("--indel", type=int, default=None, help="indel score (default: the reference's -2**31)")
     ap.add_argument("--band", type=int, default=-1, help="band half-width (-1 = full DP, the reference)")
@@ -1181,7 +1182,7 @@ def main() -> int:
     dev = torch.device("cuda", local)
     backend = os.environ.get("OVL_BENCH_BACKEND") or ("gloo" if shared else "nccl")  # nccl = RCCL on ROCm
     numa = None
-    if world > 1 and not shared and not args.no_numa_bind:
+    if (world > 1 or args.numa_bind) and not shared and not args.no_numa_bind:
         numa = bind_to_gpu_node(dev)  # before the engine, its host pool and any pinned allocation
     os.environ["OVL_BENCH_NUMA_NODE"] = "" if numa is None else str(numa)
     if world > 1 or args.dist_path:
