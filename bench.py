@@ -1092,8 +1092,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra configs and stages")
     ap.add_argument("--no-numa-bind", action="store_true",
-                    help="N > 1: leave the ranks' CPU affinity alone (default: each rank on its GPU's NUMA node)")
-    ap.add_argument("--numa-bind", action="store_true", help=argparse.SUPPRESS)  # (A/B: bind at N = 1 too)
+                    help="leave the CPU affinity alone (default: each process on its GPU's NUMA node)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of all-core CPU-baseline work")
     ap.add_argument("--indel", type=int, default=None, help="indel score (default: the reference's -2**31)")
     ap.add_argument("--band", type=int, default=-1, help="band half-width (-1 = full DP, the reference)")
@@ -1182,7 +1181,9 @@ def main() -> int:
     dev = torch.device("cuda", local)
     backend = os.environ.get("OVL_BENCH_BACKEND") or ("gloo" if shared else "nccl")  # nccl = RCCL on ROCm
     numa = None
-    if (world > 1 or args.numa_bind) and not shared and not args.no_numa_bind:
+    # (N = 1 too: on the 2-socket box the step's host side -- expansion threads, pinned arrays -- runs on whichever
+    # socket the scheduler picks; bound, 0.140-0.149 ms against 0.138-0.169 unbound, tools/gpu_r04_numa.sh)
+    if not shared and not args.no_numa_bind:
         numa = bind_to_gpu_node(dev)  # before the engine, its host pool and any pinned allocation
     os.environ["OVL_BENCH_NUMA_NODE"] = "" if numa is None else str(numa)
     if world > 1 or args.dist_path:
@@ -1248,6 +1249,7 @@ def main() -> int:
                     "packed 2 B/pair chunks expanded by host threads while the next chunk scores, the last "
                     "~20 % stored directly)",
             "parallelism": "1 GPU",
+            "host_numa_node": int(os.environ["OVL_BENCH_NUMA_NODE"]) if os.environ.get("OVL_BENCH_NUMA_NODE") else None,
             "kernel": w.kernel,
             "scoring": {"match": 10, "mismatch": -1, "indel": w.indel, "band": w.band},
         },
