@@ -94,6 +94,7 @@ struct Knobs {
                                   // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
                                   // instead of uniform_kernel reading b16 + tile deltas in place (tests)
+    int32_t lat_tiles = 8;        // OVL_LAT_TILES (A/B, round 4): uniform_kernel latency mode up to this many tiles per CU
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -473,7 +474,7 @@ int32_t ungapped_rs_log2(const Dev* c, int64_t n_pairs) {
     int32_t rs_log2 = 0;
     const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
     while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
-    if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * 8) ? 1 : 0;
+    if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * c->k.lat_tiles) ? 1 : 0;
     return rs_log2;
 }
 
@@ -697,6 +698,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
 
     if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_LAT_TILES")) k.lat_tiles = std::max(0, atoi(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
