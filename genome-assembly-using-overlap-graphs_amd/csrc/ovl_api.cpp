@@ -94,7 +94,6 @@ struct Knobs {
                                   // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
                                   // instead of uniform_kernel reading b16 + tile deltas in place (tests)
-    int32_t lat_tiles = 8;        // OVL_LAT_TILES (A/B, round 4): uniform_kernel latency mode up to this many tiles per CU
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -110,6 +109,13 @@ constexpr int64_t kBlocksPerCu = 32;
 // profiles/r04_band_lane_ab.json, ms one lane / two lanes): 40: 6.07 / 6.99, 48: 7.13 / 8.04, 56: 8.29 / 9.09,
 // 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD
 constexpr int32_t kBandLane2Min = 64;
+// uniform_kernel's latency mode (two wavefronts per tile) up to this many 64-pair tiles per CU in a launch: a
+// rank's shard at N = 4 / 8 (0.5 M / 0.25 M pairs) 0.068 -> 0.062 / 0.051 -> 0.047 ms per step, the whole list's
+// 0.87 M-pair chunks unchanged in throughput mode, 64 tiles per CU (those chunks too) slower: 0.141 -> 0.153 ms
+// (tools/gpu_r04_lat.sh, profiles/r04_lat_mode_ab.json).  Host-encoded lists keep 8: only throughput mode reads
+// them in place.
+constexpr int64_t kLatTiles = 32;
+constexpr int64_t kLatTilesIx = 8;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
 // host expansion of packed results: pairs per pool part at least (finer parts than 64 K: the expansion of a
@@ -469,19 +475,21 @@ int ensure_heavy(Dev* c) {
 }
 
 // rs_log2 of an ungapped launch over n pairs: bit shifts split over 1 << rs_log2 lanes (the general kernel),
-// or (uniform kernel, 2 planes) latency mode when rs_log2 > 0
-int32_t ungapped_rs_log2(const Dev* c, int64_t n_pairs) {
+// or (uniform kernel, 2 planes) latency mode when rs_log2 > 0: up to kLatTiles tiles per CU for device lists,
+// up to kLatTilesIx for a host-encoded list (which only throughput mode reads in place)
+int32_t ungapped_rs_log2(const Dev* c, int64_t n_pairs, bool ix = false) {
     int32_t rs_log2 = 0;
     const int64_t want_waves = (int64_t)c->cu_count * 4 * 4;
     while (rs_log2 < 2 && ((n_pairs << rs_log2) + 63) / 64 < want_waves) ++rs_log2;
-    if (c->planes == 2) rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * c->k.lat_tiles) ? 1 : 0;
+    if (c->planes == 2)
+        rs_log2 = ((n_pairs + 63) / 64 <= (int64_t)c->cu_count * (ix ? kLatTilesIx : kLatTiles)) ? 1 : 0;
     return rs_log2;
 }
 
 // An ungapped launch over n pairs runs uniform_kernel in throughput mode, the one that can read a
 // host-encoded pair list in place (uniform_kernel IX)
 bool ix_launch(const Dev* c, int64_t n_pairs) {
-    return c->planes == 2 && c->lmax > 0 && c->wmax >= 1 && c->wmax <= 8 && ungapped_rs_log2(c, n_pairs) == 0;
+    return c->planes == 2 && c->lmax > 0 && c->wmax >= 1 && c->wmax <= 8 && ungapped_rs_log2(c, n_pairs, true) == 0;
 }
 
 int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t* d_b, int64_t n_pairs,
@@ -521,7 +529,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         // general kernel: split a pair's bit shifts over 1, 2 or 4 lanes until the grid
         // has enough wavefronts.  Uniform kernel: latency mode (two wavefronts per tile,
         // side pairs beside the sweep) when there is about one tile per wavefront slot.
-        g.rs_log2 = ungapped_rs_log2(c, n_pairs);
+        g.rs_log2 = ungapped_rs_log2(c, n_pairs, c->ix_b16 != nullptr);
         // uniform-length fast path (2 bit planes): pairs of two reads of length lmax;
         // uniform_kernel scores the other pairs through its LDS side ring
         g.lw = c->planes == 2 ? c->lmax : 0;
@@ -698,7 +706,6 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
 
     if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LAT_TILES")) k.lat_tiles = std::max(0, atoi(e));
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
