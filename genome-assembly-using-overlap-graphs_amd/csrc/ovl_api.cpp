@@ -94,7 +94,7 @@ struct Knobs {
                                   // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
                                   // instead of uniform_kernel reading b16 + tile deltas in place (tests)
-    int32_t one_launch = 1;       // OVL_ONE_LAUNCH=0 (A/B, round 4): a launch per chunk instead of one for the call
+    int32_t one_launch = 0;       // OVL_ONE_LAUNCH=1 (A/B, round 4): one launch for the call's chunks (sink 3)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six

@@ -563,9 +563,9 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
 # ----------------------------------------------------------------------------- one launch over the chunks
 @pytest.mark.parametrize("one", ["1", "0"])
 def test_one_launch_over_the_chunks(oracle_mod, one):
-    """The resident target list into pinned arrays: by default one uniform_kernel launch scores every chunk
-    (sink 3), the host expanding each packed chunk when the launch's completion flag for it lands; with
-    OVL_ONE_LAUNCH=0 a launch per chunk.  Exact call after call (the flags carry a per-call sequence number), with
+    """The resident target list into pinned arrays: with OVL_ONE_LAUNCH=1 one uniform_kernel launch scores every
+    chunk (sink 3), the host expanding each packed chunk when the launch's completion flag for it lands; by
+    default (0) a launch per chunk.  Exact call after call (the flags carry a per-call sequence number), with
     timing on and off, and for a direct share of 0 (every chunk packed)."""
     from ovlgraph.candidates import dedup_reads
     from ovlgraph.hostmem import pinned_empty
