@@ -1113,18 +1113,25 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     }
 #endif
     if constexpr (OM == 3) {
-        // every result this wave stored (its tiles and their side pairs) is visible to the host before its
-        // tiles count; the wave that completes a chunk's count publishes the call's sequence number for it
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        // every result this wave stored (its tiles and their side pairs) is complete before its tiles count:
+        // the packed staging is fine-grained host memory, which the L2 does not hold, so the wave's own store
+        // acknowledgements suffice (a system-scope release per wave -- an L2 write-back each on gfx950 -- made
+        // the launch 0.93 ms); the wave that completes a chunk's count releases at system scope once and
+        // publishes the call's sequence number for it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int32_t cnt[kOvlMaxChunks] = {tcnt0, tcnt1, tcnt2, tcnt3};
         if (lane == 0) {
 #pragma unroll
             for (int c = 0; c < kOvlMaxChunks; ++c) {
                 if (cnt[c] == 0) continue;
-                const uint32_t before = __hip_atomic_fetch_add(cd.done + c, (uint32_t)cnt[c], __ATOMIC_ACQ_REL,
+                // (system scope: performed at memory, coherent across the XCDs' L2s, which an agent-scope
+                // atomic on gfx950 is not guaranteed to be)
+                const uint32_t before = __hip_atomic_fetch_add(cd.done + c, (uint32_t)cnt[c], __ATOMIC_RELAXED,
                                                                __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((int64_t)before + cnt[c] == cd.tiles[c])
-                    __hip_atomic_store(cd.flags + c, cd.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((int64_t)before + cnt[c] == cd.tiles[c]) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                    __hip_atomic_store(cd.flags + c, cd.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
     }
