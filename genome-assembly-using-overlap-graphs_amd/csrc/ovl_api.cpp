@@ -110,6 +110,9 @@ constexpr int64_t kBlocksPerCu = 32;
 // profiles/r04_band_lane_ab.json, ms one lane / two lanes): 40: 6.07 / 6.99, 48: 7.13 / 8.04, 56: 8.29 / 9.09,
 // 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD
 constexpr int32_t kBandLane2Min = 64;
+// sink 3's completion counters (uniform_kernel): per chunk one counter and 64 slot counters, each on its own
+// 64-byte line
+constexpr size_t kChunkDoneBytes = sizeof(uint32_t) * 16 * (kOvlMaxChunks + 64 * kOvlMaxChunks);
 // uniform_kernel's latency mode (two wavefronts per tile) up to this many 64-pair tiles per CU in a launch: a
 // rank's shard at N = 4 / 8 (0.5 M / 0.25 M pairs) 0.068 -> 0.062 / 0.051 -> 0.047 ms per step, the whole list's
 // 0.87 M-pair chunks unchanged in throughput mode, 64 tiles per CU (those chunks too) slower: 0.141 -> 0.153 ms
@@ -810,7 +813,7 @@ hipError_t init_dev(Dev* d) {
     memset(d->chunk_flags, 0, 64);
     e = hipHostGetDevicePointer((void**)&d->chunk_flags_dev, d->chunk_flags, 0);
     if (e != hipSuccess) return e;
-    e = ensure(d->chunk_done, 64);
+    e = ensure(d->chunk_done, kChunkDoneBytes);
     if (e != hipSuccess) return e;
     e = hipHostGetDevicePointer((void**)&d->h_flag_dev, d->h_flag, 0);
     if (e != hipSuccess) return e;
@@ -1380,7 +1383,7 @@ int issue_all(const Call& C, Job& J) {
     }
     cd.done = as<uint32_t>(d->chunk_done);
     cd.flags = d->chunk_flags_dev;
-    HIPCHK(d, hipMemsetAsync(d->chunk_done.p, 0, sizeof(uint32_t) * kOvlMaxChunks, d->stream));
+    HIPCHK(d, hipMemsetAsync(d->chunk_done.p, 0, kChunkDoneBytes, d->stream));
     if (C.timing) {
         HIPCHK(d, hipEventRecord(d->t_ev[0], d->stream));
         d->kev_start = d->k_ev[0];

@@ -934,9 +934,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     // ~2.6x a uniform tile (their ring drains), and one landing in the last round of wavefronts is the
     // launch's tail.  Work item i < heavy_n is heavy tile heavy_ids[i] (ids in list tiles, this launch's
     // tiles start at tile_base); item heavy_n + t is tile t, skipped when it is heavy (done already).
-    const bool hf = !LAT && heavy_ids != nullptr;
+    const bool hf = !LAT && OM != 3 && heavy_ids != nullptr;  // (sink 3: tiles in order, their chunks in turn)
     const int64_t n_items = hf ? n_tiles + heavy_n : n_tiles;
-    int32_t tcnt0 = 0, tcnt1 = 0, tcnt2 = 0, tcnt3 = 0;  // sink 3: this wave's finished tiles per chunk
     for (int64_t base = (int64_t)blockIdx.x * G; base < n_items; base += (int64_t)gridDim.x * G) {
         const int64_t item = base + grp;  // wave-uniform
         int64_t tile = item;
@@ -950,15 +949,6 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         }
         const int64_t p = tile * 64 + lane;
         const bool mine = item < n_items && tile < n_tiles && p < n_pairs;
-        if constexpr (OM == 3) {
-            if (item < n_items && tile < n_tiles) {  // (wave-uniform) one more tile of its chunk for this wave
-                const int c = chunk_of_tile(cd, tile);
-                tcnt0 += c == 0;
-                tcnt1 += c == 1;
-                tcnt2 += c == 2;
-                tcnt3 += c == 3;
-            }
-        }
         int32_t a = 0, b = 0;
         if constexpr (IX) {
             if (mine) {
@@ -1113,22 +1103,32 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     }
 #endif
     if constexpr (OM == 3) {
-        // every result this wave stored (its tiles and their side pairs) is complete before its tiles count:
-        // the packed staging is fine-grained host memory, which the L2 does not hold, so the wave's own store
-        // acknowledgements suffice (a system-scope release per wave -- an L2 write-back each on gfx950 -- made
-        // the launch 0.93 ms); the wave that completes a chunk's count releases at system scope once and
-        // publishes the call's sequence number for it
+        // Every result this wave stored (its tiles and their side pairs) is complete before its tiles count: the
+        // packed staging is fine-grained host memory, which the L2 does not hold, so the wave's own store
+        // acknowledgements suffice (a system-scope release per wave -- an L2 write-back each on gfx950 -- made the
+        // launch 0.93 ms).  Counting is two-level so that no address takes more than a few hundred atomics (one
+        // counter per chunk took every wave's atomic in turn at the memory: 0.37 ms): tile t counts in slot
+        // t % 64 of its chunk (counters a 64-byte line apart), the tile completing a slot counts in the chunk's
+        // counter, and the slot completing the chunk releases at system scope once and publishes the call's
+        // sequence number in the chunk's flag.  (System-scope atomics: performed at memory, coherent across
+        // the XCDs' L2s.)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int32_t cnt[kOvlMaxChunks] = {tcnt0, tcnt1, tcnt2, tcnt3};
         if (lane == 0) {
-#pragma unroll
-            for (int c = 0; c < kOvlMaxChunks; ++c) {
-                if (cnt[c] == 0) continue;
-                // (system scope: performed at memory, coherent across the XCDs' L2s, which an agent-scope
-                // atomic on gfx950 is not guaranteed to be)
-                const uint32_t before = __hip_atomic_fetch_add(cd.done + c, (uint32_t)cnt[c], __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((int64_t)before + cnt[c] == cd.tiles[c]) {
+            for (int64_t base = (int64_t)blockIdx.x * G; base < n_tiles; base += (int64_t)gridDim.x * G) {
+                const int64_t tile = base + grp;  // (the loop's tiles again: in order, heavy-first off)
+                if (tile >= n_tiles) continue;
+                const int c = chunk_of_tile(cd, tile);
+                const int64_t t0 = c ? (cd.pair_end[c - 1] >> 6) : 0, t1 = t0 + cd.tiles[c];
+                const int s_ = (int)(tile & 63);
+                // tiles of [t0, t1) in slot s_: f(t1) - f(t0), f(x) = #{t < x : t % 64 == s_}
+                const int64_t want = (t1 > s_ ? (t1 - s_ + 63) / 64 : 0) - (t0 > s_ ? (t0 - s_ + 63) / 64 : 0);
+                uint32_t* slot = cd.done + 16 * (kOvlMaxChunks + 64 * c + s_);
+                const uint32_t b1 = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((int64_t)b1 + 1 != want) continue;
+                const int64_t slots = cd.tiles[c] < 64 ? cd.tiles[c] : 64;
+                const uint32_t b2 = __hip_atomic_fetch_add(cd.done + 16 * c, 1u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((int64_t)b2 + 1 == slots) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                     __hip_atomic_store(cd.flags + c, cd.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
