@@ -648,19 +648,17 @@ def pair_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 
 SINKS = {0: "int32 results in HBM (copy-engine transfer after)", 1: "int32 results stored into pinned host memory",
-         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)",
-         3: "one launch over the call's chunks: packed 2 B/pair into pinned staging for the first (host threads "
-            "expand each as its completion flag lands), int32 into the pinned arrays for the last"}
+         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)"}
 
 
 def kernel_name(w, sink: int, pairs: int) -> str:
     """The uniform_kernel instantiation a launch of `pairs` pairs with result sink `sink` runs (ovl_plan
     "ungapped", 2 bit planes, int32 keys; latency mode at <= 32 tiles per CU for device lists, ovl_api.cpp
-    kLatTiles; never for sink 3)."""
+    kLatTiles)."""
     if w.kernel != "ungapped":
         return f"{w.kernel} kernel"
     lmax = w.eng.info()["lmax"]
-    lat = sink != 3 and (pairs + 63) // 64 <= 256 * 32
+    lat = (pairs + 63) // 64 <= 256 * 32
     # (the fifth parameter, IX, is true only for host pair lists read in their encoding)
     return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}, false>"
 
@@ -680,11 +678,10 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
     cum = np.zeros(w.hi - w.lo + 1, dtype=np.int64)
     np.cumsum(pair_bytes(lens, w.a[w.lo:w.hi], w.b[w.lo:w.hi]), out=cum[1:])
     w.eng.set_timing(True)
-    runs, links = [], []
+    runs = []
     for _ in range(reps):
         w.step()
         runs.append(w.eng.last_launches())
-        links.append(w.eng.last_transfer()["link_bytes"])
     w.eng.set_timing(False)
     by_sink = {}
     for recs in runs:
@@ -707,8 +704,7 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
         byts = int(np.median(d["bytes"]))
         launches = len(d["ms"]) / reps
         ach = byts / (ms * 1e-3) / 1e9
-        # (sink 3: the call's result bytes over the link, packed and direct; the list itself is resident)
-        link = int(np.median(links)) if sink == 3 else pairs * LINK_BYTES_PER_PAIR.get(sink, 0)
+        link = pairs * LINK_BYTES_PER_PAIR.get(sink, 0)
         table.append({"sink": sink, "what": SINKS.get(sink, "?"), "kernel": kernel_name(w, sink, pairs),
                       "link_bytes_per_launch": link, "link_gbs": link / (ms * 1e-3) / 1e9,
                       "link_frac": link / (ms * 1e-3) / 1e9 / LINK_PEAK_GBS,

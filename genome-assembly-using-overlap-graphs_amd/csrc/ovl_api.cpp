@@ -94,7 +94,6 @@ struct Knobs {
                                   // instead of the compact encoding (encode_chunk; tests)
     int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
                                   // instead of uniform_kernel reading b16 + tile deltas in place (tests)
-    int32_t one_launch = 0;       // OVL_ONE_LAUNCH=1 (A/B, round 4): one launch for the call's chunks (sink 3)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -110,9 +109,6 @@ constexpr int64_t kBlocksPerCu = 32;
 // profiles/r04_band_lane_ab.json, ms one lane / two lanes): 40: 6.07 / 6.99, 48: 7.13 / 8.04, 56: 8.29 / 9.09,
 // 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD
 constexpr int32_t kBandLane2Min = 64;
-// sink 3's completion counters (uniform_kernel): per chunk one counter and 64 slot counters, each on its own
-// 64-byte line
-constexpr size_t kChunkDoneBytes = sizeof(uint32_t) * 16 * (kOvlMaxChunks + 64 * kOvlMaxChunks);
 // uniform_kernel's latency mode (two wavefronts per tile) up to this many 64-pair tiles per CU in a launch: a
 // rank's shard at N = 4 / 8 (0.5 M / 0.25 M pairs) 0.068 -> 0.062 / 0.051 -> 0.047 ms per step, the whole list's
 // 0.87 M-pair chunks unchanged in throughput mode, 64 tiles per CU (those chunks too) slower: 0.141 -> 0.153 ms
@@ -195,10 +191,6 @@ struct Dev {
     uint32_t* cur_flag = nullptr;    // the flag the next launches write: err_flag (device calls) or h_flag_dev
     int32_t out_mode = 0;            // result sink of the next ungapped launches (OvlUngappedArgs::host_out):
                                      // 0 HBM, 1 host-mapped int32 arrays, 2 host-mapped packed uint16
-    uint32_t* chunk_flags = nullptr;      // one launch over a call's chunks (sink 3): host-mapped completion flags
-    uint32_t* chunk_flags_dev = nullptr;  // (kOvlMaxChunks) and their device address; tile counters in chunk_done
-    uint32_t chunk_seq = 0;               // the value a completed chunk's flag takes in the current call
-    OvlChunkDesc chunk_desc{};            // the chunks of the next sink-3 launch
     std::vector<hipEvent_t> t_ev;  // timing: kernel start/end per chunk (recorded on the stream around the launch)
     std::vector<hipEvent_t> k_ev;  // timing: the same recorded by an ungapped launch itself (kernel start / end)
     hipEvent_t kev_start = nullptr, kev_stop = nullptr;  // the next ungapped launch records these (then cleared)
@@ -208,7 +200,6 @@ struct Dev {
     char* cp_dev = nullptr;
     size_t cp_bytes = 0;
     DevBuf cp_hbm;  // the in-place encoding's chunks copied into HBM (same layout as cp_host)
-    DevBuf chunk_done;  // sink 3: finished tiles per chunk
     std::vector<hipEvent_t> dec_ev;
     int64_t cp_link = 0;
     // the next ungapped launch reads its pair list in the host encoding (OvlUngappedArgs::ix_*), or null
@@ -556,7 +547,6 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.key64 = pl.key64 ? 1 : 0;
         g.max_blocks = (int64_t)c->cu_count * kBlocksPerCu;
         g.host_out = c->out_mode;
-        if (g.host_out == 3) g.chunks = c->chunk_desc;
         g.ix_b16 = c->ix_b16;
         g.ix_d8 = c->ix_d8;
         g.ix_base = c->ix_base;
@@ -716,7 +706,6 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
 
     if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_ONE_LAUNCH")) k.one_launch = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -764,13 +753,12 @@ void destroy_dev(Dev* d) {
                       &d->score, &d->end, &d->tb, &d->err_flag, &d->k_pre, &d->k_suf, &d->k_sorted, &d->k_iota,
                       &d->k_order, &d->k_lo, &d->k_hi, &d->k_cnt, &d->k_offs, &d->k_temp, &d->cand_a, &d->cand_b,
                       &d->sh_cum, &d->sh_temp, &d->sh_cuts, &d->l_q, &d->l_r, &d->l_row, &d->l_tb, &d->l_best,
-                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids, &d->cp_hbm, &d->chunk_done})
+                      &d->lane_col, &d->seed_s, &d->seed_e, &d->tile_flags, &d->heavy_ids, &d->cp_hbm})
         release(*b);
     if (d->l_tb_host) (void)hipHostFree(d->l_tb_host);
     free_staging(d->st_in);
     free_staging(d->st_out);
     if (d->h_flag) (void)hipHostFree(d->h_flag);
-    if (d->chunk_flags) (void)hipHostFree(d->chunk_flags);
     if (d->cp_host) (void)hipHostFree(d->cp_host);
     for (hipEvent_t e : d->dec_ev)
         if (e) (void)hipEventDestroy(e);
@@ -808,13 +796,6 @@ hipError_t init_dev(Dev* d) {
     e = hipHostMalloc((void**)&d->h_flag, 64, kHostShared);
     if (e != hipSuccess) return e;
     *d->h_flag = 0;
-    e = hipHostMalloc((void**)&d->chunk_flags, 64, kHostShared);
-    if (e != hipSuccess) return e;
-    memset(d->chunk_flags, 0, 64);
-    e = hipHostGetDevicePointer((void**)&d->chunk_flags_dev, d->chunk_flags, 0);
-    if (e != hipSuccess) return e;
-    e = ensure(d->chunk_done, kChunkDoneBytes);
-    if (e != hipSuccess) return e;
     e = hipHostGetDevicePointer((void**)&d->h_flag_dev, d->h_flag, 0);
     if (e != hipSuccess) return e;
     e = ensure(d->err_flag, 16);
@@ -938,7 +919,6 @@ struct Job {
     int32_t* d_end = nullptr;
     std::vector<uint8_t> ixk;    // C.compact: chunk k's list is read in place by uniform_kernel (encode_chunk)
     std::vector<uint8_t> kexact; // timing: chunk k's kernel recorded its own start / end (k_ev)
-    bool one = false;            // one launch over all the chunks (sink 3; issue_all)
 };
 
 // Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
@@ -1285,24 +1265,7 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int64_t g = J.lo + off;
     const int64_t n = J.cb[(size_t)k + 1] - off;
     const int slot = (int)(k % kSlots);
-    if (J.one) {
-        // the launch's wave that completes chunk k stores the call's sequence number into its flag (after a
-        // system-scope release of every result of the chunk); while polling, the launch's end event tells a
-        // flag that will never come (a failed launch) from one still on its way
-        const volatile uint32_t* f = d->chunk_flags + k;
-        for (uint32_t i = 1; *f != d->chunk_seq; ++i) {
-            _mm_pause();
-            if ((i & 1023) == 0) {
-                const hipError_t q = hipEventQuery(d->ev_last);
-                if (q != hipSuccess && q != hipErrorNotReady) return fail(d, OVL_E_HIP, "scoring launch failed: %s", hipGetErrorString(q));
-                if (q == hipSuccess && *f != d->chunk_seq)
-                    return fail(d, OVL_E_HIP, "chunk %lld of the launch never completed", (long long)k);
-            }
-        }
-        std::atomic_thread_fence(std::memory_order_acquire);
-    } else {
-        HIPCHK(d, wait_event(d, d->ev_k[slot]));
-    }
+    HIPCHK(d, wait_event(d, d->ev_k[slot]));
     if (g_trace) g_trace->mark('w', k);
     struct Drained {
         int64_t k;
@@ -1347,60 +1310,6 @@ struct HostFlag {
     }
 };
 
-// One launch for all of a call's chunks (sink 3): a resident (device) pair list scored in throughput mode into
-// pinned arrays with packed chunks that fit the staging ring.  The chunks' waves share one grid, so the chip stays
-// full across chunk boundaries instead of each chunk's launch ramping up and draining on its own (§6: 3.6 resident
-// waves per SIMD in a chunk's launch against 5.4 in one over the whole list), and the host expands chunk k as soon
-// as its flag says so (drain_chunk).
-bool one_launch_ok(const Call& C, const Job& J) {
-    const Dev* d = J.d;
-    return d->k.one_launch && C.pack && C.out_pinned && !C.h_a && J.nchunks >= 2 && J.nchunks <= kOvlMaxChunks &&
-           J.n_packed <= kSlots && C.plan->kernel == OVL_KERNEL_UNGAPPED && !C.plan->key64 && d->planes == 2 &&
-           d->lmax > 0 && d->wmax >= 1 && d->wmax <= 8 && ungapped_rs_log2(d, J.hi - J.lo) == 0;
-}
-
-int issue_all(const Call& C, Job& J) {
-    Dev* d = J.d;
-    HIPCHK(d, hipSetDevice(d->device));
-    OvlChunkDesc& cd = d->chunk_desc;
-    cd = OvlChunkDesc{};
-    cd.n = (int32_t)J.nchunks;
-    cd.n_packed = (int32_t)J.n_packed;
-    cd.seq = ++d->chunk_seq;
-    if (cd.seq == 0) cd.seq = d->chunk_seq = 1;  // (0 is a flag's value before any call)
-    for (int64_t k = 0; k < J.nchunks; ++k) {
-        const int64_t lo = J.cb[(size_t)k], hi = J.cb[(size_t)k + 1];
-        cd.pair_end[k] = hi;
-        cd.tiles[k] = (hi + 63) / 64 - lo / 64;
-        if (k < J.n_packed) {
-            const size_t so = (size_t)(k % kSlots) * 2 * (size_t)d->st_cap;
-            cd.os[k] = d->st_out_dev + so;
-            cd.oe[k] = d->st_out_dev + so + d->st_cap;
-        } else {
-            cd.os[k] = J.d_score + lo;
-            cd.oe[k] = J.d_end + lo;
-        }
-    }
-    cd.done = as<uint32_t>(d->chunk_done);
-    cd.flags = d->chunk_flags_dev;
-    HIPCHK(d, hipMemsetAsync(d->chunk_done.p, 0, kChunkDoneBytes, d->stream));
-    if (C.timing) {
-        HIPCHK(d, hipEventRecord(d->t_ev[0], d->stream));
-        d->kev_start = d->k_ev[0];
-        d->kev_stop = d->k_ev[1];
-    }
-    d->out_mode = 3;
-    const int rc = launch_score(d, *C.plan, J.dev_a + J.lo, J.dev_b + J.lo, J.hi - J.lo, C.match, C.mismatch,
-                                C.indel, cd.os[0], cd.oe[0], d->stream);
-    if (C.timing) J.kexact[0] = d->kev_start == nullptr;
-    d->kev_start = d->kev_stop = nullptr;
-    d->out_mode = 1;
-    if (rc != OVL_OK) return rc;
-    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[1], d->stream));
-    HIPCHK(d, hipEventRecord(d->ev_last, d->stream));  // (the launch's end: pack_share, and drain_chunk's check)
-    return OVL_OK;
-}
-
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
     PipeTrace trace;
@@ -1414,17 +1323,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         if ((rc = setup_job(C, J)) != OVL_OK) return rc;
     trace.mark('s', 0);
     int64_t maxch = 0;
-    for (Job& J : jobs) {
-        J.one = one_launch_ok(C, J);
-        if (J.one) {
-            if ((rc = issue_all(C, J)) != OVL_OK) {
-                quiesce(jobs);
-                return rc;
-            }
-            trace.mark('i', 0);
-        }
-        maxch = std::max(maxch, J.nchunks);
-    }
+    for (const Job& J : jobs) maxch = std::max(maxch, J.nchunks);
     if (C.compact)
         for (Job& J : jobs)
             if (J.nchunks > 0 && (rc = encode_chunk(C, J, 0)) != OVL_OK) {
@@ -1434,10 +1333,6 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
         for (Job& J : jobs) {
             if (k >= J.nchunks) continue;
-            if (J.one) {  // (issued already: drain its packed chunks in order)
-                if (k < J.n_packed && (rc = drain_chunk(C, J, k)) != OVL_OK) break;
-                continue;
-            }
             const auto issue = [&]() -> int {
                 const int r = issue_chunk(C, J, k);
                 trace.mark('i', k);
@@ -1454,7 +1349,6 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     }
     for (Job& J : jobs) {
         if (rc != OVL_OK) break;
-        if (J.one) continue;
         for (int64_t k = std::max<int64_t>(0, J.nchunks - (kSlots - 1)); k < J.nchunks; ++k)
             if (chunk_staged(C, J, k) && (rc = drain_chunk(C, J, k)) != OVL_OK) break;
     }
@@ -1495,13 +1389,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
             *d->h_flag = 0;
             rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
         }
-        if (C.timing && J.one) {  // one launch for every chunk: sink 3
-            float ms = 0.f;
-            const hipEvent_t* ev = J.kexact[0] ? &d->k_ev[0] : &d->t_ev[0];
-            if (hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess) ms = 0.f;
-            c->t_launches.push_back({d->device, 3, J.hi - J.lo, (double)ms});
-            kms = std::max(kms, (double)ms);
-        } else if (C.timing) {
+        if (C.timing) {
             double s = 0.0;
             for (int64_t k = 0; k < J.nchunks; ++k) {
                 float ms = 0.f;

@@ -10,26 +10,6 @@ __device__ __forceinline__ void ovl_flag_error(uint32_t* flag) {
     __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One launch over all the pipeline chunks of a host-array call (uniform_kernel, result sink 3): chunk c holds the
-// launch's pairs [c ? pair_end[c - 1] : 0, pair_end[c]) (boundaries at multiples of 64); chunks below n_packed
-// store packed results into their staging slot (os / oe as sink 2), the others int32 into the caller's pinned
-// arrays (sink 1), both indexed by the chunk-local pair.  A wavefront adds the tiles it has finished of chunk c to
-// done[c] (device memory, zeroed before the launch) after a system-scope release, and the one that completes the
-// chunk stores seq into flags[c] (host memory): the host expands chunk c once it reads seq there, while the same
-// launch goes on with the next chunks.
-constexpr int kOvlMaxChunks = 4;
-struct OvlChunkDesc {
-    int32_t n;
-    int32_t n_packed;
-    uint32_t seq;
-    int64_t pair_end[kOvlMaxChunks];
-    int64_t tiles[kOvlMaxChunks];
-    int32_t* os[kOvlMaxChunks];
-    int32_t* oe[kOvlMaxChunks];
-    uint32_t* done;
-    uint32_t* flags;
-};
-
 struct OvlUngappedArgs {
     const uint32_t* sfx;
     const uint32_t* pfx;
@@ -60,9 +40,7 @@ struct OvlUngappedArgs {
                              // copy engine moves it into HBM on the second stream, where the kernel reads it
     int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
                          // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
-                         // out_score as uint16, the score of the few pairs that need it in out_end; 3 per chunk
-                         // (chunks)
-    OvlChunkDesc chunks; // host_out 3: the call's chunks (one launch for all of them)
+                         // out_score as uint16, the score of the few pairs that need it in out_end
     hipEvent_t ev_start; // non-null (timing): uniform_kernel's launch records these at the kernel's own start and
     hipEvent_t ev_stop;  // end (hipExtLaunchKernelGGL), without the dispatch wait that stream events include
 };

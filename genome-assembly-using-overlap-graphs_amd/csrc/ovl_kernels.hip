@@ -107,36 +107,6 @@ __device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
     return match != mismatch ? 1.0f / (float)(match - mismatch) : 0.f;
 }
 
-// sink 3 (OvlChunkDesc): pair p of the launch into its chunk's sink, chunk-local (the chunk picked by selects over
-// the unrolled boundaries: no dynamic index into the kernel arguments)
-__device__ __forceinline__ void put_chunked(const OvlChunkDesc& cd, int64_t p, int32_t sc, int32_t en, int32_t n,
-                                            int32_t match, float inv) {
-    int32_t* os = cd.os[0];
-    int32_t* oe = cd.oe[0];
-    int64_t base = 0;
-    bool packed = cd.n_packed > 0;
-#pragma unroll
-    for (int c = 1; c < kOvlMaxChunks; ++c) {
-        if (c < cd.n && p >= cd.pair_end[c - 1]) {
-            os = cd.os[c];
-            oe = cd.oe[c];
-            base = cd.pair_end[c - 1];
-            packed = c < cd.n_packed;
-        }
-    }
-    if (packed) put_pair<2>(os, oe, p - base, sc, en, n, match, inv);
-    else put_pair<1>(os, oe, p - base, sc, en, n, match, inv);
-}
-
-// the chunk of a launch's tile t (wave-uniform)
-__device__ __forceinline__ int chunk_of_tile(const OvlChunkDesc& cd, int64_t t) {
-    int c = 0;
-#pragma unroll
-    for (int k = 1; k < kOvlMaxChunks; ++k)
-        if (k < cd.n && t * 64 >= cd.pair_end[k - 1]) c = k;
-    return c;
-}
-
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
 // would otherwise sum a block's word counts with an extra v_add3)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t v, uint32_t acc) {
@@ -834,7 +804,7 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
                                              const int32_t* __restrict__ len, int32_t n_reads, int r0,
                                              int rs_log2, int32_t jbound, int32_t match, int32_t mismatch,
                                              int32_t* __restrict__ out_score, int32_t* __restrict__ out_end,
-                                             uint32_t* __restrict__ err_flag, const OvlChunkDesc* cd = nullptr) {
+                                             uint32_t* __restrict__ err_flag) {
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = (W * P + 3) & ~3;
     bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
@@ -849,8 +819,7 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
     if (mine && r0 == 0) {
         int32_t sc, en;
         Key<KM>::decode(full, sc, en);
-        if constexpr (OM == 3) put_chunked(*cd, p, ok ? sc : -1, ok ? en : -1, n, match, pack_inv(match, mismatch));
-        else put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, n, match, pack_inv(match, mismatch));
+        put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, n, match, pack_inv(match, mismatch));
     }
 }
 
@@ -882,8 +851,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag,
     const int32_t* __restrict__ heavy_ids, const uint8_t* __restrict__ tile_flags, int32_t heavy_n,
     int64_t tile_base, const uint16_t* __restrict__ ix_b16, const uint8_t* __restrict__ ix_d8,
-    const int32_t* __restrict__ ix_base, const OvlChunkDesc cd) {
-    static_assert(OM != 3 || (!LAT && KM == 0), "sink 3: throughput mode, int32 keys");
+    const int32_t* __restrict__ ix_base) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
     constexpr int SROW = (W * P + 3) & ~3;
@@ -917,7 +885,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         int4 e = make_int4(0, 0, 0, 0);
         if (mine) e = ring[(head + slot) & (RING - 1)];
         general_unit<P, W, KM, OM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
-                                     mismatch, out_score, out_end, err_flag, &cd);
+                                     mismatch, out_score, out_end, err_flag);
         head += count;
     };
 #ifdef OVL_TRACE
@@ -934,7 +902,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     // ~2.6x a uniform tile (their ring drains), and one landing in the last round of wavefronts is the
     // launch's tail.  Work item i < heavy_n is heavy tile heavy_ids[i] (ids in list tiles, this launch's
     // tiles start at tile_base); item heavy_n + t is tile t, skipped when it is heavy (done already).
-    const bool hf = !LAT && OM != 3 && heavy_ids != nullptr;  // (sink 3: tiles in order, their chunks in turn)
+    const bool hf = !LAT && heavy_ids != nullptr;
     const int64_t n_items = hf ? n_tiles + heavy_n : n_tiles;
     for (int64_t base = (int64_t)blockIdx.x * G; base < n_items; base += (int64_t)gridDim.x * G) {
         const int64_t item = base + grp;  // wave-uniform
@@ -1085,8 +1053,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
-            if constexpr (OM == 3) put_chunked(cd, p, ok ? sc : -1, ok ? en : -1, na, match, pack_inv(match, mismatch));
-            else put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, na, match, pack_inv(match, mismatch));
+            put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, na, match, pack_inv(match, mismatch));
         }
         OVL_TR_CLOCK(4, (uint32_t)best);
 #ifndef OVL_ABLATE_DRAIN
@@ -1102,39 +1069,6 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         if (tail > head) drain(tail - head);
     }
 #endif
-    if constexpr (OM == 3) {
-        // Every result this wave stored (its tiles and their side pairs) is complete before its tiles count: the
-        // packed staging is fine-grained host memory, which the L2 does not hold, so the wave's own store
-        // acknowledgements suffice (a system-scope release per wave -- an L2 write-back each on gfx950 -- made the
-        // launch 0.93 ms).  Counting is two-level so that no address takes more than a few hundred atomics (one
-        // counter per chunk took every wave's atomic in turn at the memory: 0.37 ms): tile t counts in slot
-        // t % 64 of its chunk (counters a 64-byte line apart), the tile completing a slot counts in the chunk's
-        // counter, and the slot completing the chunk releases at system scope once and publishes the call's
-        // sequence number in the chunk's flag.  (System-scope atomics: performed at memory, coherent across
-        // the XCDs' L2s.)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-            for (int64_t base = (int64_t)blockIdx.x * G; base < n_tiles; base += (int64_t)gridDim.x * G) {
-                const int64_t tile = base + grp;  // (the loop's tiles again: in order, heavy-first off)
-                if (tile >= n_tiles) continue;
-                const int c = chunk_of_tile(cd, tile);
-                const int64_t t0 = c ? (cd.pair_end[c - 1] >> 6) : 0, t1 = t0 + cd.tiles[c];
-                const int s_ = (int)(tile & 63);
-                // tiles of [t0, t1) in slot s_: f(t1) - f(t0), f(x) = #{t < x : t % 64 == s_}
-                const int64_t want = (t1 > s_ ? (t1 - s_ + 63) / 64 : 0) - (t0 > s_ ? (t0 - s_ + 63) / 64 : 0);
-                uint32_t* slot = cd.done + 16 * (kOvlMaxChunks + 64 * c + s_);
-                const uint32_t b1 = __hip_atomic_fetch_add(slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((int64_t)b1 + 1 != want) continue;
-                const int64_t slots = cd.tiles[c] < 64 ? cd.tiles[c] : 64;
-                const uint32_t b2 = __hip_atomic_fetch_add(cd.done + 16 * c, 1u, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((int64_t)b2 + 1 == slots) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                    __hip_atomic_store(cd.flags + c, cd.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-            }
-        }
-    }
 }
 
 // General kernel: any lengths <= 32W and P bit planes (used when the read set
@@ -1661,13 +1595,12 @@ static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStrea
         hipExtLaunchKernelGGL(uniform_kernel<W, KM, LAT, OM, IX>, dim3(blocks), dim3(256), 0, stream, g.ev_start,
                               g.ev_stop, 0, g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full,
                               g.match, g.mismatch, g.out_score, g.out_end, g.err_flag, g.heavy_ids, g.tile_flags,
-                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base, g.chunks);
+                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
         return;
     }
     uniform_kernel<W, KM, LAT, OM, IX><<<blocks, 256, 0, stream>>>(
         g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full, g.match, g.mismatch, g.out_score,
-        g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base,
-        g.chunks);
+        g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
 }
 
 template <int W, int KM, bool LAT>
@@ -1692,12 +1625,6 @@ static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStrea
         case 2:
             if constexpr (KM == 0) {  // packed results: int32 keys only (the host asks for them only then)
                 launch_uniform_4<W, KM, LAT, 2>(g, blocks, stream);
-                return true;
-            }
-            return false;
-        case 3:
-            if constexpr (KM == 0 && !LAT) {  // one launch over the call's chunks
-                launch_uniform_4<W, KM, LAT, 3>(g, blocks, stream);
                 return true;
             }
             return false;
@@ -1801,9 +1728,6 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->host_out >= 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
-    if (g->host_out == 3 && (g->rs_log2 > 0 || g->ix_b16 || g->chunks.n < 1 || g->chunks.n > kOvlMaxChunks ||
-                             g->chunks.pair_end[g->chunks.n - 1] != g->n_pairs || !g->chunks.done || !g->chunks.flags))
-        return hipErrorInvalidValue;  // one launch over the chunks: throughput mode, device or host int32 lists
     if (g->ix_b16 && (g->lw <= 0 || g->key64 || g->rs_log2 > 0 || g->heavy_ids || !g->ix_d8 || !g->ix_base))
         return hipErrorInvalidValue;  // host-encoded lists: uniform throughput mode only
     if (g->lw > 0) {

@@ -137,8 +137,7 @@ class OverlapEngine:
 
     def last_launches(self) -> List[Dict[str, float]]:
         """The scoring launches of the last host-array call made with timing on (ovl_last_launches):
-        [{device, sink (0 HBM, 1 int32 into host memory, 2 packed into host staging, 3 one launch over the
-        call's packed and direct chunks), pairs, ms}]."""
+        [{device, sink (0 HBM, 1 int32 into host memory, 2 packed into host staging), pairs, ms}]."""
         n = ctypes.c_int32()
         check(self._L.ovl_last_launches(self._ctx, 0, None, None, None, None, ctypes.byref(n)), self._ctx)
         k = n.value

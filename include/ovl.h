@@ -100,9 +100,9 @@ int ovl_set_timing(ovl_ctx* ctx, int32_t on);
 int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 /* The scoring launches of the last host-array call made with timing on, in issue order: *out_n = count;
  * entry i < cap gives the device ordinal, the result sink (1 int32 stored into host memory; 2 packed 2 B/pair
- * into host staging, expanded by host threads; 3 one launch over all of the call's chunks, packed and int32;
- * 0, HBM, only in ovl_score_device), the pairs and the launch's duration in ms (HIP events recorded by the
- * kernel's own launch for ungapped chunks, else on its stream).  Any output pointer may be NULL. */
+ * into host staging, expanded by host threads; 0, HBM, only in ovl_score_device), the pairs and the launch's
+ * duration in ms (HIP events recorded by the kernel's own launch for ungapped chunks, else on its stream).
+ * Any output pointer may be NULL. */
 int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs, double* ms,
                       int32_t* out_n);
 /* Link traffic of the last host-array scoring call (always recorded): link_bytes = pair-list bytes the

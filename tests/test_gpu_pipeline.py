@@ -560,42 +560,6 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
     np.testing.assert_array_equal(le[idx], re_)
 
 
-# ----------------------------------------------------------------------------- one launch over the chunks
-@pytest.mark.parametrize("one", ["1", "0"])
-def test_one_launch_over_the_chunks(oracle_mod, one):
-    """The resident target list into pinned arrays: with OVL_ONE_LAUNCH=1 one uniform_kernel launch scores every
-    chunk (sink 3), the host expanding each packed chunk when the launch's completion flag for it lands; by
-    default (0) a launch per chunk.  Exact call after call (the flags carry a per-call sequence number), with
-    timing on and off, and for a direct share of 0 (every chunk packed)."""
-    from ovlgraph.candidates import dedup_reads
-    from ovlgraph.hostmem import pinned_empty
-    from ovlgraph.reads import config_reads
-    reads, _ = dedup_reads(config_reads("target", seed=0))
-    for env in ({"OVL_ONE_LAUNCH": one}, {"OVL_ONE_LAUNCH": one, "OVL_PACK_DIRECT_PCT": "0"}):
-        eng = _engine_env(env)
-        try:
-            eng.set_reads(reads)
-            a, b = eng.candidates(5)
-            ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
-            n = a.shape[0]
-            out = (pinned_empty(n), pinned_empty(n))
-            for it in range(8):
-                out[0][:] = -7
-                out[1][:] = -7
-                eng.set_timing(it % 2 == 1)
-                eng.score_candidates(out=out)
-                np.testing.assert_array_equal(out[0], ref_s, err_msg=f"{env} call {it}")
-                np.testing.assert_array_equal(out[1], ref_e, err_msg=f"{env} call {it}")
-                if it % 2 == 1:
-                    sinks = [r["sink"] for r in eng.last_launches()]
-                    assert (sinks == [3]) if one == "1" else (3 not in sinks and len(sinks) >= 2), sinks
-                    assert sum(r["pairs"] for r in eng.last_launches()) == n
-            x = eng.last_transfer()
-            assert x["link_bytes"] == 2 * x["packed_pairs"] + 8 * (n - x["packed_pairs"]), x
-        finally:
-            eng.close()
-
-
 # ----------------------------------------------------------------------------- the step's transport
 @pytest.mark.parametrize("cfg", ["target", "cfg3"])
 def test_step_transport_vs_oracle(oracle_mod, cfg):

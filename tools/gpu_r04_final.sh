@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, end of round on one box: every GPU test, smoke, the default bench line (N = 1, CPU baseline), the N = 2
-# rehearsal, the one-launch A/B and the target profile (kernel trace + PMC) of the final tree
+# rehearsal and the target profile (kernel trace + PMC) of the final tree
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=${1:-r04z}
@@ -18,7 +18,5 @@ echo "bench ok"
 timeout -k 10 500 python -u bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/n2.json 2> $OUT/n2.err \
   || { echo "n2 failed"; tail -30 $OUT/n2.err; exit 1; }
 echo "n2 ok"
-SHARD_AB_SETTINGS="one=;per_chunk=OVL_ONE_LAUNCH:0" SHARD_AB_NS=1,2,4,8 timeout -k 10 400 python -u tools/shard_step_ab.py 5 30 > $OUT/one_ab.json 2> $OUT/one_ab.err || { echo "one ab failed"; tail -30 $OUT/one_ab.err; exit 1; }
-echo "one ab ok"
 bash tools/gpu_r04_profile.sh target ${TAG}_target || exit 1
 echo "all ok"
