@@ -6,9 +6,10 @@
 // storing int32 results into other pinned memory at the same time (as the step's direct chunk does).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I genome-assembly-using-overlap-graphs_amd/csrc \
 //     tools/expand_probe.hip -o genome-assembly-using-overlap-graphs_amd/build/expand_probe -lpthread
-//   expand_probe [reps [numa node]]
+//   expand_probe [reps [numa node, -2: the GPU's own]]
 #include <hip/hip_runtime.h>
 
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -56,7 +57,18 @@ static bool bind_node(int node) {
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 30;
-    if (argc > 2 && atoi(argv[2]) >= 0) printf("bind to node %d: %s\n", atoi(argv[2]), bind_node(atoi(argv[2])) ? "ok" : "failed");
+    int node = argc > 2 ? atoi(argv[2]) : -1;
+    if (node == -2) {  // the visible GPU's node, from its PCI address
+        char bus[64] = {0}, path[160];
+        CK(hipDeviceGetPCIBusId(bus, sizeof(bus), 0));
+        for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+        snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+        FILE* fh = fopen(path, "r");
+        if (!fh || fscanf(fh, "%d", &node) != 1) node = -1;
+        if (fh) fclose(fh);
+        printf("gpu %s node %d\n", bus, node);
+    }
+    if (node >= 0) printf("bind to node %d: %s\n", node, bind_node(node) ? "ok" : "failed");
     const size_t n = 857408, n_direct = 360000;
     const ovl_expand::Fn f = ovl_expand::pick(nullptr);
     CopyPool& pool = CopyPool::get();

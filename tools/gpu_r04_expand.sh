@@ -4,12 +4,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/${1:-r04x}
 mkdir -p $OUT
-NODE=$(python3 -c "
-import glob
-for p in glob.glob('/sys/class/drm/card*/device/numa_node'):
-    v = open(p).read().strip()
-    if v not in ('', '-1'): print(v); break
-else: print(-1)")
+# the visible GPU's node from its PCI address (the probe's "-2"); the first /sys/class/drm card, which this script
+# read before, can be another GPU of the host on another node
+NODE=$(genome-assembly-using-overlap-graphs_amd/build/expand_probe 0 -2 | sed -n 's/^gpu .* node \(-\?[0-9]*\)$/\1/p')
 echo "gpu node $NODE"
 B=genome-assembly-using-overlap-graphs_amd/build/expand_probe
 timeout -k 10 120 $B 30 -1 > $OUT/unbound.txt 2>&1 || { echo "unbound failed"; cat $OUT/unbound.txt; exit 1; }
