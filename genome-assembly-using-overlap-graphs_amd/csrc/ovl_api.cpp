@@ -107,7 +107,8 @@ constexpr int64_t kLaneMinPairs = 65536;
 constexpr int64_t kBlocksPerCu = 32;
 // band knob: two lanes per pair (band_lane2_kernel) from this half-width.  Measured at cfg5 (tools/band_ab.py,
 // profiles/r04_band_lane_ab.json, ms one lane / two lanes): 40: 6.07 / 6.99, 48: 7.13 / 8.04, 56: 8.29 / 9.09,
-// 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD
+// 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD.  With
+// the row table built once per row (profiles/r04_band_table_ab.json): 48: 6.60 / 7.59, 64: 10.52 / 9.63
 constexpr int32_t kBandLane2Min = 64;
 // uniform_kernel's latency mode (two wavefronts per tile) up to this many 64-pair tiles per CU in a launch: a
 // rank's shard at N = 4 / 8 (0.5 M / 0.25 M pairs) 0.068 -> 0.062 / 0.051 -> 0.047 ms per step, the whole list's

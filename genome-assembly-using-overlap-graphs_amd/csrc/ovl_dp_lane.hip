@@ -354,9 +354,10 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
 // oracle -- in G = dp - indel*(i+j) units (s2 = s - 2*indel).
 //
 // Scores: the t codes of the row's window sit as bytes in NBW words (byte k = t[j_k - 1]) and slide
-// down one byte per row; the row's profile is P = perm(TBL, T ^ x) -- byte (x ^ t) of an 8-byte
-// table: 0 -> match, 1..3 -> mismatch, 4..7 -> the pad code of positions left of t (s2 = -2*indel,
-// i.e. s = 0, which keeps dp = 0 for every j <= 0 cell: column 0 and the band cells left of it).
+// down one byte per row; the row's profile is P = perm(TBL_x, T) -- byte t of the row's 8-byte table:
+// bytes 0..3 mismatch with the match at byte x (built once per row: tbl_mm ^ (tbl_dm << 8x)), byte 4 the
+// pad code of positions left of t (s2 = -2*indel, i.e. s = 0, which keeps dp = 0 for every j <= 0 cell:
+// column 0 and the band cells left of it).  (Round 4 took the per-word x ^ t out of the cell loop.)
 // Virtual leading rows (end-aligned rows, i <= 0) use s2 = -indel, which maps row 0's G pattern
 // (-indel * j, diagonals shifting one column per row) onto itself, edge cells included.
 //
@@ -388,8 +389,9 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
     const uint32_t b_ma = (uint32_t)(match - 2 * g) & 0xFFu;
     const uint32_t b_mm = (uint32_t)(mismatch - 2 * g) & 0xFFu;
     const uint32_t b_pad = (uint32_t)(-2 * g) & 0xFFu;
-    const uint32_t tbl_lo = b_ma | (b_mm << 8) | (b_mm << 16) | (b_mm << 24);  // x ^ t = 0..3
-    const uint32_t tbl_hi = b_pad * 0x01010101u;                             // x ^ t = 4..7
+    const uint32_t tbl_mm = b_mm * 0x01010101u;  // the row table's bytes t = 0..3 before byte x takes the match
+    const uint32_t tbl_dm = b_ma ^ b_mm;
+    const uint32_t tbl_hi = b_pad * 0x01010101u;  // bytes 4..7: the pad code
     const uint32_t p_virt = ((uint32_t)(-g) & 0xFFu) * 0x01010101u;
     for (int64_t tile = wslot; tile < ntiles; tile += nslots) {
         const int64_t p = tile * 64 + lane;
@@ -468,16 +470,20 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
                 tnew = __builtin_amdgcn_ubfe(T0, r, 1) | (__builtin_amdgcn_ubfe(T1, r, 1) << 1);
                 tnew = it + ub < 0 ? PAD : tnew;
             }
-            const uint32_t x4 = __builtin_amdgcn_perm(0u, x, 0u);  // x in every byte
+            // the row's 8-byte table (byte t = s2(x, t); virtual rows: s2 = -indel everywhere), built once per
+            // row, so a profile word is one perm of it by the window word
+            uint32_t tlo = tbl_mm ^ (tbl_dm << (8 * x)), thi = tbl_hi;
+            if constexpr (MASKED) {
+                const bool virt = it < sk;
+                tlo = virt ? p_virt : tlo;
+                thi = virt ? p_virt : thi;
+            }
             // the profile word of cells 4w..4w+3, built just before its cells (one live word, not NBW: band 64
             // keeps 129 cells and 33 window words in registers)
             uint32_t P = 0;
 #pragma unroll
             for (int k = 0; k < NB; ++k) {
-                if ((k & 3) == 0) {
-                    P = __builtin_amdgcn_perm(tbl_hi, tbl_lo, T[k >> 2] ^ x4);
-                    if constexpr (MASKED) P = it < sk ? p_virt : P;
-                }
+                if ((k & 3) == 0) P = __builtin_amdgcn_perm(thi, tlo, T[k >> 2]);
                 const int32_t d = V[k] + (int32_t)(int8_t)(uint8_t)(P >> (8 * (k & 3)));
                 if constexpr (NB == 1) V[k] = d;
                 else if (k == 0) V[k] = max(d, V[k + 1]);
@@ -585,8 +591,9 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
     const uint32_t b_ma = (uint32_t)(match - 2 * g) & 0xFFu;
     const uint32_t b_mm = (uint32_t)(mismatch - 2 * g) & 0xFFu;
     const uint32_t b_pad = (uint32_t)(-2 * g) & 0xFFu;
-    const uint32_t tbl_lo = b_ma | (b_mm << 8) | (b_mm << 16) | (b_mm << 24);  // x ^ t = 0..3
-    const uint32_t tbl_hi = b_pad * 0x01010101u;                             // x ^ t = 4..7
+    const uint32_t tbl_mm = b_mm * 0x01010101u;  // the row table's bytes t = 0..3 before byte x takes the match
+    const uint32_t tbl_dm = b_ma ^ b_mm;
+    const uint32_t tbl_hi = b_pad * 0x01010101u;  // bytes 4..7: the pad code
     const uint32_t p_virt = ((uint32_t)(-g) & 0xFFu) * 0x01010101u;
     const int32_t kbase = h ? H - 1 : -1;  // diagonal of local cell 0
     // the partner lane's value (lanes 2q <-> 2q+1)
@@ -669,7 +676,12 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
             const uint32_t tnew = h ? tn_prev : tn_c;
             x_prev = x_c;
             tn_prev = tn_c;
-            const uint32_t x4 = __builtin_amdgcn_perm(0u, x, 0u);  // x in every byte
+            uint32_t tlo = tbl_mm ^ (tbl_dm << (8 * x)), thi = tbl_hi;  // the row's table (band_lane_kernel)
+            if constexpr (MASKED) {
+                const bool virt = it < sk;
+                tlo = virt ? p_virt : tlo;
+                thi = virt ? p_virt : thi;
+            }
             // left of local cell 0: lane 1 takes lane 0's last cell of iteration t - 1 (finished last step)
             const int32_t carry = swap(V[H - 1]);
             int32_t left = h ? carry : NEG;
@@ -677,10 +689,7 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
             uint32_t P = 0;
 #pragma unroll
             for (int j = 0; j < H; ++j) {
-                if ((j & 3) == 0) {
-                    P = __builtin_amdgcn_perm(tbl_hi, tbl_lo, T[j >> 2] ^ x4);
-                    if constexpr (MASKED) P = it < sk ? p_virt : P;
-                }
+                if ((j & 3) == 0) P = __builtin_amdgcn_perm(thi, tlo, T[j >> 2]);
                 const int32_t d = V[j] + (int32_t)(int8_t)(uint8_t)(P >> (8 * (j & 3)));
                 const int32_t up = j + 1 < H ? V[j + 1] : upin;
                 int32_t v = max(max(d, up), left);
