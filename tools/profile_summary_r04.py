@@ -35,7 +35,7 @@ def short(name):
 def main():
     run, rnd, cfg = sys.argv[1], sys.argv[2], sys.argv[3]
     shard = sys.argv[4] if len(sys.argv) > 4 else None  # e.g. shard0of8
-    key = f"{cfg}/{shard}" if shard else cfg
+    workload = f"{cfg}/{shard}" if shard else cfg
     stem = f"{rnd}_{cfg}_{shard}" if shard else f"{rnd}_{cfg}"
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     stats = glob.glob(os.path.join(run, "kt", "**", "*kernel_stats.csv"), recursive=True)[0]
@@ -116,7 +116,7 @@ def main():
     cmd = "bench.py --config %s --steps 20 --warmup 5 --no-cpu-baseline --no-extra" % cfg
     if shard:
         cmd += " --shard " + shard.replace("shard", "").replace("of", "/")
-    out = {"workload": key, "headline_kernel": bench["roofline"]["kernel"], "command": cmd,
+    out = {"workload": workload, "headline_kernel": bench["roofline"]["kernel"], "command": cmd,
            "bench_roofline_same_run": bench["roofline"], "kernels": kernels,
            "source": "tools/gpu_r04_profile.sh, tools/profile_summary_r04.py"}
     json.dump(out, open(os.path.join(root, "profiles", f"{stem}_pmc.json"), "w"), indent=1)
