@@ -48,6 +48,22 @@ __device__ __forceinline__ int32_t wave_min(int32_t v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 
+// band kernels, four rows at a time: bits b0..b3 of v4 into bit 0 of bytes 0..3 (the products' terms land on
+// distinct bits, so no carries)
+__device__ __forceinline__ uint32_t spread4(uint32_t v4) { return (v4 * 0x00204081u) & 0x01010101u; }
+
+// rows r0..r0+3 of a 32-row block of two bit planes as bytes (codes 0..3)
+__device__ __forceinline__ uint32_t codes4(uint32_t p0, uint32_t p1, uint32_t r0) {
+    return spread4(__builtin_amdgcn_ubfe(p0, r0, 4)) | (spread4(__builtin_amdgcn_ubfe(p1, r0, 4)) << 1);
+}
+
+// the bytes k of c4 with u0 + k < 0 (t positions left of the read) replaced by the pad code 4
+__device__ __forceinline__ uint32_t pad4(uint32_t c4, int32_t u0) {
+    const int32_t np = min(max(-u0, 0), 4);
+    const uint32_t mask = np >= 4 ? 0xFFFFFFFFu : ((1u << (8 * np)) - 1u);
+    return (c4 & ~mask) | (0x04040404u & mask);
+}
+
 }  // namespace
 
 // codes: dense symbol codes (ovl_set_reads), off/len per read.  colbuf: rcap dwords per lane for each
@@ -462,17 +478,12 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
             t0n = *reinterpret_cast<const uint2*>(tp + 2 * q0);
             t1n = *reinterpret_cast<const uint2*>(tp + 2 * q1);
         };
-        auto row = [&](int32_t it, uint32_t x, uint32_t tnew, auto masked_tag) {
+        // x8 = 8 * the row symbol, tnew = the t code entering after the row (both from body's four-row words)
+        auto row = [&](int32_t it, uint32_t x8, uint32_t tnew, auto masked_tag) {
             constexpr bool MASKED = decltype(masked_tag)::value;
-            if constexpr (PL) {
-                const uint32_t r = (uint32_t)it & 31u;
-                x = __builtin_amdgcn_ubfe(S0, r, 1) | (__builtin_amdgcn_ubfe(S1, r, 1) << 1);
-                tnew = __builtin_amdgcn_ubfe(T0, r, 1) | (__builtin_amdgcn_ubfe(T1, r, 1) << 1);
-                tnew = it + ub < 0 ? PAD : tnew;
-            }
             // the row's 8-byte table (byte t = s2(x, t); virtual rows: s2 = -indel everywhere), built once per
             // row, so a profile word is one perm of it by the window word
-            uint32_t tlo = tbl_mm ^ (tbl_dm << (8 * x)), thi = tbl_hi;
+            uint32_t tlo = tbl_mm ^ (tbl_dm << x8), thi = tbl_hi;
             if constexpr (MASKED) {
                 const bool virt = it < sk;
                 tlo = virt ? p_virt : tlo;
@@ -495,7 +506,10 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
             for (int w = 0; w < NBW; ++w) T[w] = __builtin_amdgcn_alignbit(w + 1 < NBW ? T[w + 1] : 0u, T[w], 8);
             T[(NB - 1) >> 2] |= tnew << (8 * ((NB - 1) & 3));
         };
+        // rows it..it+3: their symbols (times 8, the table shift) and entering t codes as the bytes of one word
+        // each, extracted once per four rows
         auto body = [&](int32_t it, auto masked_tag) {
+            uint32_t xs8, ts;
             if constexpr (PL) {
                 if ((it & 31) == 0) {  // next 32 rows: rotate the block words, prefetch the block after
                     S0 = sn.x;
@@ -504,16 +518,17 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
                     T1 = __builtin_amdgcn_alignbit(t1n.y, t0n.y, tsh);
                     if (it + 32 < R) fetch_planes((it + 32) >> 5);
                 }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) row(it + k, 0u, 0u, masked_tag);
+                const uint32_t r0 = (uint32_t)it & 31u;
+                xs8 = codes4(S0, S1, r0) << 3;
+                ts = pad4(codes4(T0, T1, r0), it + ub);
             } else {
-                uint32_t s4[4], t4[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { s4[k] = qs[k]; t4[k] = qt[k]; }
+                xs8 = (qs[0] | (qs[1] << 8) | (qs[2] << 16) | (qs[3] << 24)) << 3;
+                ts = qt[0] | (qt[1] << 8) | (qt[2] << 16) | (qt[3] << 24);
                 if (it + 4 < R) fetch4(it + 4);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) row(it + k, s4[k], t4[k], masked_tag);
             }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                row(it + k, __builtin_amdgcn_ubfe(xs8, 8 * k, 8), __builtin_amdgcn_ubfe(ts, 8 * k, 8), masked_tag);
         };
         if constexpr (PL) fetch_planes(0);
         else fetch4(0);
@@ -665,18 +680,14 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
             t0n = *reinterpret_cast<const uint2*>(tp + 2 * q0);
             t1n = *reinterpret_cast<const uint2*>(tp + 2 * q1);
         };
-        // the row symbol / entering code of the previous step's iteration; before step 0 that is iteration -1,
-        // a virtual row (its symbol unused) whose entering code lane 1 appends in step 0
-        uint32_t x_prev = 0, tn_prev = tcode(ub - 1);
-        // step t: lane 0 runs iteration t, lane 1 iteration t - 1 (x_c / tn_c: iteration t's)
-        auto step = [&](int32_t t, uint32_t x_c, uint32_t tn_c, auto masked_tag) {
+        // the four-row words (body) of the previous group; before step 0 byte 3 is iteration -1's: a virtual row
+        // (its symbol unused) whose entering code lane 1 appends in step 0
+        uint32_t xs8_prev = 0, ts_prev = tcode(ub - 1) << 24;
+        // step t: lane 0 runs iteration t, lane 1 iteration t - 1; x8 (8 * symbol) and tnew are the lane's own
+        auto step = [&](int32_t t, uint32_t x8, uint32_t tnew, auto masked_tag) {
             constexpr bool MASKED = decltype(masked_tag)::value;
             const int32_t it = t - h;
-            const uint32_t x = h ? x_prev : x_c;
-            const uint32_t tnew = h ? tn_prev : tn_c;
-            x_prev = x_c;
-            tn_prev = tn_c;
-            uint32_t tlo = tbl_mm ^ (tbl_dm << (8 * x)), thi = tbl_hi;  // the row's table (band_lane_kernel)
+            uint32_t tlo = tbl_mm ^ (tbl_dm << x8), thi = tbl_hi;  // the row's table (band_lane_kernel)
             if constexpr (MASKED) {
                 const bool virt = it < sk;
                 tlo = virt ? p_virt : tlo;
@@ -709,7 +720,11 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
             const uint32_t bottom = (uint32_t)swap((int32_t)(T[0] & 0xFFu));
             T[(H - 1) >> 2] |= (h ? tnew : bottom) << (8 * ((H - 1) & 3));
         };
+        // steps t..t+3: iterations t..t+3's symbols (times 8) and entering codes as the bytes of one word each,
+        // extracted once per four steps; lane 1 takes them one iteration late (byte k - 1, byte 0 from the
+        // previous group's byte 3)
         auto body = [&](int32_t t, auto masked_tag) {
+            uint32_t xs8, ts;
             if constexpr (PL) {
                 if ((t & 31) == 0) {  // next 32 rows: rotate the block words, prefetch the block after
                     S0 = sn.x;
@@ -718,22 +733,21 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
                     T1 = __builtin_amdgcn_alignbit(t1n.y, t0n.y, tsh);
                     if (t + 32 < R) fetch_planes((t + 32) >> 5);
                 }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t r = (uint32_t)(t + k) & 31u;
-                    const uint32_t xc = __builtin_amdgcn_ubfe(S0, r, 1) | (__builtin_amdgcn_ubfe(S1, r, 1) << 1);
-                    uint32_t tc = __builtin_amdgcn_ubfe(T0, r, 1) | (__builtin_amdgcn_ubfe(T1, r, 1) << 1);
-                    tc = t + k + ub < 0 ? PAD : tc;
-                    step(t + k, xc, tc, masked_tag);
-                }
+                const uint32_t r0 = (uint32_t)t & 31u;
+                xs8 = codes4(S0, S1, r0) << 3;
+                ts = pad4(codes4(T0, T1, r0), t + ub);
             } else {
-                uint32_t s4[4], t4[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { s4[k] = qs[k]; t4[k] = qt[k]; }
+                xs8 = (qs[0] | (qs[1] << 8) | (qs[2] << 16) | (qs[3] << 24)) << 3;
+                ts = qt[0] | (qt[1] << 8) | (qt[2] << 16) | (qt[3] << 24);
                 if (t + 4 < R) fetch4(t + 4);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) step(t + k, s4[k], t4[k], masked_tag);
             }
+            const uint32_t xl = h ? __builtin_amdgcn_alignbyte(xs8, xs8_prev, 3) : xs8;
+            const uint32_t tl = h ? __builtin_amdgcn_alignbyte(ts, ts_prev, 3) : ts;
+            xs8_prev = xs8;
+            ts_prev = ts;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                step(t + k, __builtin_amdgcn_ubfe(xl, 8 * k, 8), __builtin_amdgcn_ubfe(tl, 8 * k, 8), masked_tag);
         };
         // row n on this lane's cells: in-band cells with 0 <= j <= m, largest value, first j
         int32_t best = INT32_MIN, bend = -1;
@@ -753,8 +767,8 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
         for (; t < mcut + 1 && t < R; t += 4) body(t, std::true_type{});
         for (; t < R; t += 4) body(t, std::false_type{});
         if (!h) scan();  // lane 0 has finished iteration R - 1
-        // step R: lane 1's last iteration (R - 1); lane 0's cells are no longer read
-        step(R, 0u, 0u, std::true_type{});
+        // step R: lane 1's last iteration (R - 1, byte 3 of the last group); lane 0's cells are no longer read
+        step(R, xs8_prev >> 24, ts_prev >> 24, std::true_type{});
         if (h) scan();
         const int32_t ob = swap(best), oe = swap(bend);
         if (live && !h) {

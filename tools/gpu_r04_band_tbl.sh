@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 4: band kernels with the row table built once per row (no x ^ t per window word): banded parity on the
-# new build, then cfg5 band times of the previous build (build/ablate_oldband) and the new one in alternating
+# round 4: band kernels, A/B of the previous build (build/ablate_oldband) against the new one: banded parity on the
+# new build, then cfg5 band times of both in alternating
 # processes (tools/band_ab.py, one lane and two lanes per pair)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
