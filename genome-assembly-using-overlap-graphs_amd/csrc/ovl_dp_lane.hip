@@ -693,9 +693,9 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
                 tlo = virt ? p_virt : tlo;
                 thi = virt ? p_virt : thi;
             }
-            // left of local cell 0: lane 1 takes lane 0's last cell of iteration t - 1 (finished last step)
-            const int32_t carry = swap(V[H - 1]);
-            int32_t left = h ? carry : NEG;
+            // left of local cell 0: lane 1 takes lane 0's last cell of iteration t - 1 (finished last step); lane 0's
+            // cell 0 is the dummy, set to -inf whatever its inputs
+            int32_t left = swap(V[H - 1]);
             int32_t upin = NEG;
             uint32_t P = 0;
 #pragma unroll
@@ -706,9 +706,9 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
                 int32_t v = max(max(d, up), left);
                 if (j == 0) {
                     if (!h) v = NEG;  // lane 0's dummy: the missing left of k = 0
-                    // lane 0's last cell takes as up lane 1's cell 0 after iteration t - 1 (just computed)
-                    const int32_t r = swap(v);
-                    upin = h ? NEG : r;
+                    // lane 0's last cell takes as up lane 1's cell 0 after iteration t - 1 (just computed); lane 1's
+                    // receives lane 0's dummy, -inf: the missing up of k = 2W
+                    upin = swap(v);
                 }
                 V[j] = v;
                 left = v;
