@@ -836,7 +836,11 @@ constexpr int kBandLaneMax = 64;
 template <int W, bool PL>
 hipError_t launch_band_lane_w(const OvlDpArgs* g, const OvlLaneArgs* k, int64_t blocks, hipStream_t stream) {
     constexpr int NB = 2 * W + 1;
-    constexpr int OCC = NB <= 25 ? 6 : (NB <= 57 ? 4 : (NB <= 65 ? 3 : (NB <= 113 ? 2 : 1)));
+    constexpr int OCC = NB <= 9 ? 8 : (NB <= 25 ? 6 : (NB <= 57 ? 4 : (NB <= 65 ? 3 : (NB <= 113 ? 2 : 1))));
+    if constexpr (OCC == 8) {  // (the grid the caller sized for 6 wavefronts per SIMD, grown to 8)
+        const int64_t tiles = (g->n_pairs + 63) / 64;
+        blocks = std::max<int64_t>(1, (std::min<int64_t>(k->slots / 6 * 8, tiles) + 3) / 4);
+    }
     ovl::band_lane_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
         g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx,
         g->n_pairs, g->mcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,

@@ -12,7 +12,7 @@ OLD="$GRAFT_REPO_ROOT/genome-assembly-using-overlap-graphs_amd/build/ablate_oldb
 for pass in 1 2; do
   for L in old new; do
     if [ $L = old ]; then LP="OVL_LIB_PATH=$OLD"; else LP=""; fi
-    env $LP BAND_AB_BANDS=8,16,32,48,64 timeout -k 10 300 python -u tools/band_ab.py 3 5 > $OUT/${L}_$pass.json 2>>$OUT/err.log || { echo "band ab failed $L"; tail -20 $OUT/err.log; exit 1; }
+    env $LP BAND_AB_BANDS=${BANDS:-8,16,32,48,64} timeout -k 10 300 python -u tools/band_ab.py 3 5 > $OUT/${L}_$pass.json 2>>$OUT/err.log || { echo "band ab failed $L"; tail -20 $OUT/err.log; exit 1; }
     python3 -c "
 import json; d=json.load(open('$OUT/${L}_$pass.json'))
 print('$L pass $pass', ' '.join(f\"{b}:{v['lane1']['median']}/{v['lane2']['median']}\" for b, v in d['ms'].items()))"
