@@ -648,7 +648,8 @@ def pair_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 
 SINKS = {0: "int32 results in HBM (copy-engine transfer after)", 1: "int32 results stored into pinned host memory",
-         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)"}
+         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)",
+         3: "tile records (9-bit codes + escapes, ~1.2 B/pair) stored into pinned host staging (host threads expand)"}
 
 
 def kernel_name(w, sink: int, pairs: int) -> str:
@@ -663,7 +664,8 @@ def kernel_name(w, sink: int, pairs: int) -> str:
     return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}, false>"
 
 
-# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed)
+# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed; 3 tile
+# records: 72 B per 64 pairs plus 2 B per escape, measured per call -- in_step_rooflines)
 LINK_BYTES_PER_PAIR = {0: 0, 1: 8, 2: 2}
 # a kernel's stores into pinned host memory, measured on the box (profiles/r02_pcie_write.txt)
 LINK_PEAK_GBS = 55.3
@@ -679,10 +681,20 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
     np.cumsum(pair_bytes(lens, w.a[w.lo:w.hi], w.b[w.lo:w.hi]), out=cum[1:])
     w.eng.set_timing(True)
     runs = []
+    rec_bpp = []
     for _ in range(reps):
         w.step()
         runs.append(w.eng.last_launches())
+        # tile records' bytes per pair: the call's link bytes less those of its other sinks
+        x = w.eng.last_transfer()
+        rec = [r["pairs"] for r in runs[-1] if r["sink"] == 3]
+        if rec:
+            other = sum(r["pairs"] * LINK_BYTES_PER_PAIR.get(r["sink"], 0) for r in runs[-1] if r["sink"] != 3)
+            rec_bpp.append((x["link_bytes"] - other) / sum(rec))
     w.eng.set_timing(False)
+    bpp = dict(LINK_BYTES_PER_PAIR)
+    if rec_bpp:
+        bpp[3] = float(np.median(rec_bpp))
     by_sink = {}
     for recs in runs:
         off = 0
@@ -704,8 +716,9 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
         byts = int(np.median(d["bytes"]))
         launches = len(d["ms"]) / reps
         ach = byts / (ms * 1e-3) / 1e9
-        link = pairs * LINK_BYTES_PER_PAIR.get(sink, 0)
+        link = int(pairs * bpp.get(sink, 0))
         table.append({"sink": sink, "what": SINKS.get(sink, "?"), "kernel": kernel_name(w, sink, pairs),
+                      "link_bytes_per_pair": bpp.get(sink, 0),
                       "link_bytes_per_launch": link, "link_gbs": link / (ms * 1e-3) / 1e9,
                       "link_frac": link / (ms * 1e-3) / 1e9 / LINK_PEAK_GBS,
                       "launches_per_step": launches, "launch_ms": ms, "launch_ms_all": ms_all,

@@ -84,8 +84,10 @@ struct Knobs {
     int32_t lane_prof = 1;        // OVL_LANE_PROF=0: compare/select scores instead of the byte profile (tests)
     int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
-    int32_t pack = 1;             // OVL_PACK=0: host-array results cross the link as int32 pairs even when the
-                                  // packed form (2 bytes per pair) holds (tests)
+    int32_t pack = 2;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
+                                  // form holds; 1 packed as 2 bytes per pair only; 2 (default) as tile records
+                                  // (~1.2 bytes per pair, ovl_kernels.hip put_tile9) where the launch runs in
+                                  // throughput mode, else 2 bytes per pair (tests)
     int64_t pack_min = 1 << 16;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
                                   // (64 K: a 250 K-pair shard -- N = 8 at the target point -- 0.057 -> 0.054 ms)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
@@ -117,6 +119,12 @@ constexpr int32_t kBandLane2Min = 64;
 // them in place.
 constexpr int64_t kLatTiles = 32;
 constexpr int64_t kLatTilesIx = 8;
+// ovl_set_reads keeps a host copy of the resident read set's bytes (same_reads) up to this size
+constexpr int64_t kResidentCopyMax = int64_t(256) << 20;
+// tile records (put_tile9): the mismatch rate at a pair's best end that the 9-bit codes centre on, / 256 -- at the
+// target point (match 10, mismatch -1) X / j clusters at 0.64 for the pairs that are no true overlap (~98 % of
+// the candidates), and 5 % of the pairs escape; the model decides only the escape share, never a result
+constexpr int32_t kRecRho = 164;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
 // host expansion of packed results: pairs per pool part at least (finer parts than 64 K: the expansion of a
@@ -159,6 +167,7 @@ struct Dev {
     hipEvent_t scratch_evt = nullptr;     // last launch that used lane_col / seed_* ...
     hipEvent_t ev_last = nullptr;         // packed calls into pinned arrays: after the last (direct) chunk
     double pack_pct = -1.0;               // live direct share of packed calls into pinned arrays (pack_share)
+    int32_t rho = kRecRho;                // tile records: the model's mismatch rate at a pair's best end, / 256
     double pack_pct_h = -1.0;             // the same for calls with a compact host pair list (the host also
                                           // encodes the list, so its balance point differs)
     hipStream_t scratch_stream = nullptr; // ... and its stream (launches on other streams wait for it)
@@ -251,6 +260,7 @@ struct ovl_ctx {
     };
     std::vector<Launch> t_launches;  // timing on: every scoring launch of the last host-array call
     int64_t x_link_bytes = 0, x_packed_pairs = 0;  // ovl_last_transfer
+    int64_t x_res_bytes = 0, x_rec_pairs = 0, x_esc = 0;  // ovl_last_results
     int64_t x_ix_pairs = 0, x_dec_pairs = 0;       // ovl_last_pair_list
 };
 
@@ -551,6 +561,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.ix_b16 = c->ix_b16;
         g.ix_d8 = c->ix_d8;
         g.ix_base = c->ix_base;
+        g.rho = c->rho;
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
         if (!g.ix_b16 && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
@@ -698,7 +709,7 @@ Knobs read_knobs() {
     if (const char* e = getenv("OVL_DP_LANE")) k.dp_lane = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_LANE_PROF")) k.lane_prof = atoi(e) ? 1 : 0;
     if (const char* e = getenv("OVL_LANE_SFX")) k.lane_sfx = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_PACK")) k.pack = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
@@ -719,6 +730,19 @@ void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(
 // Packed results (ovl_kernels.hip put_pair, sink 2) into the caller's int32 arrays (ovl_expand.h), split
 // over the host pool.  The vector width is the widest this CPU runs unless OVL_EXPAND_ISA names one
 // (scalar, sse2, avx2, avx512; A/B knob).
+// Tile records (put_tile9, sink 3) into the caller's int32 arrays, parts on tile boundaries; the escapes seen
+int64_t host_expand9(int32_t* s, int32_t* e, const uint8_t* rec, const int32_t* esc, const ovl_expand::Rec9& k,
+                     size_t n) {
+    static const ovl_expand::Fn9 f = ovl_expand::pick9();
+    std::atomic<int64_t> m{0};
+    CopyPool::get().parallel(n, kExpandPart, [&](size_t lo, size_t hi) {
+        int64_t mi = 0;
+        f(s, e, rec, esc, k, true, lo, hi, &mi);
+        m.fetch_add(mi, std::memory_order_relaxed);
+    });
+    return m.load();
+}
+
 void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
                  bool nt, size_t n, size_t min_part) {
     static const ovl_expand::Fn f = [] {
@@ -920,6 +944,8 @@ struct Job {
     int32_t* d_end = nullptr;
     std::vector<uint8_t> ixk;    // C.compact: chunk k's list is read in place by uniform_kernel (encode_chunk)
     std::vector<uint8_t> kexact; // timing: chunk k's kernel recorded its own start / end (k_ev)
+    std::vector<uint8_t> om;     // chunk k's result sink (OvlUngappedArgs::host_out): 1 int32, 2 packed, 3 records
+    int64_t n_esc = 0;           // escapes seen by the expansion of the record chunks
 };
 
 // Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
@@ -956,6 +982,12 @@ int setup_job(const Call& C, Job& J) {
         J.cb.push_back(o);
     }
     J.nchunks = (int64_t)J.cb.size() - 1;
+    // sinks: packed chunks as tile records where their launch runs in throughput mode (every pair of a tile
+    // scored by one wavefront), else 2 bytes per pair; the rest int32
+    J.om.assign((size_t)J.nchunks, 1);
+    J.n_esc = 0;
+    for (int64_t k = 0; k < J.n_packed; ++k)
+        J.om[(size_t)k] = d->k.pack >= 2 && ungapped_rs_log2(d, J.cb[(size_t)k + 1] - J.cb[(size_t)k]) == 0 ? 3 : 2;
     for (int64_t k = 0; k < J.nchunks; ++k) J.chunk = std::max(J.chunk, J.cb[(size_t)k + 1] - J.cb[(size_t)k]);
     const size_t bytes = sizeof(int32_t) * (size_t)n;
     if (C.compact) {
@@ -1004,7 +1036,7 @@ int setup_job(const Call& C, Job& J) {
     if ((need_in || need_out) && J.chunk > d->st_cap) {
         free_staging(d->st_in);
         free_staging(d->st_out);
-        d->st_cap = J.chunk;
+        d->st_cap = (J.chunk + 63) & ~int64_t(63);  // (a slot's tile records start on 256 bytes)
     }
     if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
     if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
@@ -1236,25 +1268,26 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     }
     int32_t* os = staged_out ? d->st_out_dev + so : J.d_score + off;
     int32_t* oe = staged_out ? d->st_out_dev + so + d->st_cap : J.d_end + off;
-    d->out_mode = C.pack && k < J.n_packed ? 2 : 1;
+    d->out_mode = J.om[(size_t)k];
+    hipStream_t ks = d->stream;
     if (C.timing) {
-        HIPCHK(d, hipEventRecord(d->t_ev[2 * k], d->stream));
+        HIPCHK(d, hipEventRecord(d->t_ev[2 * k], ks));
         if (C.plan->kernel == OVL_KERNEL_UNGAPPED) {  // (a chunk of one ungapped launch: time the kernel itself)
             d->kev_start = d->k_ev[2 * k];
             d->kev_stop = d->k_ev[2 * k + 1];
         }
     }
-    int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, d->stream);
+    int rc = launch_score(d, *C.plan, ka, kb, n, C.match, C.mismatch, C.indel, os, oe, ks);
     if (C.timing) J.kexact[(size_t)k] = d->kev_start == nullptr && C.plan->kernel == OVL_KERNEL_UNGAPPED;
     d->kev_start = d->kev_stop = nullptr;
     d->ix_b16 = nullptr;
     d->ix_d8 = nullptr;
     d->ix_base = nullptr;
     if (rc != OVL_OK) return rc;
-    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], d->stream));
-    if (staged_in || staged_out) HIPCHK(d, hipEventRecord(d->ev_k[slot], d->stream));
+    if (C.timing) HIPCHK(d, hipEventRecord(d->t_ev[2 * k + 1], ks));
+    if (staged_in || staged_out) HIPCHK(d, hipEventRecord(d->ev_k[slot], ks));
     if (C.pack && C.out_pinned && J.n_packed < J.nchunks && k == J.nchunks - 1)
-        HIPCHK(d, hipEventRecord(d->ev_last, d->stream));
+        HIPCHK(d, hipEventRecord(d->ev_last, ks));
     return OVL_OK;
 }
 
@@ -1275,6 +1308,12 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
         }
     } drained{k};
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
+    if (C.pack && J.om[(size_t)k] == 3) {
+        J.n_esc += host_expand9(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base),
+                                reinterpret_cast<const uint8_t*>(ss), ss + d->st_cap,
+                                {C.match, C.mismatch, d->lmax, d->rho}, (size_t)n);
+        return OVL_OK;
+    }
     if (C.pack) {
         host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
                     ss + d->st_cap, C.match, C.mismatch, true, (size_t)n, kExpandPart);
@@ -1398,7 +1437,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
                 const hipEvent_t* ev = exact ? &d->k_ev[2 * (size_t)k] : &d->t_ev[2 * (size_t)k];
                 if (hipEventElapsedTime(&ms, ev[0], ev[1]) == hipSuccess) s += ms;
                 // the chunk's result sink (issue_chunk): packed staging, or int32 into host memory
-                const int32_t sink = C.pack && k < J.n_packed ? 2 : 1;
+                const int32_t sink = J.om[(size_t)k];
                 c->t_launches.push_back({d->device, sink, J.cb[(size_t)k + 1] - J.cb[(size_t)k], (double)ms});
             }
             kms = std::max(kms, s);
@@ -1406,19 +1445,31 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     }
     c->t_kernel_ms = kms;
     c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    int64_t link = 0, packed = 0, ix = 0, dec = 0;
+    int64_t link = 0, packed = 0, ix = 0, dec = 0, res_all = 0, rec = 0, esc = 0;
     for (const Job& J : jobs) {
         const int64_t n = J.hi - J.lo;
         if (n <= 0) continue;
         const int64_t np = J.n_packed ? J.cb[(size_t)J.n_packed] : 0;
         packed += np;
-        link += (C.compact ? J.d->cp_link : (C.h_a ? 8 * n : 0)) + 2 * np + 8 * (n - np);
+        int64_t res = 8 * (n - np);  // results: int32 pairs, 2 bytes per packed pair, 72 bytes per record + escapes
+        for (int64_t k = 0; k < J.n_packed; ++k) {
+            const int64_t nk = J.cb[(size_t)k + 1] - J.cb[(size_t)k];
+            res += J.om[(size_t)k] == 3 ? 72 * ((nk + 63) / 64) : 2 * nk;
+            if (J.om[(size_t)k] == 3) rec += nk;
+        }
+        res += 2 * J.n_esc;
+        esc += J.n_esc;
+        res_all += res;
+        link += (C.compact ? J.d->cp_link : (C.h_a ? 8 * n : 0)) + res;
         if (C.compact)
             for (int64_t k = 0; k < J.nchunks; ++k)
                 (J.ixk[(size_t)k] ? ix : dec) += J.cb[(size_t)k + 1] - J.cb[(size_t)k];
     }
     c->x_link_bytes = link;
     c->x_packed_pairs = packed;
+    c->x_res_bytes = res_all;
+    c->x_rec_pairs = rec;
+    c->x_esc = esc;
     c->x_ix_pairs = ix;
     c->x_dec_pairs = dec;
     return rc;
@@ -1610,6 +1661,14 @@ OVL_API int ovl_last_transfer(const ovl_ctx* c, int64_t* link_bytes, int64_t* pa
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     if (link_bytes) *link_bytes = c->x_link_bytes;
     if (packed_pairs) *packed_pairs = c->x_packed_pairs;
+    return OVL_OK;
+}
+
+OVL_API int ovl_last_results(const ovl_ctx* c, int64_t* result_bytes, int64_t* record_pairs, int64_t* escapes) {
+    if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    if (result_bytes) *result_bytes = c->x_res_bytes;
+    if (record_pairs) *record_pairs = c->x_rec_pairs;
+    if (escapes) *escapes = c->x_esc;
     return OVL_OK;
 }
 
@@ -1824,7 +1883,9 @@ int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n
     if (n_reads > 0 && offsets[n_reads] > offsets[0] && !seqs) return fail(c, OVL_E_ARG, "seqs is NULL");
     DeviceGuard guard;
     if (same_reads(c, seqs, offsets, n_reads)) {
-        // already resident on every device: only the candidate list goes, as after an upload
+        // already resident on every device: only the candidate list goes, as after an upload (and the sharer
+        // count is refreshed as an upload would, when it is older than its interval)
+        CpuShare::get().refresh();
         for (Dev* d : c->devs) {
             d->cand_n = -1;
             d->heavy_for = -1;
@@ -1878,9 +1939,16 @@ int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n
     const int64_t base = n_reads > 0 ? offsets[0] : 0;
     c->res_off.resize((size_t)n_reads + 1);
     for (int32_t i = 0; i <= n_reads; ++i) c->res_off[(size_t)i] = n_reads > 0 ? offsets[i] - base : 0;
-    c->res_bytes.resize((size_t)h.total);
-    if (h.total > 0) host_copy(c->res_bytes.data(), seqs + base, (size_t)h.total);
-    c->res_valid = true;
+    // (a host copy of the bytes, so only for read sets up to kResidentCopyMax: larger ones are uploaded every call
+    // rather than doubling their host memory)
+    c->res_valid = h.total <= kResidentCopyMax;
+    c->res_bytes.clear();
+    if (c->res_valid) {
+        c->res_bytes.resize((size_t)h.total);
+        if (h.total > 0) host_copy(c->res_bytes.data(), seqs + base, (size_t)h.total);
+    } else {
+        c->res_bytes.shrink_to_fit();
+    }
     return OVL_OK;
 }
 

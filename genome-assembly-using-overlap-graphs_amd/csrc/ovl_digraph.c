@@ -847,9 +847,13 @@ static int row_advance(RowCtx* R, int64_t u, int all) {
                 Py_XDECREF(wv);
                 Py_XDECREF(ev);
                 const int bad = !d || PyDict_SetItem(R->rows[u], PyList_GET_ITEM(R->P->names, vb + cb), d);
-                Py_XDECREF(d);
-                if (bad) return -1;
-                R->dptr[e] = d; /* borrowed: the successor dict holds it */
+                if (bad) {
+                    Py_XDECREF(d);
+                    return -1;
+                }
+                /* owned (released in build_overlap_stream's exit): a duplicated (a, b) pair replaces the row's
+                   entry, freeing the first dict while its head's predecessor cursor may still be short of it */
+                R->dptr[e] = d;
                 ++R->n_ins;
             }
             R->dec[e] = 1;
@@ -1188,6 +1192,7 @@ done:
         pthread_join(scc_th, NULL);
         Py_END_ALLOW_THREADS
     }
+    const Py_ssize_t L_N = L.N, L_E = L.E;  /* (layout_free zeroes L) */
     layout_free(&L);
     cols_release(&C);
     if (bs.obj) PyBuffer_Release(&bs);
@@ -1200,14 +1205,17 @@ done:
         PyMem_Free(ints);
     }
     if (rows) {
-        for (Py_ssize_t i = 0; i < L.N; ++i) Py_XDECREF(rows[i]);
+        for (Py_ssize_t i = 0; i < L_N; ++i) Py_XDECREF(rows[i]);
         PyMem_Free(rows);
     }
     if (pin) {
-        for (Py_ssize_t i = 0; i < L.N; ++i) Py_XDECREF(pin[i]);
+        for (Py_ssize_t i = 0; i < L_N; ++i) Py_XDECREF(pin[i]);
         PyMem_Free(pin);
     }
-    PyMem_Free(dptr);
+    if (dptr) {
+        for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(dptr[e]);
+        PyMem_Free(dptr);
+    }
     PyMem_Free(rread);
     PyMem_Free(bgoff);
     PyMem_Free(blist);

@@ -323,7 +323,10 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                 const int64_t dead = pp[kmin].q;
                 const int32_t tail_of_dead = pp[kmin].tail;
                 removed[nrem++] = dead;
-                alive[(size_t)dead] = 0;
+                // release store: the streamed dict builder and the component helper read alive[] with acquire
+                // loads on other threads (ovl_remove_cycles_stream), and a node found alone in its component
+                // relies on removals becoming visible in program order
+                __atomic_store_n(&alive[(size_t)dead], (uint8_t)0, __ATOMIC_RELEASE);
                 E[dead].skip = 1;
                 sinks.removed(dead, alive);
                 // rewind the DFS to the moment `dead` was about to be yielded

@@ -156,7 +156,8 @@ int env_pool_threads() {
 // word (batch generation << 32 | next part).  Idle workers poll the claim word and take parts by compare-and-swap
 // on it, so a part goes to a worker within a cache-line transfer; the swap only succeeds for the current
 // generation, so a worker that read a finished batch's word never runs its function.  Workers that polled longer
-// than spin_us_ sleep on a condition variable, and the caller wakes them only when some are asleep.  (Round 4:
+// than spin_us_ sleep on a condition variable, and the caller wakes them only when some are asleep (spin_us_ is 0,
+// so every batch wakes them, only when this process's part of the CPUs is below two).  (Round 4:
 // the mutex-and-queue form handed a batch's parts out one lock at a time, ~11 us per batch of 12 parts on the
 // box -- a fixed cost per expanded chunk, tools/shard_step_ab.py traces.)
 class CopyPool {
@@ -193,7 +194,11 @@ class CopyPool {
     // inline instead of waiting on itself.
     void parallel_parts(const std::vector<size_t>& b, const std::function<void(size_t, size_t, size_t)>& f,
                         const std::function<void()>& pre = nullptr) {
-        const int spin = CpuShare::get().sharers() > 1 ? 0 : spin_cfg_;
+        // poll while this process's part of the CPUs holds its threads (pool_rule sizes them to it): ranks of a
+        // multi-GPU job on one node each own their part, and a sleeping worker's wake-up (~5-10 us) would be paid
+        // per batch; only a part below two CPUs (many processes on few CPUs) sleeps at once
+        const CpuShare& cs = CpuShare::get();
+        const int spin = cs.cpus() / std::max(1, cs.sharers()) >= 2 ? spin_cfg_ : 0;
         spin_us_.store(spin, std::memory_order_relaxed);
         const size_t parts = b.size() - 1;
         if (parts <= 1 || in_batch_) {
@@ -322,7 +327,7 @@ class CopyPool {
     int spin_cfg_ = 100;              // microseconds a worker polls for work after its last part
     static inline thread_local bool in_batch_ = false;  // this thread is inside parallel_parts (nested calls
                                                         // run inline)
-    std::atomic<int> spin_us_{100};   // 0 while other processes share this CPU set
+    std::atomic<int> spin_us_{100};   // 0 while this process's part of the CPU set is below two CPUs
     std::mutex mu_, call_mu_;
     std::condition_variable cv_, done_;
 };

@@ -49,6 +49,8 @@ SIGNATURES = {
     "ovl_last_launches": (ctypes.c_int, [_P, _i32, _P, _P, _P, _P, _pi32]),
     "ovl_last_transfer": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "ovl_last_pair_list": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "ovl_last_results": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_int64)]),
     "ovl_last_error": (ctypes.c_char_p, [_P]),
     "ovl_score_pairs": (ctypes.c_int, [_P, _P, _P, _i32, _P, _P, _i64, _i32, _i32, _i64, _i32, _P, _P]),
     "ovl_set_reads": (ctypes.c_int, [_P, _P, _P, _i32]),

@@ -149,10 +149,14 @@ class OverlapEngine:
                 for i in range(min(k, n.value))]
 
     def last_transfer(self) -> Dict[str, int]:
-        """{link_bytes, packed_pairs} of the last host-array scoring call (ovl_last_transfer)."""
+        """{link_bytes, packed_pairs} of the last host-array scoring call (ovl_last_transfer) and its results'
+        part: result_bytes, record_pairs (crossed as tile records), escapes (ovl_last_results)."""
         b, p = ctypes.c_int64(), ctypes.c_int64()
         check(self._L.ovl_last_transfer(self._ctx, ctypes.byref(b), ctypes.byref(p)), self._ctx)
-        return {"link_bytes": b.value, "packed_pairs": p.value}
+        r, q, e = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.ovl_last_results(self._ctx, ctypes.byref(r), ctypes.byref(q), ctypes.byref(e)), self._ctx)
+        return {"link_bytes": b.value, "packed_pairs": p.value, "result_bytes": r.value, "record_pairs": q.value,
+                "escapes": e.value}
 
     def last_pair_list(self) -> Dict[str, int]:
         """{in_place_pairs, decoded_pairs} of the last host-array call (ovl_last_pair_list): how the compact
@@ -263,7 +267,11 @@ class OverlapEngine:
                 ctypes.c_int64(indel), ctypes.c_int32(band), _ptr(sc), _ptr(en))
         check(self._L.ovl_plan(ctx, match, mismatch, indel, band, ctypes.byref(ctypes.c_int32())), ctx)
 
+        keep = (self, sc, en)  # the closure owns the result arrays (and the engine) its pointers name
+
         def score() -> None:
+            if keep[0]._ctx is None:
+                raise RuntimeError("range_scorer: the engine is closed")
             rc = fn(*args)
             if rc:
                 check(rc, ctx)

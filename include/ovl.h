@@ -106,10 +106,15 @@ int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs, double* ms,
                       int32_t* out_n);
 /* Link traffic of the last host-array scoring call (always recorded): link_bytes = pair-list bytes the
- * devices read from host memory + result bytes they stored there (2 per pair in packed chunks, 8 per pair
- * otherwise; the few packed pairs whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose results crossed packed and
+ * devices read from host memory + result bytes they stored there (ovl_last_results: 2 per pair in packed
+ * chunks, 72 per 64 pairs plus 2 per escape in tile records, 8 per pair otherwise; the few packed pairs whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose results crossed packed and
  * were expanded on the host. */
 int ovl_last_transfer(const ovl_ctx* ctx, int64_t* link_bytes, int64_t* packed_pairs);
+/* The results' part of the last host-array call's link bytes (always recorded): result_bytes = what the kernels
+ * stored into host memory for the results (8 per int32 pair, 2 per packed pair, 72 per tile record of 64 pairs
+ * plus 2 per escaped pair); record_pairs = pairs that crossed as tile records (packed chunks in throughput mode);
+ * escapes = those of them whose code could not hold their (end, mismatches) and crossed as 2-byte words. */
+int ovl_last_results(const ovl_ctx* ctx, int64_t* result_bytes, int64_t* record_pairs, int64_t* escapes);
 /* How the last host-array call's pair list reached the kernels (always recorded): in_place_pairs = pairs of
  * chunks the scoring kernel read in their compact encoding (b as uint16, a as tile deltas); decoded_pairs =
  * pairs of compact chunks decoded into HBM first (runs / widen kernels).  Both 0 for a call whose list crossed

@@ -19,3 +19,17 @@ def test_expand_variants_match_scalar(tmp_path):
     lines = r.stdout.splitlines()
     assert lines[-1] == "ok"
     assert "checked sse2" in lines
+
+
+def test_tile_records_decode(tmp_path):
+    """The tile records of ovl_kernels.hip put_tile9 (sink 3: 9-bit codes around a mismatch-rate model, escapes
+    as OM 2 words): tests/c/expand9_test.cpp encodes random results with the host restatement of put_tile9 and
+    checks the scalar decoder and the widest this CPU runs give every (score, end) back."""
+    exe = tmp_path / "expand9_test"
+    r = subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(PKG, "csrc"),
+                        "-o", str(exe), os.path.join(ROOT, "tests", "c", "expand9_test.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.splitlines()[-1] == "ok"

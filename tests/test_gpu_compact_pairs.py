@@ -167,10 +167,10 @@ def test_compact_adaptive_share(oracle_mod, target):
 
 
 def _pair_link_bytes(eng, n):
-    """Bytes of the pair list that crossed the link in the last call (results subtracted: 2 B per packed
-    pair, 8 B per int32 pair)."""
+    """Bytes of the pair list that crossed the link in the last call (the results' bytes subtracted,
+    ovl_last_results)."""
     t = eng.last_transfer()
-    return t["link_bytes"] - 2 * t["packed_pairs"] - 8 * (n - t["packed_pairs"])
+    return t["link_bytes"] - t["result_bytes"]
 
 
 @pytest.mark.parametrize("pinned", [False, True])

@@ -162,6 +162,59 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
         eng.close()
 
 
+@pytest.mark.parametrize("pack", ["1", "2"])
+@pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
+def test_tile_records(oracle_mod, cfg2, pack, scoring):
+    """Packed chunks in throughput mode cross the link as tile records (OVL_PACK=2, the default: ovl_kernels.hip
+    put_tile9, 9-bit codes around a mismatch-rate model, escapes as 2-byte words; OVL_PACK=1 keeps 2 bytes per
+    pair): cfg2's list tiled six times (731 K pairs, so the packed chunks run in throughput mode) with bad pairs,
+    scored under scorings that move the mismatch counts far from the model (every such pair an escape: match ==
+    mismatch, mismatch > match), into pinned, pageable and misaligned arrays, all packed and with a direct share;
+    every (score, end) equals the oracle's, and the call's link bytes are the records' (72 per tile + 2 per
+    escape) or OM 2's 2 per pair."""
+    from ovlgraph import OvlError
+    from ovlgraph.hostmem import pinned_empty
+    reads, a0, b0 = cfg2
+    match, mismatch = scoring
+    rs0, re0 = oracle_mod.batch_ungapped(reads, a0, b0, match, mismatch)
+    a, b = np.tile(a0, 6), np.tile(b0, 6)
+    ref_s, ref_e = np.tile(rs0, 6), np.tile(re0, 6)
+    n = a.shape[0] - 5
+    bad = np.array([0, 63, 64, 1000, n // 2, n - 1])
+    b = b.copy()
+    b[bad] = len(reads) + 3
+    ref_s, ref_e = ref_s.copy(), ref_e.copy()
+    ref_s[bad] = ref_e[bad] = -1
+    for pct in ("0", "25"):
+        eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_DIRECT_PCT": pct, "OVL_PAIRS_COMPACT": "0"})
+        try:
+            eng.set_reads(reads)
+            outs = {"pinned": (pinned_empty(n), pinned_empty(n)),
+                    "pageable": (np.empty(n, np.int32), np.empty(n, np.int32)),
+                    "misaligned": (np.empty(n + 1, np.int32)[1:], np.empty(n + 3, np.int32)[3:])}
+            for name, out in outs.items():
+                out[0][:] = 7
+                out[1][:] = 7
+                with pytest.raises(OvlError, match="OVL_E_INDEX"):
+                    eng.score(a[:n], b[:n], match, mismatch, out=out)
+                np.testing.assert_array_equal(out[0], ref_s[:n], err_msg=f"{name} pct {pct}")
+                np.testing.assert_array_equal(out[1], ref_e[:n], err_msg=f"{name} pct {pct}")
+                x = eng.last_transfer()
+                np_ = x["packed_pairs"]
+                assert np_ > 0 and x["link_bytes"] == 8 * n + x["result_bytes"], x
+                res = x["result_bytes"] - 8 * (n - np_)  # the packed part's result bytes
+                if pack == "1":
+                    assert res == 2 * np_ and x["record_pairs"] == 0, (name, x)
+                else:
+                    assert x["record_pairs"] == np_, (name, x)  # every packed chunk in throughput mode
+                    tiles = (np_ + 63) // 64
+                    assert res == 72 * tiles + 2 * x["escapes"], (name, x)
+                    if scoring == (10, -1):  # the model's own scoring: most pairs coded in 9 bits
+                        assert x["escapes"] < 0.25 * np_, (name, x)
+        finally:
+            eng.close()
+
+
 def test_packed_adaptive_share(oracle_mod, cfg2, cfg2_ref):
     """The direct share of packed calls into pinned arrays adapts call by call (no OVL_PACK_DIRECT_PCT):
     every call's results stay exact and the packed part stays within its bounds (50-98 % of the pairs)."""
@@ -585,7 +638,12 @@ def test_step_transport_vs_oracle(oracle_mod, cfg):
             np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
             x = eng.last_transfer()
             assert 0 < x["packed_pairs"] < n, x
-            assert x["link_bytes"] == 2 * x["packed_pairs"] + 8 * (n - x["packed_pairs"]), x
+            # (no pair list crosses: the link bytes are the results', tile records for the packed chunks in
+            # throughput mode -- 72 B per 64 pairs and 2 B per escape -- 2 B per other packed pair, 8 B per direct)
+            assert x["link_bytes"] == x["result_bytes"], x
+            q = x["record_pairs"]
+            assert x["result_bytes"] == 72 * ((q + 63) // 64) + 2 * x["escapes"] + 2 * (x["packed_pairs"] - q) + \
+                8 * (n - x["packed_pairs"]), x
         fresh = eng.score_candidates()
         np.testing.assert_array_equal(fresh[0], ref_s)
         np.testing.assert_array_equal(fresh[1], ref_e)

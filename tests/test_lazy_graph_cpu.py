@@ -165,3 +165,28 @@ def test_streamed_removal_equals_serial(monkeypatch, ms, scc):
     z = np.zeros(0, np.int32)
     L = og.remove_cycles_from_graph(og.OverlapEdges(["AC", "CA"], [1, 2], z, z, z, z).to_digraph())
     assert list(L.nodes()) == ["AC_0", "CA_0", "CA_1"] and L.number_of_edges() == 0
+
+
+def test_streamed_removal_duplicated_pairs(monkeypatch):
+    """A column set holding the same (a, b) pair twice (not a list overlapGraphs.py:43-52 makes, but OverlapEdges
+    accepts it): the streamed build replaces the row's entry with the second pair's attribute dict while the head's
+    predecessor cursor may still be short of the first; it holds its own reference to every attribute dict it has
+    inserted, so the result equals the replay-then-dicts path's (no read of a freed dict)."""
+    d, c, a, b, sc, en = _case(21, n_reads=400)
+    rng = np.random.default_rng(5)
+    dup = np.sort(rng.choice(len(a), size=len(a) // 4, replace=False))
+    order = np.sort(np.concatenate([np.arange(len(a)), dup]), kind="stable")
+    a2, b2 = a[order], b[order]
+    sc2 = sc[order].copy()
+    sc2[np.r_[False, order[1:] == order[:-1]]] += 1  # the repeated pair carries other attributes
+    en2 = np.arange(len(a2), dtype=np.int32)
+    E = og.OverlapEdges(d, c, a2, b2, sc2, en2)
+    out = {}
+    for off in (False, True):
+        monkeypatch.setattr(og, "_STREAM_OFF", off)
+        t = {}
+        out[off] = (og.remove_cycles_from_graph(E.to_digraph(), timing=t), t)
+    (Ls, ts), (Lr, tr) = out[False], out[True]
+    assert ts["overlapped"] and not tr["overlapped"] and ts["removed"] == tr["removed"]
+    _same_views(Ls, Lr)
+    assert nx.is_directed_acyclic_graph(Ls)
