@@ -649,7 +649,8 @@ def pair_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 SINKS = {0: "int32 results in HBM (copy-engine transfer after)", 1: "int32 results stored into pinned host memory",
          2: "packed 2 B/pair results stored into pinned host staging (host threads expand)",
-         3: "tile records (9-bit codes + escapes, ~1.2 B/pair) stored into pinned host staging (host threads expand)"}
+         3: "streamed tile records (15-bit codes + a phase bit per dword, 2 B/pair + 4 B per special pair) stored "
+            "into pinned host staging, expanded by host threads while the kernel runs"}
 
 
 def kernel_name(w, sink: int, pairs: int) -> str:
@@ -659,13 +660,13 @@ def kernel_name(w, sink: int, pairs: int) -> str:
     if w.kernel != "ungapped":
         return f"{w.kernel} kernel"
     lmax = w.eng.info()["lmax"]
-    lat = (pairs + 63) // 64 <= 256 * 32
+    lat = sink != 3 and (pairs + 63) // 64 <= 256 * 32  # (streamed records: always throughput mode)
     # (the fifth parameter, IX, is true only for host pair lists read in their encoding)
     return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}, false>"
 
 
-# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed; 3 tile
-# records: 72 B per 64 pairs plus 2 B per escape, measured per call -- in_step_rooflines)
+# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed; 3
+# streamed tile records: 128 B per 64 pairs plus 4 B per special pair, measured per call -- in_step_rooflines)
 LINK_BYTES_PER_PAIR = {0: 0, 1: 8, 2: 2}
 # a kernel's stores into pinned host memory, measured on the box (profiles/r02_pcie_write.txt)
 LINK_PEAK_GBS = 55.3

@@ -85,9 +85,9 @@ struct Knobs {
     int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
     int32_t pack = 2;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
-                                  // form holds; 1 packed as 2 bytes per pair only; 2 (default) as tile records
-                                  // (~1.2 bytes per pair, ovl_kernels.hip put_tile9) where the launch runs in
-                                  // throughput mode, else 2 bytes per pair (tests)
+                                  // form holds; 1 packed as 2 bytes per pair, expanded chunk by chunk after each
+                                  // chunk's kernel; 2 (default) as streamed tile records (ovl_kernels.hip
+                                  // put_tile_rec), expanded by host threads while the kernel still runs (tests)
     int64_t pack_min = 1 << 16;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
                                   // (64 K: a 250 K-pair shard -- N = 8 at the target point -- 0.057 -> 0.054 ms)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
@@ -121,10 +121,11 @@ constexpr int64_t kLatTiles = 32;
 constexpr int64_t kLatTilesIx = 8;
 // ovl_set_reads keeps a host copy of the resident read set's bytes (same_reads) up to this size
 constexpr int64_t kResidentCopyMax = int64_t(256) << 20;
-// tile records (put_tile9): the mismatch rate at a pair's best end that the 9-bit codes centre on, / 256 -- at the
-// target point (match 10, mismatch -1) X / j clusters at 0.64 for the pairs that are no true overlap (~98 % of
-// the candidates), and 5 % of the pairs escape; the model decides only the escape share, never a result
-constexpr int32_t kRecRho = 164;
+// streamed tile records: tiles per group of the expansion (groups go round-robin to the pool's parts, so every
+// part has records arriving while the kernel runs), and pairs per pipeline chunk at most
+constexpr int64_t kRecGroupTiles = 8;
+constexpr size_t kRecSkip = 32;  // incomplete records a pass of the expansion skips before it polls again
+constexpr int64_t kRecChunk = int64_t(1) << 22;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
 // host expansion of packed results: pairs per pool part at least (finer parts than 64 K: the expansion of a
@@ -167,7 +168,14 @@ struct Dev {
     hipEvent_t scratch_evt = nullptr;     // last launch that used lane_col / seed_* ...
     hipEvent_t ev_last = nullptr;         // packed calls into pinned arrays: after the last (direct) chunk
     double pack_pct = -1.0;               // live direct share of packed calls into pinned arrays (pack_share)
-    int32_t rho = kRecRho;                // tile records: the model's mismatch rate at a pair's best end, / 256
+    // streamed tile records, per staging slot: the phase bit of the slot's record dwords (every dword of tiles
+    // [0, rec_hw) carries it; the dwords above are still zero from the allocation) and its high-water mark
+    uint8_t rec_phase[kSlots] = {};
+    int64_t rec_hw[kSlots] = {};
+    uint32_t rec_phase_next = 0;          // the phase the next record launch stores (launch_score_chunk),
+    int64_t rec_tiles = 0;                // its tiles [0, rec_tiles) as records, the rest as int32 into
+    int32_t* dir_score = nullptr;         // these (device addresses of the caller's pinned arrays; null: none)
+    int32_t* dir_end = nullptr;
     double pack_pct_h = -1.0;             // the same for calls with a compact host pair list (the host also
                                           // encodes the list, so its balance point differs)
     hipStream_t scratch_stream = nullptr; // ... and its stream (launches on other streams wait for it)
@@ -524,7 +532,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         if (rc != OVL_OK) return rc;
         seed_end = as<int32_t>(c->seed_e);
     }
-    if (c->ix_b16 && (pl.kernel != OVL_KERNEL_UNGAPPED || pl.key64 || !ix_launch(c, n_pairs)))
+    if (c->ix_b16 && (pl.kernel != OVL_KERNEL_UNGAPPED || pl.key64 || (c->out_mode != 3 && !ix_launch(c, n_pairs))))
         return fail(c, OVL_E_UNSUPPORTED, "host-encoded pair list on a launch that cannot read it");
     if (pl.kernel == OVL_KERNEL_UNGAPPED) {
         OvlUngappedArgs g{};
@@ -561,7 +569,11 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.ix_b16 = c->ix_b16;
         g.ix_d8 = c->ix_d8;
         g.ix_base = c->ix_base;
-        g.rho = c->rho;
+        g.rec_phase = c->rec_phase_next;
+        g.rec_tiles = c->out_mode == 3 ? c->rec_tiles : 0;
+        g.dir_score = c->out_mode == 3 ? c->dir_score : nullptr;
+        g.dir_end = c->out_mode == 3 ? c->dir_end : nullptr;
+        if (c->out_mode == 3) g.rs_log2 = 0;  // (records: throughput mode, every pair of a tile in one wave)
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
         if (!g.ix_b16 && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
@@ -730,19 +742,6 @@ void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(
 // Packed results (ovl_kernels.hip put_pair, sink 2) into the caller's int32 arrays (ovl_expand.h), split
 // over the host pool.  The vector width is the widest this CPU runs unless OVL_EXPAND_ISA names one
 // (scalar, sse2, avx2, avx512; A/B knob).
-// Tile records (put_tile9, sink 3) into the caller's int32 arrays, parts on tile boundaries; the escapes seen
-int64_t host_expand9(int32_t* s, int32_t* e, const uint8_t* rec, const int32_t* esc, const ovl_expand::Rec9& k,
-                     size_t n) {
-    static const ovl_expand::Fn9 f = ovl_expand::pick9();
-    std::atomic<int64_t> m{0};
-    CopyPool::get().parallel(n, kExpandPart, [&](size_t lo, size_t hi) {
-        int64_t mi = 0;
-        f(s, e, rec, esc, k, true, lo, hi, &mi);
-        m.fetch_add(mi, std::memory_order_relaxed);
-    });
-    return m.load();
-}
-
 void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
                  bool nt, size_t n, size_t min_part) {
     static const ovl_expand::Fn f = [] {
@@ -945,7 +944,13 @@ struct Job {
     std::vector<uint8_t> ixk;    // C.compact: chunk k's list is read in place by uniform_kernel (encode_chunk)
     std::vector<uint8_t> kexact; // timing: chunk k's kernel recorded its own start / end (k_ev)
     std::vector<uint8_t> om;     // chunk k's result sink (OvlUngappedArgs::host_out): 1 int32, 2 packed, 3 records
-    int64_t n_esc = 0;           // escapes seen by the expansion of the record chunks
+    int64_t n_esc = 0;           // special pairs seen by the expansion of the record chunks
+    int64_t drained = 0;         // chunks [0, drained) are drained (run_pipeline)
+    int64_t rec_end = 0;         // packed pairs [0, rec_end); streamed records: the pairs from rec_end on are
+                                 // stored as int32 by the last chunk's launch (its tiles from rec_end / 64)
+    int64_t n_bad = 0;           // bad pairs seen by the expansion of the record chunks (their special words)
+    bool ended = true;           // every launch of the job is known finished (false: a streamed chunk returned
+                                 // on its records alone; run_pipeline then needs no stream synchronisation)
 };
 
 // Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
@@ -960,34 +965,46 @@ int setup_job(const Call& C, Job& J) {
     HIPCHK(d, hipSetDevice(d->device));
     const bool need_in = C.h_a && !C.in_pinned && !C.compact, need_out = !C.out_pinned || C.pack;
     J.chunk = pick_chunk(d, n, need_in || need_out, C.pack);
+    const bool stream = C.pack && d->k.pack >= 2;  // streamed records: fewer, larger chunks (the host expands
+                                                   // each while its kernel runs)
+    if (stream && d->k.pipe_chunk <= 0) J.chunk = std::min(n, kRecChunk);
     // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
     if (C.pack) {
         double& share = C.compact ? d->pack_pct_h : d->pack_pct;
         if (share < 0.0) share = C.compact ? 2.0 * d->k.pack_direct_pct : d->k.pack_direct_pct;
-        const int64_t pct = d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct;
+        // (streamed records: no direct share unless OVL_PACK_DIRECT_PCT asks for one -- it lengthens the launch
+        // on the link and makes the call wait for the kernel's end: 0 % was fastest at N = 2 / 4 / 8 and within
+        // 4 % at N = 1, profiles/r05_stream_share_ab.json)
+        const int64_t pct = stream ? (d->k.pack_adapt ? 0 : d->k.pack_direct_pct)
+                                   : (d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct);
         packed = C.out_pinned ? (n - n * pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
         // (a ramp of growing chunks -- 196 K, x 1.5 each -- to start the host's expansion sooner measured slower:
         // 0.208 against 0.145 ms at the target point, each extra chunk costing an issue and a later direct
         // chunk; profiles/r04_pool_ab_*.json)
-        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
-        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
-        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
-        if (packed > 0) J.cb.push_back(packed);
+        // (streamed records: the chunks cover every pair, and the last one's launch stores its pairs from
+        // `packed` on as int32 straight into the caller's pinned arrays -- one launch, no second kernel)
+        const int64_t span = stream ? n : packed;
+        const int64_t pieces = (span + J.chunk - 1) / J.chunk;
+        const int64_t step = pieces ? (((span + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+        for (int64_t o = step; o < span; o += step) J.cb.push_back(o);
+        if (span > 0) J.cb.push_back(span);
         J.n_packed = (int64_t)J.cb.size() - 1;
     }
-    for (int64_t o = packed; o < n;) {
+    J.rec_end = stream ? packed : J.cb.back();
+    for (int64_t o = J.cb.back(); o < n;) {  // (the direct chunks; none when streamed: the chunks cover every pair)
         o = std::min(n, o + J.chunk);
         J.cb.push_back(o);
     }
     J.nchunks = (int64_t)J.cb.size() - 1;
-    // sinks: packed chunks as tile records where their launch runs in throughput mode (every pair of a tile
-    // scored by one wavefront), else 2 bytes per pair; the rest int32
+    // sinks: packed chunks as streamed tile records (OVL_PACK=1: 2 bytes per pair); the rest int32
     J.om.assign((size_t)J.nchunks, 1);
     J.n_esc = 0;
-    for (int64_t k = 0; k < J.n_packed; ++k)
-        J.om[(size_t)k] = d->k.pack >= 2 && ungapped_rs_log2(d, J.cb[(size_t)k + 1] - J.cb[(size_t)k]) == 0 ? 3 : 2;
+    J.n_bad = 0;
+    J.ended = true;
+    J.drained = 0;
+    for (int64_t k = 0; k < J.n_packed; ++k) J.om[(size_t)k] = stream ? 3 : 2;
     for (int64_t k = 0; k < J.nchunks; ++k) J.chunk = std::max(J.chunk, J.cb[(size_t)k + 1] - J.cb[(size_t)k]);
     const size_t bytes = sizeof(int32_t) * (size_t)n;
     if (C.compact) {
@@ -1039,7 +1056,15 @@ int setup_job(const Call& C, Job& J) {
         d->st_cap = (J.chunk + 63) & ~int64_t(63);  // (a slot's tile records start on 256 bytes)
     }
     if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
-    if (need_out && !d->st_out) HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
+    if (need_out && !d->st_out) {
+        HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
+        // (streamed records: every record dword and special word starts at zero, phase 0)
+        memset(d->st_out, 0, (size_t)kSlots * 2 * (size_t)d->st_cap * sizeof(int32_t));
+        for (int i = 0; i < kSlots; ++i) {
+            d->rec_phase[i] = 0;
+            d->rec_hw[i] = 0;
+        }
+    }
     if (C.timing && (int64_t)d->t_ev.size() < 2 * J.nchunks) {
         while ((int64_t)d->t_ev.size() < 2 * J.nchunks) {
             hipEvent_t ev;
@@ -1055,7 +1080,8 @@ int setup_job(const Call& C, Job& J) {
 
 // OVL_TRACE_PIPE=1 (diagnostics): one stderr line per host-array call with the microsecond offsets of its
 // pipeline events (s setup, i<k> chunk k issued, w<k> its results ready on the host side, d<k> drained,
-// y final synchronisation).
+// y final synchronisation; streamed records: f<k> the calling thread's first record expanded, p<k> its part
+// done, k<k> the chunk's kernel seen finished).
 struct PipeTrace {
     bool on;
     std::chrono::steady_clock::time_point t0;
@@ -1127,7 +1153,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
     // throughput-mode uniform launch; else the decode below.
     // (OVL_TRACE_PIPE: 'x' marks a chunk that cannot be read in place, with the first failed condition)
     const int ix_why = wd != 2 ? 1 : !d->k.pairs_ix ? 2 : C.plan->kernel != OVL_KERNEL_UNGAPPED ? 3
-                       : C.plan->key64 ? 4 : !ix_launch(d, n) ? 5 : 0;
+                       : C.plan->key64 ? 4 : !(J.om[(size_t)k] == 3 || ix_launch(d, n)) ? 5 : 0;
     if (g_trace && ix_why) g_trace->mark('x', ix_why);
     if (ix_why == 0) {
         uint8_t* d8 = reinterpret_cast<uint8_t*>(ha);
@@ -1269,6 +1295,22 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     int32_t* os = staged_out ? d->st_out_dev + so : J.d_score + off;
     int32_t* oe = staged_out ? d->st_out_dev + so + d->st_cap : J.d_end + off;
     d->out_mode = J.om[(size_t)k];
+    if (d->out_mode == 3) {
+        // streamed records: this launch stores the other phase; a slot growing past its high-water mark first
+        // gives the new tiles' dwords the old phase (they are zero, i.e. phase 0, until then)
+        const int64_t nt = (std::max<int64_t>(0, std::min(n, J.rec_end - off)) + 63) / 64;
+        uint32_t* rec = reinterpret_cast<uint32_t*>(d->st_out + so);
+        if (nt > d->rec_hw[slot]) {
+            if (d->rec_phase[slot])
+                std::fill(rec + 32 * d->rec_hw[slot], rec + 32 * nt, 0x80000000u);
+            d->rec_hw[slot] = nt;
+        }
+        d->rec_phase_next = d->rec_phase[slot] ^ 1u;
+        // the chunk's tiles from rec_end on store int32 into the caller's pinned arrays (the direct share)
+        d->rec_tiles = (std::max<int64_t>(0, std::min(n, J.rec_end - off)) + 63) / 64;
+        d->dir_score = d->rec_tiles * 64 < n ? J.d_score + off : nullptr;
+        d->dir_end = d->rec_tiles * 64 < n ? J.d_end + off : nullptr;
+    }
     hipStream_t ks = d->stream;
     if (C.timing) {
         HIPCHK(d, hipEventRecord(d->t_ev[2 * k], ks));
@@ -1291,6 +1333,156 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     return OVL_OK;
 }
 
+// Streamed tile records of chunk k (sink 3; ovl_kernels.hip put_tile_rec, ovl_expand.h): the host pool expands
+// the records into the caller's arrays as they arrive, while the chunk's kernel still runs.  The chunk's tiles
+// go in groups of kRecGroupTiles round-robin to the pool's parts, so every part has records landing throughout
+// the kernel; a part's passes take every complete record among its tiles, skipping incomplete ones (records of
+// one round of waves land in any order), and poll when a pass found nothing.
+//   The call needs the kernel's end only when the chunk has direct tiles (int32 stores the host cannot see
+// arrive) or timing is on (`need_end`): then part 0 -- the calling thread -- waits for the chunk's event after
+// its own tiles.  Otherwise the results are complete once every record is read: bad pairs arrive as special
+// words (the kernel sets no host flag for record tiles), nothing of this call is left to land in host memory,
+// and the stream orders the next call's launches after this kernel, so the call returns ~5 us before the
+// kernel's completion signal could be seen (tools/launch_probe.hip).
+//   A kernel that fails must not leave a part polling forever: part 0 queries the event while it polls, any
+// part queries it after kLostPolls fruitless polls, and a record still incomplete well after the kernel has
+// finished -- which the kernel's end makes impossible -- ends the call with OVL_E_INTERNAL.  The special words
+// read are zeroed again, and tiles above this chunk's that an earlier, larger chunk left in this slot get this
+// launch's phase, so the slot's next launch finds every dword it does not write yet in the other phase.
+int stream_chunk(const Call& C, Job& J, int64_t k) {
+    constexpr uint32_t kLostPolls = 1u << 14;
+    Dev* d = J.d;
+    const int64_t off = J.cb[(size_t)k];
+    const int64_t g = J.lo + off;
+    const int64_t n = J.cb[(size_t)k + 1] - off;
+    const int slot = (int)(k % kSlots);
+    const int64_t nrec = std::max<int64_t>(0, std::min(n, J.rec_end - off));  // pairs of the records
+    const int64_t nt = (nrec + 63) / 64;
+    const bool need_end = nrec < n || C.timing;
+    uint32_t* rec = reinterpret_cast<uint32_t*>(d->st_out + (size_t)slot * 2 * (size_t)d->st_cap);
+    uint32_t* sp = rec + d->st_cap;
+    const uint32_t phase = d->rec_phase[slot] ^ 1u;
+    int32_t* S = C.out_s + (g - C.out_base);
+    int32_t* E = C.out_e + (g - C.out_base);
+    const ovl_expand::RecK rk{C.match, C.mismatch};
+    static const bool a512 = ovl_expand::rec_avx512();
+    // non-temporal stores where the arrays are aligned: regular stores (read for ownership) measured 1.2-1.9x
+    // slower at every shard size (profiles/r05_rec_store_ab.json)
+    const bool al = ((uintptr_t)S & 63) == 0 && ((uintptr_t)E & 63) == 0;
+    const hipEvent_t ev = d->ev_k[slot];
+    // 0 the kernel may still run, 1 it has finished, 2 error (kernel failure or an incomplete record)
+    std::atomic<int> state{0};
+    std::atomic<int64_t> specials{0}, bad{0};
+    std::atomic<hipError_t> herr{hipSuccess};
+    const auto query = [&] {  // the kernel's event; false on a failure
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) {
+            int z = 0;
+            if (state.compare_exchange_strong(z, 1, std::memory_order_acq_rel) && g_trace) g_trace->mark('k', k);
+        } else if (q != hipErrorNotReady) {
+            herr.store(q);
+            state.store(2, std::memory_order_release);
+            return false;
+        }
+        return true;
+    };
+    CopyPool& pool = CopyPool::get();
+    const std::vector<size_t> parts = pool.cut(64 * 64, 64);
+    const int64_t P = (int64_t)parts.size() - 1;
+    const int64_t ngroups = (nt + kRecGroupTiles - 1) / kRecGroupTiles;
+    pool.parallel_parts(parts, [&](size_t i, size_t, size_t) {
+        uint32_t polls = 0;  // fruitless polls in a row
+        int64_t after = 0;   // polls since the kernel was seen finished
+        // one poll of an incomplete record or special word: false ends the part (error)
+        const auto wait = [&]() -> bool {
+            _mm_pause();
+            const int st = state.load(std::memory_order_acquire);
+            if (st == 2) return false;
+            if (st == 1) {
+                if (++after > (int64_t(1) << 22)) {  // (~0.1 s after the kernel's end)
+                    state.store(2, std::memory_order_release);
+                    return false;
+                }
+                return true;
+            }
+            ++polls;
+            if ((i == 0 && (polls & 63) == 0) || (polls & (kLostPolls - 1)) == 0) return query();
+            return true;
+        };
+        // this part's tiles (its groups, in order); a pass expands every complete record among them and skips
+        // the incomplete ones until kRecSkip of them, so a pass costs a few polls when little has landed
+        std::vector<int32_t> pend;
+        pend.reserve((size_t)((nt / P) + 2 * kRecGroupTiles));
+        for (int64_t gi = (int64_t)i; gi < ngroups; gi += P)
+            for (int64_t t = gi * kRecGroupTiles, t1 = std::min(nt, (gi + 1) * kRecGroupTiles); t < t1; ++t)
+                pend.push_back((int32_t)t);
+        int64_t m = 0;
+        int nbad = 0;
+        bool first = i == 0 && g_trace;
+        while (!pend.empty()) {
+            size_t keep = 0, skipped = 0, x = 0, took = 0;
+            for (; x < pend.size() && skipped < kRecSkip; ++x) {
+                const int64_t t = pend[x];
+                const size_t cnt = (size_t)std::min<int64_t>(64, nrec - 64 * t);
+                const uint32_t* r = rec + 32 * t;
+                int got;
+                if (a512 && cnt == 64) {
+                    bool ready = false;
+                    got = ovl_expand::rec_tile_avx512(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, phase, al, &ready,
+                                                      &nbad, wait);
+                    if (!ready) got = -2;
+                } else {
+                    got = ovl_expand::rec_tile_ready_scalar(r, phase)
+                              ? ovl_expand::rec_tile_scalar(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, cnt, &nbad,
+                                                            wait)
+                              : -2;
+                }
+                if (got == -1) return;  // (state 2: the caller reports it)
+                if (got >= 0) {
+                    m += got;
+                    ++took;
+                    if (first) {
+                        g_trace->mark('f', k);
+                        first = false;
+                    }
+                } else {
+                    pend[keep++] = (int32_t)t;
+                    ++skipped;
+                }
+            }
+            for (; x < pend.size(); ++x) pend[keep++] = pend[x];
+            pend.resize(keep);
+            if (took) polls = 0;
+            else if (!pend.empty() && !wait()) return;
+        }
+        specials.fetch_add(m, std::memory_order_relaxed);
+        bad.fetch_add(nbad, std::memory_order_relaxed);
+        if (i == 0 && need_end) {  // the kernel's end (its event): direct tiles, timing
+            if (g_trace) g_trace->mark('p', k);
+            while (state.load(std::memory_order_acquire) == 0 && query()) _mm_pause();
+        }
+    });
+    _mm_sfence();
+    if (state.load() == 2) {
+        // the slot's dwords and special words are in no known state: reallocated (zeroed) by the next call
+        (void)hipStreamSynchronize(d->stream);
+        free_staging(d->st_out);
+        d->st_cap = 0;
+        const hipError_t e = herr.load();
+        if (e != hipSuccess) return fail(d, OVL_E_HIP, "HIP error %d (%s) in the scoring kernel", (int)e,
+                                         hipGetErrorString(e));
+        return fail(d, OVL_E_INTERNAL, "a result record was incomplete after its kernel finished");
+    }
+    if (nt < d->rec_hw[slot]) {
+        for (int64_t w = 32 * nt; w < 32 * d->rec_hw[slot]; ++w) rec[w] ^= 0x80000000u;
+    }
+    d->rec_phase[slot] = (uint8_t)phase;
+    J.n_esc += specials.load();
+    J.n_bad += bad.load();
+    J.ended = need_end;  // (the stream's earlier launches end before this chunk's)
+    return OVL_OK;
+}
+
 // Pageable outputs: copy chunk k out of its staging slot once its results are there (the kernel that stored
 // them has finished).
 int drain_chunk(const Call& C, Job& J, int64_t k) {
@@ -1299,6 +1491,11 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int64_t g = J.lo + off;
     const int64_t n = J.cb[(size_t)k + 1] - off;
     const int slot = (int)(k % kSlots);
+    if (J.om[(size_t)k] == 3) {
+        const int rc = stream_chunk(C, J, k);
+        if (g_trace) g_trace->mark('d', k);
+        return rc;
+    }
     HIPCHK(d, wait_event(d, d->ev_k[slot]));
     if (g_trace) g_trace->mark('w', k);
     struct Drained {
@@ -1308,12 +1505,6 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
         }
     } drained{k};
     const int32_t* ss = d->st_out + (size_t)slot * 2 * (size_t)d->st_cap;
-    if (C.pack && J.om[(size_t)k] == 3) {
-        J.n_esc += host_expand9(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base),
-                                reinterpret_cast<const uint8_t*>(ss), ss + d->st_cap,
-                                {C.match, C.mismatch, d->lmax, d->rho}, (size_t)n);
-        return OVL_OK;
-    }
     if (C.pack) {
         host_expand(C.out_s + (g - C.out_base), C.out_e + (g - C.out_base), reinterpret_cast<const uint16_t*>(ss),
                     ss + d->st_cap, C.match, C.mismatch, true, (size_t)n, kExpandPart);
@@ -1383,14 +1574,21 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
             if (C.compact && k + 1 < J.nchunks) rc = encode_chunk(C, J, k + 1, issue);
             else rc = issue();
             if (rc != OVL_OK) break;
-            const int64_t j = k - (kSlots - 1);
-            if (j >= 0 && chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
+            // drain in order: a streamed record chunk once the chunk after it is queued (its kernel follows on
+            // the device while the host expands), other staged chunks kSlots - 1 behind
+            while (J.drained <= k) {
+                const int64_t j = J.drained;
+                if (chunk_staged(C, J, j) && k - j < (J.om[(size_t)j] == 3 ? 1 : kSlots - 1)) break;
+                if (chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
+                ++J.drained;
+            }
+            if (rc != OVL_OK) break;
         }
     }
     for (Job& J : jobs) {
         if (rc != OVL_OK) break;
-        for (int64_t k = std::max<int64_t>(0, J.nchunks - (kSlots - 1)); k < J.nchunks; ++k)
-            if (chunk_staged(C, J, k) && (rc = drain_chunk(C, J, k)) != OVL_OK) break;
+        for (; J.drained < J.nchunks; ++J.drained)
+            if (chunk_staged(C, J, J.drained) && (rc = drain_chunk(C, J, J.drained)) != OVL_OK) break;
     }
     if (rc != OVL_OK) {
         quiesce(jobs);
@@ -1415,7 +1613,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         }
     }
     for (Job& J : jobs) {
-        if (J.nchunks == 0) continue;
+        if (J.nchunks == 0 || !J.ended) continue;  // (streamed records, all read: nothing left to land)
         HIPCHK(c, hipSetDevice(J.d->device));
         HIPCHK(c, hipStreamSynchronize(J.d->stream));
     }
@@ -1425,8 +1623,8 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         Dev* d = J.d;
         if (J.nchunks == 0) continue;
-        if (*(volatile uint32_t*)d->h_flag) {
-            *d->h_flag = 0;
+        if ((J.ended && *(volatile uint32_t*)d->h_flag) || J.n_bad > 0) {
+            if (J.ended) *d->h_flag = 0;
             rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
         }
         if (C.timing) {
@@ -1449,15 +1647,15 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (const Job& J : jobs) {
         const int64_t n = J.hi - J.lo;
         if (n <= 0) continue;
-        const int64_t np = J.n_packed ? J.cb[(size_t)J.n_packed] : 0;
+        const int64_t np = J.n_packed ? std::min(J.rec_end, J.cb[(size_t)J.n_packed]) : 0;
         packed += np;
-        int64_t res = 8 * (n - np);  // results: int32 pairs, 2 bytes per packed pair, 72 bytes per record + escapes
+        int64_t res = 8 * (n - np);  // results: int32 pairs, 2 bytes per packed pair, 128 per record + specials
         for (int64_t k = 0; k < J.n_packed; ++k) {
-            const int64_t nk = J.cb[(size_t)k + 1] - J.cb[(size_t)k];
-            res += J.om[(size_t)k] == 3 ? 72 * ((nk + 63) / 64) : 2 * nk;
+            const int64_t nk = std::min(J.cb[(size_t)k + 1], np) - std::min(J.cb[(size_t)k], np);
+            res += J.om[(size_t)k] == 3 ? 128 * ((nk + 63) / 64) : 2 * nk;
             if (J.om[(size_t)k] == 3) rec += nk;
         }
-        res += 2 * J.n_esc;
+        res += 4 * J.n_esc;
         esc += J.n_esc;
         res_all += res;
         link += (C.compact ? J.d->cp_link : (C.h_a ? 8 * n : 0)) + res;

@@ -180,176 +180,180 @@ __attribute__((target("avx512f,avx512bw"))) inline void expand_avx512(int32_t* s
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Tile records (ovl_kernels.hip put_tile9, sink 3): per 64-pair tile t a record at rec + 256 t --
-//   bytes [0, 64) the low 8 bits of lane l's 9-bit code c, byte l;  bytes [64, 72) bit l = bit 8 of c;
-//   bytes [72, ..) the uint16 OM 2 word of each lane whose code is 511 (an escape), in lane order.
-// c != 511: j = lw - (c >> 4), X = ((j * rho) >> 8) + (c & 15) - 8, score = match*j + (mismatch - match)*X.
-// An escape's word decodes as `one` does (0xFFFF bad, X = 0xFF: the score in esc[i]).  Ranges [lo, hi) start on
-// a tile (lo % 64 == 0); the escapes seen are added to *n_esc.
+// Streamed tile records (ovl_kernels.hip put_tile_rec, sink 3): tile t's record is 32 dwords at rec + 32 t,
+//   dword w = phase << 31 | c[w + 32] << 15 | c[w]    (c[l]: the 15-bit code of the tile's pair l)
+// c = j(j + 1)/2 + X (end j, X mismatches over L = j compared bases): score = match*j + (mismatch - match)*X.
+// c = 0x7FFF: the pair's special word sp[i] (i the pair's index in the chunk) holds it --
+//   1 << 31 | j << 16 | X << 8 | n: score = match*n + (mismatch - match)*X, end j;  0xFFFFFFFF: (-1, -1);
+//   0: not arrived yet.  The reader zeroes a special word once it has read it (the slot's invariant: every
+//   special word is 0 between calls).
+// A record is complete when every dword's bit 31 is the launch's phase (rec_tile_ready).  j from c: the
+// largest j with j(j + 1)/2 <= c is floor((sqrt(8c + 1) - 1) / 2), exact in float for c < 2^15 (8c + 1 is a
+// perfect square exactly when X = 0, and otherwise lies >= 1 from one, far above float's error at 2^18).
 
-struct Rec9 {
-    int32_t match, mismatch, lw, rho;
+constexpr uint32_t kRecSpecial = 0x7FFFu;
+
+struct RecK {
+    int32_t match, mismatch;
 };
 
-using Fn9 = void (*)(int32_t* s, int32_t* e, const uint8_t* rec, const int32_t* esc, const Rec9& k, bool nt,
-                     size_t lo, size_t hi, int64_t* n_esc);
-
-// an escape's word v for pair i -> (score, end)
-inline void rec9_esc(int32_t& s, int32_t& e, const int32_t* esc, const Rec9& k, uint32_t v, size_t i) {
-    const uint32_t j = v >> 8, x = v & 0xFFu;
-    if (v == 0xFFFFu) {
-        s = e = -1;
-        return;
-    }
-    s = x == 0xFFu ? esc[i] : k.match * (int32_t)(j - x) + k.mismatch * (int32_t)x;
+inline void rec_decode_code(uint32_t c, const RecK& k, int32_t& s, int32_t& e) {
+    const uint32_t j = (uint32_t)(int32_t)((__builtin_sqrtf((float)(8 * c + 1)) - 1.0f) * 0.5f);
+    const int32_t x = (int32_t)(c - (j * (j + 1) >> 1));
+    s = k.match * (int32_t)j + (k.mismatch - k.match) * x;
     e = (int32_t)j;
 }
 
-// one tile's pairs [t0, t0 + cnt), scalar
-inline int64_t rec9_tile_scalar(int32_t* s, int32_t* e, const uint8_t* r, const int32_t* esc, const Rec9& k,
-                                size_t t0, size_t cnt) {
-    uint64_t hm;
-    memcpy(&hm, r + 64, 8);
-    const uint8_t* ev = r + 72;
-    int64_t m = 0;
+// a special word (non-zero) -> (score, end)
+inline void rec_decode_special(uint32_t v, const RecK& k, int32_t& s, int32_t& e) {
+    if (v == 0xFFFFFFFFu) {
+        s = e = -1;
+        return;
+    }
+    const int32_t j = (int32_t)(v >> 16 & 0xFFu), x = (int32_t)(v >> 8 & 0xFFu), n = (int32_t)(v & 0xFFu);
+    s = k.match * n + (k.mismatch - k.match) * x;
+    e = j;
+}
+
+// all 32 dwords of the record carry `phase` in bit 31
+inline bool rec_tile_ready_scalar(const uint32_t* r, uint32_t phase) {
+    const volatile uint32_t* v = r;
+    for (int w = 0; w < 32; ++w)
+        if ((v[w] >> 31) != phase) return false;
+    return true;
+}
+
+// Waits for special word sp[i] (spinning while `wait` says to), decodes it and zeroes it; a bad pair adds 1 to
+// *bad.  False if `wait` gave up first.
+template <typename Wait>
+inline bool rec_take_special(uint32_t* sp, size_t i, const RecK& k, int32_t& s, int32_t& e, int* bad, Wait&& wait) {
+    volatile uint32_t* v = sp + i;
+    uint32_t x;
+    while ((x = *v) == 0u)
+        if (!wait()) return false;
+    rec_decode_special(x, k, s, e);
+    *bad += x == 0xFFFFFFFFu;
+    *v = 0u;
+    return true;
+}
+
+// one complete record's pairs [0, cnt) (cnt <= 64) into s / e (scalar); the specials' count (the bad pairs
+// among them added to *bad), or -1 if one never came
+template <typename Wait>
+inline int rec_tile_scalar(int32_t* s, int32_t* e, const uint32_t* r, uint32_t* sp, const RecK& k, size_t cnt,
+                           int* bad, Wait&& wait) {
+    const volatile uint32_t* v = r;
+    int m = 0;
     for (size_t l = 0; l < cnt; ++l) {
-        const uint32_t c = r[l] | (uint32_t)((hm >> l) & 1u) << 8;
-        const size_t i = t0 + l;
-        if (c == 511u) {
-            uint16_t v;
-            memcpy(&v, ev + 2 * m++, 2);
-            rec9_esc(s[i], e[i], esc, k, v, i);
-            continue;
+        const uint32_t c = (v[l & 31] >> (l < 32 ? 0 : 15)) & 0x7FFFu;
+        if (c == kRecSpecial) {
+            if (!rec_take_special(sp, l, k, s[l], e[l], bad, wait)) return -1;
+            ++m;
+        } else {
+            rec_decode_code(c, k, s[l], e[l]);
         }
-        const int32_t j = k.lw - (int32_t)(c >> 4);
-        const int32_t x = ((j * k.rho) >> 8) + (int32_t)(c & 15u) - 8;
-        s[i] = k.match * j + (k.mismatch - k.match) * x;
-        e[i] = j;
     }
     return m;
 }
 
-inline void expand9_scalar(int32_t* s, int32_t* e, const uint8_t* rec, const int32_t* esc, const Rec9& k, bool,
-                           size_t lo, size_t hi, int64_t* n_esc) {
-    int64_t m = 0;
-    for (size_t t0 = lo; t0 < hi; t0 += 64)
-        m += rec9_tile_scalar(s, e, rec + 4 * t0, esc, k, t0, hi - t0 < 64 ? hi - t0 : 64);
-    if (n_esc) *n_esc += m;
-}
-
-// 64 pairs per step: the codes as two 32-lane 16-bit vectors, four 64-byte stores per array
-__attribute__((target("avx512f,avx512bw"))) inline void expand9_avx512(int32_t* s, int32_t* e, const uint8_t* rec,
-                                                                       const int32_t* esc, const Rec9& k, bool nt,
-                                                                       size_t lo, size_t hi, int64_t* n_esc) {
-    const bool al = nt && ((uintptr_t)(s + lo) & 63) == 0 && ((uintptr_t)(e + lo) & 63) == 0;
-    const __m512i vlw = _mm512_set1_epi16((int16_t)k.lw), vrho = _mm512_set1_epi16((int16_t)k.rho);
-    const __m512i v15 = _mm512_set1_epi16(15), v8 = _mm512_set1_epi16(8), v256 = _mm512_set1_epi16(256);
-    const __m512i vm = _mm512_set1_epi16((int16_t)k.match), vd = _mm512_set1_epi16((int16_t)(k.mismatch - k.match));
-    const __m512i ff = _mm512_set1_epi8((char)0xFF);
-    int64_t m = 0;
-    size_t t0 = lo;
-    for (; t0 + 64 <= hi; t0 += 64) {
-        const uint8_t* r = rec + 4 * t0;
-        const __m512i bytes = _mm512_loadu_si512(r);
-        uint64_t hm;
-        memcpy(&hm, r + 64, 8);
-        const uint64_t em = _mm512_cmpeq_epi8_mask(bytes, ff) & hm;
-        __m512i out[8];  // s 0..3, e 0..3 (16 pairs each)
-        for (int h = 0; h < 2; ++h) {
-            __m512i c = _mm512_cvtepu8_epi16(h ? _mm512_extracti64x4_epi64(bytes, 1) : _mm512_castsi512_si256(bytes));
-            c = _mm512_mask_add_epi16(c, (__mmask32)(hm >> (32 * h)), c, v256);
-            const __m512i j = _mm512_sub_epi16(vlw, _mm512_srli_epi16(c, 4));
-            const __m512i xc = _mm512_srli_epi16(_mm512_mullo_epi16(j, vrho), 8);
-            const __m512i x = _mm512_sub_epi16(_mm512_add_epi16(xc, _mm512_and_si512(c, v15)), v8);
-            const __m512i sc = _mm512_add_epi16(_mm512_mullo_epi16(j, vm), _mm512_mullo_epi16(x, vd));
-            out[2 * h] = _mm512_cvtepi16_epi32(_mm512_castsi512_si256(sc));
-            out[2 * h + 1] = _mm512_cvtepi16_epi32(_mm512_extracti64x4_epi64(sc, 1));
-            out[4 + 2 * h] = _mm512_cvtepu16_epi32(_mm512_castsi512_si256(j));
-            out[4 + 2 * h + 1] = _mm512_cvtepu16_epi32(_mm512_extracti64x4_epi64(j, 1));
+// AVX-512: readiness check and decode of one full record (64 pairs) from the same two loads; *ready = false
+// (nothing written) when the record is incomplete.  Stores non-temporally when `al` (s and e 64-byte aligned).
+// Returns the specials' count, or -1 if `wait` gave up on one.
+template <typename Wait>
+__attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(int32_t* s, int32_t* e,
+                                                                                  const uint32_t* r, uint32_t* sp,
+                                                                                  const RecK& k, uint32_t phase,
+                                                                                  bool al, bool* ready, int* bad,
+                                                                                  Wait&& wait) {
+    const __m512i w0 = _mm512_load_si512(r), w1 = _mm512_load_si512(r + 16);
+    const __m512i sign = _mm512_set1_epi32((int)0x80000000u);
+    const __mmask16 want = phase ? (__mmask16)0xFFFF : (__mmask16)0;
+    if (_mm512_test_epi32_mask(w0, sign) != want || _mm512_test_epi32_mask(w1, sign) != want) {
+        *ready = false;
+        return 0;
+    }
+    *ready = true;
+    const __m512i m15 = _mm512_set1_epi32(0x7FFF), one = _mm512_set1_epi32(1);
+    const __m512i vm = _mm512_set1_epi32(k.match), vd = _mm512_set1_epi32(k.mismatch - k.match);
+    const __m512 f8 = _mm512_set1_ps(8.0f), f1 = _mm512_set1_ps(1.0f), fh = _mm512_set1_ps(0.5f);
+    __m512i S[4], E[4];
+    __mmask16 spm[4];
+    const __m512i cs[4] = {_mm512_and_si512(w0, m15), _mm512_and_si512(w1, m15),
+                           _mm512_and_si512(_mm512_srli_epi32(w0, 15), m15),
+                           _mm512_and_si512(_mm512_srli_epi32(w1, 15), m15)};
+    int specials = 0;
+    for (int q = 0; q < 4; ++q) {  // pairs 16q .. 16q + 15
+        const __m512i c = cs[q];
+        const __m512 f = _mm512_sqrt_ps(_mm512_fmadd_ps(_mm512_cvtepi32_ps(c), f8, f1));
+        const __m512i j = _mm512_cvttps_epi32(_mm512_mul_ps(_mm512_sub_ps(f, f1), fh));
+        const __m512i tri = _mm512_srli_epi32(_mm512_mullo_epi32(j, _mm512_add_epi32(j, one)), 1);
+        const __m512i x = _mm512_sub_epi32(c, tri);
+        S[q] = _mm512_add_epi32(_mm512_mullo_epi32(j, vm), _mm512_mullo_epi32(x, vd));
+        E[q] = j;
+        spm[q] = _mm512_cmpeq_epi32_mask(c, m15);
+        specials |= spm[q];
+    }
+    if (specials) {
+        alignas(64) int32_t ts[64], te[64];
+        for (int q = 0; q < 4; ++q) {
+            _mm512_store_si512(ts + 16 * q, S[q]);
+            _mm512_store_si512(te + 16 * q, E[q]);
         }
-        if (em) {  // escapes: patched in the vectors (lane order = the order of their words)
-            alignas(64) int32_t ts[64], te[64];
-            for (int q = 0; q < 4; ++q) {
-                _mm512_store_si512(ts + 16 * q, out[q]);
-                _mm512_store_si512(te + 16 * q, out[4 + q]);
+        int m = 0;
+        for (int q = 0; q < 4; ++q)
+            for (uint32_t b = spm[q]; b; b &= b - 1, ++m) {
+                const int l = 16 * q + __builtin_ctz(b);
+                // (the device stores it before the record's dword, but nothing orders their arrival)
+                if (!rec_take_special(sp, (size_t)l, k, ts[l], te[l], bad, wait)) return -1;
             }
-            const uint8_t* ev = r + 72;
-            int q = 0;
-            for (uint64_t b = em; b; b &= b - 1, ++q) {
-                const int l = __builtin_ctzll(b);
-                uint16_t v;
-                memcpy(&v, ev + 2 * q, 2);
-                rec9_esc(ts[l], te[l], esc, k, v, t0 + l);
-            }
-            m += q;
-            for (int q4 = 0; q4 < 4; ++q4) {
-                out[q4] = _mm512_load_si512(ts + 16 * q4);
-                out[4 + q4] = _mm512_load_si512(te + 16 * q4);
-            }
+        for (int q = 0; q < 4; ++q) {
+            S[q] = _mm512_load_si512(ts + 16 * q);
+            E[q] = _mm512_load_si512(te + 16 * q);
         }
         for (int q = 0; q < 4; ++q) {
-            put512(s + t0 + 16 * q, out[q], al);
-            put512(e + t0 + 16 * q, out[4 + q], al);
+            put512(s + 16 * q, S[q], al);
+            put512(e + 16 * q, E[q], al);
         }
+        return m;
     }
-    int64_t mt = 0;
-    if (t0 < hi) mt = rec9_tile_scalar(s, e, rec + 4 * t0, esc, k, t0, hi - t0);
-    if (n_esc) *n_esc += m + mt;
-    _mm_sfence();
+    for (int q = 0; q < 4; ++q) {
+        put512(s + 16 * q, S[q], al);
+        put512(e + 16 * q, E[q], al);
+    }
+    return 0;
 }
 
-inline Fn9 pick9() {
+// this CPU runs rec_tile_avx512
+inline bool rec_avx512() {
 #if defined(__HIP_DEVICE_COMPILE__)
-    return expand9_scalar;
+    return false;
 #else
     __builtin_cpu_init();
-    const bool a512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
-    return a512 ? expand9_avx512 : expand9_scalar;
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+           __builtin_cpu_supports("avx512dq");
 #endif
 }
 
-// The record encoder (put_tile9 restated on the host), for the CPU tests of the decoders: lane l of tile t
-// holds pair t0 + l's (score, end) for cnt <= 64 pairs; n is read a's length (j > n: a window pair, its score
-// into esc), end -1 a bad pair.  Returns the record's bytes (72 + 2 * escapes).
-inline size_t encode9_tile(uint8_t* r, int32_t* esc, const Rec9& k, const int32_t* sc, const int32_t* en,
-                           const int32_t* n, size_t t0, size_t cnt) {
-    uint64_t hm = 0;
-    size_t m = 0;
-    for (size_t l = 0; l < 64; ++l) {
-        uint32_t c = 0, v = 0;
-        bool is_esc = false;
-        if (l < cnt) {
-            const size_t i = t0 + l;
-            const int32_t j = en[i];
-            if (j < 0) {
-                is_esc = true;
-                v = 0xFFFFu;
-            } else if (j > n[i]) {
-                is_esc = true;
-                v = (uint32_t)j << 8 | 0xFFu;
-                esc[i] = sc[i];
-            } else {
-                const int32_t x = k.match == k.mismatch ? 0 : (k.match * j - sc[i]) / (k.match - k.mismatch);
-                const int32_t dj = k.lw - j, dx = x - ((j * k.rho) >> 8) + 8;
-                const uint32_t cc = (uint32_t)(16 * dj + dx);
-                if ((uint32_t)dj < 32u && (uint32_t)dx < 16u && cc != 511u) {
-                    c = cc;
-                } else {
-                    is_esc = true;
-                    v = (uint32_t)j << 8 | (uint32_t)x;
-                }
-            }
+// The record encoder (put_tile_rec restated on the host), for the CPU tests of the decoders: pairs [0, cnt) of
+// a tile from (sc, en, n) -- n read a's length (j > n: a window pair), en -1 a bad pair; specials into sp.
+inline void encode_rec_tile(uint32_t* r, uint32_t* sp, const RecK& k, const int32_t* sc, const int32_t* en,
+                            const int32_t* n, size_t cnt, uint32_t phase) {
+    uint32_t c[64] = {0};
+    for (size_t l = 0; l < cnt; ++l) {
+        const int32_t j = en[l];
+        if (j < 0) {
+            c[l] = kRecSpecial;
+            sp[l] = 0xFFFFFFFFu;
+        } else if (j > n[l]) {
+            const int32_t x = k.match == k.mismatch ? 0 : (k.match * n[l] - sc[l]) / (k.match - k.mismatch);
+            c[l] = kRecSpecial;
+            sp[l] = 0x80000000u | (uint32_t)j << 16 | (uint32_t)x << 8 | (uint32_t)n[l];
+        } else {
+            const int32_t x = k.match == k.mismatch ? 0 : (k.match * j - sc[l]) / (k.match - k.mismatch);
+            c[l] = ((uint32_t)j * (uint32_t)(j + 1) >> 1) + (uint32_t)x;
         }
-        if (is_esc) {
-            c = 511u;
-            const uint16_t w = (uint16_t)v;
-            memcpy(r + 72 + 2 * m++, &w, 2);
-        }
-        r[l] = (uint8_t)c;
-        hm |= (uint64_t)(c >> 8) << l;
     }
-    memcpy(r + 64, &hm, 8);
-    return 72 + 2 * m;
+    for (int w = 0; w < 32; ++w) r[w] = phase << 31 | c[w + 32] << 15 | c[w];
 }
 
 // isa: "scalar", "sse2", "avx2", "avx512" or NULL / "" (the widest this CPU runs); NULL if unsupported

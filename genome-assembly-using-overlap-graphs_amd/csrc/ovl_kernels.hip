@@ -107,59 +107,43 @@ __device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
     return match != mismatch ? 1.0f / (float)(match - mismatch) : 0.f;
 }
 
-// OM 3: a 64-pair tile's results as one record of <= 200 bytes in a 256-byte slot of the host-mapped staging
-// (rec = out_score as bytes, slot tile * 256), 1.1-1.4 bytes per pair over the link instead of OM 2's 2:
-//   bytes [0, 64)   the low 8 bits of each lane's 9-bit code, 4 lanes per dword;
-//   bytes [64, 72)  a 64-bit mask: bit l = bit 8 of lane l's code;
-//   bytes [72, ..)  the OM 2 word (j << 8 | X, j << 8 | 0xFF, 0xFFFF) of every lane whose code is 511, in lane
-//                   order (j << 8 | 0xFF with the score in out_end[p], as OM 2).
-// Code c = 16 * (lw - j) + (X - xc(j) + 8) when lw - j < 32 and the mismatch count X lies within [-8, 8) of
-// xc(j) = (j * rho) >> 8 (rho / 256: the host's model of the mismatch rate at a pair's best end), c != 511; every
-// other pair is an escape (c = 511).  The model only decides how many pairs escape, never a result: the host
-// (ovl_expand.h expand9) inverts the code exactly.  At the target point (rho 164) 5 % of the pairs escape.
-// Every lane of the wavefront calls it (the ballots); lanes with !mine store nothing of their own.
-__device__ __forceinline__ void put_tile9(int32_t* out_score, int32_t* out_end, int64_t tile, int64_t p, bool mine,
-                                          int32_t sc, int32_t en, int32_t n, int32_t lw, int32_t match, float inv,
-                                          int32_t rho, int lane) {
-    uint32_t v16 = 0, c = 0;
-    bool esc = false;
+// OM 3: streamed tile records.  A 64-pair tile's results as one 128-byte record at out_score + 32 * tile
+// (dwords), which host threads read while the kernel still runs (ovl_expand.h rec_tile_ready / expand_rec):
+//   dword w (w < 32) = phase << 31 | c[w + 32] << 15 | c[w]   (c[l]: lane l's 15-bit code)
+// The phase bit (the host flips it each time it reuses the staging slot) tells the host which dwords this
+// launch has written: every dword is one aligned 32-bit store, so a dword whose phase bit is the launch's
+// holds the launch's payload, and a record is complete when all 32 are.  No fence, no counter, no
+// acknowledgement wait on the device (the rejected one-grid transport paid an L2 write-back per wave for its
+// counters).  Code c of a pair with end j <= n (read a's length; L = j compared bases, aligners.py:27-48 with
+// gaps that cannot win, so score = match*j + (mismatch - match)*X) is j(j + 1)/2 + X, X <= j <= 254 (< 0x7FFF).
+// Every other pair has c = 0x7FFF and a special word in out_end[p] (the host reads it and zeroes it again):
+//   1 << 31 | j << 16 | X << 8 | n   a shorter read a inside b's window (j > n: L = n, score = match*n +
+//                                    (mismatch - match)*X);
+//   0xFFFFFFFF                       a bad pair (-1, -1).
+// 2 link bytes per pair (+ 4 per special), a fixed layout whatever the mismatch counts.  Every lane of the
+// wavefront calls it (the cross-half exchange); lanes with !mine code 0, which the host never reads.
+__device__ __forceinline__ void put_tile_rec(int32_t* out_score, int32_t* out_end, int64_t tile, int64_t p, bool mine,
+                                             int32_t sc, int32_t en, int32_t n, int32_t match, float inv,
+                                             uint32_t phase, int lane) {
+    uint32_t c = 0;
     if (mine) {
         if (en < 0) {
-            esc = true;
-            v16 = 0xFFFFu;
+            c = 0x7FFFu;
+            __builtin_nontemporal_store(0xFFFFFFFFu, reinterpret_cast<uint32_t*>(out_end) + p);
         } else if (en > n) {
-            esc = true;
-            v16 = ((uint32_t)en << 8) | 0xFFu;
-            __builtin_nontemporal_store(sc, out_end + p);
+            // X = (match*n - score) / (match - mismatch), an exact quotient below 2^8: float is exact
+            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * n - sc) * inv);
+            c = 0x7FFFu;
+            __builtin_nontemporal_store(0x80000000u | (uint32_t)en << 16 | x << 8 | (uint32_t)n,
+                                        reinterpret_cast<uint32_t*>(out_end) + p);
         } else {
             const uint32_t x = (uint32_t)__builtin_rintf((float)(match * en - sc) * inv);
-            const int32_t dj = lw - en;
-            const int32_t dx = (int32_t)x - ((en * rho) >> 8) + 8;
-            const uint32_t cc = (uint32_t)(16 * dj + dx);
-            if ((uint32_t)dj < 32u && (uint32_t)dx < 16u && cc != 511u) {
-                c = cc;
-            } else {
-                esc = true;
-                v16 = ((uint32_t)en << 8) | x;
-            }
+            c = ((uint32_t)en * (uint32_t)(en + 1) >> 1) + x;
         }
     }
-    if (esc) c = 511u;
-    const uint64_t em = __ballot(esc);
-    const uint64_t hm = __ballot((c & 256u) != 0u);
-    uint8_t* rec = reinterpret_cast<uint8_t*>(out_score) + tile * 256;
-    // four lanes' low bytes into one dword (quad rotations), stored by the quad's first lane
-    const int b0 = (int)(c & 0xFFu);
-    const int b1 = __builtin_amdgcn_update_dpp(0, b0, 0x39, 0xF, 0xF, false);  // quad_perm [1, 2, 3, 0]
-    const int b2 = __builtin_amdgcn_update_dpp(0, b0, 0x4E, 0xF, 0xF, false);  // quad_perm [2, 3, 0, 1]
-    const int b3 = __builtin_amdgcn_update_dpp(0, b0, 0x93, 0xF, 0xF, false);  // quad_perm [3, 0, 1, 2]
-    const uint32_t w = (uint32_t)b0 | ((uint32_t)b1 << 8) | ((uint32_t)b2 << 16) | ((uint32_t)b3 << 24);
-    if ((lane & 3) == 0) __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(rec) + (lane >> 2));
-    if (lane == 0) __builtin_nontemporal_store(hm, reinterpret_cast<uint64_t*>(rec + 64));
-    if (esc) {
-        const int rank = __popcll(em & ((1ull << lane) - 1ull));
-        __builtin_nontemporal_store((uint16_t)v16, reinterpret_cast<uint16_t*>(rec + 72) + rank);
-    }
+    const uint32_t hi = (uint32_t)__shfl_xor((int)c, 32, 64);
+    if (lane < 32)
+        __builtin_nontemporal_store(phase << 31 | hi << 15 | c, reinterpret_cast<uint32_t*>(out_score) + tile * 32 + lane);
 }
 
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
@@ -906,10 +890,11 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag,
     const int32_t* __restrict__ heavy_ids, const uint8_t* __restrict__ tile_flags, int32_t heavy_n,
     int64_t tile_base, const uint16_t* __restrict__ ix_b16, const uint8_t* __restrict__ ix_d8,
-    const int32_t* __restrict__ ix_base, int32_t rho) {
+    const int32_t* __restrict__ ix_base, uint32_t rec_phase, int64_t rec_tiles, int32_t* __restrict__ dir_score,
+    int32_t* __restrict__ dir_end) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
-    static_assert(OM != 3 || (KM == 0 && !LAT), "tile records (OM 3): throughput mode, int32 keys");
+    static_assert(OM != 3 || (KM == 0 && !LAT), "streamed tile records (OM 3): throughput mode, int32 keys");
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = (W * P + 3) & ~3;
     // t-truncated pairs in the sweep (snapshot): throughput mode with int32 keys.  Not in latency mode,
@@ -1079,7 +1064,9 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             tmask |= 1u << (__builtin_amdgcn_readlane(tm, (int)__builtin_ctzll(bm)) & 31);
         OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
         if constexpr (!LAT) {
-            if (mine && !ok) ovl_flag_error(err_flag);
+            // (a record tile's bad pair travels as its special word: the host may return before this kernel ends,
+            // so the host flag -- read after the end -- is only for the direct tiles)
+            if (mine && !ok && (OM != 3 || tile >= rec_tiles)) ovl_flag_error(err_flag);
             const bool push = OM != 3 && ok && !uni && !tt;
             const uint64_t pm = __ballot(push);
             if (push)
@@ -1108,11 +1095,19 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         }
         OVL_TR_CLOCK(3, (uint32_t)best);
         if constexpr (OM == 3) {
-            // (TT: every pair of the tile is this wave's, so its record is complete here)
-            int32_t sc, en;
-            Key<KM>::decode(best, sc, en);
-            put_tile9(out_score, out_end, tile, p, mine, ok ? sc : -1, ok ? en : -1, na, lw, match,
-                      pack_inv(match, mismatch), rho, lane);
+            // (TT: every pair of the tile is this wave's, so its record is complete here; a wave past the last
+            // tile stores nothing)
+            if (tile < n_tiles) {
+                int32_t sc, en;
+                Key<KM>::decode(best, sc, en);
+                if (tile < rec_tiles) {
+                    put_tile_rec(out_score, out_end, tile, p, mine, ok ? sc : -1, ok ? en : -1, na, match,
+                                 pack_inv(match, mismatch), rec_phase, lane);
+                } else if (mine) {  // the call's direct share: int32 straight into the caller's pinned arrays
+                    put_result<true>(dir_score + p, ok ? sc : -1);
+                    put_result<true>(dir_end + p, ok ? en : -1);
+                }
+            }
         } else if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
@@ -1658,13 +1653,14 @@ static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStrea
         hipExtLaunchKernelGGL(uniform_kernel<W, KM, LAT, OM, IX>, dim3(blocks), dim3(256), 0, stream, g.ev_start,
                               g.ev_stop, 0, g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full,
                               g.match, g.mismatch, g.out_score, g.out_end, g.err_flag, g.heavy_ids, g.tile_flags,
-                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base, g.rho);
+                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base, g.rec_phase, g.rec_tiles, g.dir_score,
+                              g.dir_end);
         return;
     }
     uniform_kernel<W, KM, LAT, OM, IX><<<blocks, 256, 0, stream>>>(
         g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full, g.match, g.mismatch, g.out_score,
         g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base,
-        g.rho);
+        g.rec_phase, g.rec_tiles, g.dir_score, g.dir_end);
 }
 
 template <int W, int KM, bool LAT>
@@ -1697,7 +1693,7 @@ static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStrea
             }
             return false;
         case 3:
-            if constexpr (KM == 0 && !LAT) {  // tile records: throughput mode, int32 keys
+            if constexpr (KM == 0 && !LAT) {  // streamed tile records: throughput mode, int32 keys
                 launch_uniform_4<W, KM, LAT, 3>(g, blocks, stream);
                 return true;
             }
@@ -1802,8 +1798,9 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->host_out >= 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
-    if (g->host_out == 3 && (g->rs_log2 > 0 || g->lw > 254 || g->rho < 0 || g->rho > 255))
-        return hipErrorInvalidValue;  // tile records: throughput mode, j < 255, rho / 256 in [0, 1)
+    if (g->host_out == 3 && (g->rs_log2 > 0 || g->lw > 254 || g->rec_phase > 1 || g->rec_tiles < 0 ||
+                             (g->rec_tiles * 64 < g->n_pairs && (!g->dir_score || !g->dir_end))))
+        return hipErrorInvalidValue;  // streamed tile records: throughput mode, j <= 254, a phase bit
     if (g->ix_b16 && (g->lw <= 0 || g->key64 || g->rs_log2 > 0 || g->heavy_ids || !g->ix_d8 || !g->ix_base))
         return hipErrorInvalidValue;  // host-encoded lists: uniform throughput mode only
     if (g->lw > 0) {

@@ -21,7 +21,7 @@ ABI_VERSION = 3
 OVL_OK = 0
 ERRORS = {
     -1: "OVL_E_ARG", -2: "OVL_E_HIP", -3: "OVL_E_OOM", -4: "OVL_E_UNSUPPORTED",
-    -5: "OVL_E_RANGE", -6: "OVL_E_STATE", -7: "OVL_E_INDEX",
+    -5: "OVL_E_RANGE", -6: "OVL_E_STATE", -7: "OVL_E_INDEX", -8: "OVL_E_INTERNAL",
 }
 KERNELS = {0: "none", 1: "ungapped", 2: "dp", 3: "banded"}
 

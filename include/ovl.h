@@ -46,7 +46,8 @@ enum {
     OVL_E_UNSUPPORTED = -4,  /* read too long, >256 symbols, band at scores too large for int32 cells */
     OVL_E_RANGE = -5,        /* scoring magnitudes would overflow the int32 DP table */
     OVL_E_STATE = -6,        /* no resident reads (ovl_set_reads not called) */
-    OVL_E_INDEX = -7         /* a pair index is outside [0, n_reads) */
+    OVL_E_INDEX = -7,        /* a pair index is outside [0, n_reads) */
+    OVL_E_INTERNAL = -8      /* a streamed result record never completed although its kernel had finished */
 };
 
 enum {
@@ -100,20 +101,22 @@ int ovl_set_timing(ovl_ctx* ctx, int32_t on);
 int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 /* The scoring launches of the last host-array call made with timing on, in issue order: *out_n = count;
  * entry i < cap gives the device ordinal, the result sink (1 int32 stored into host memory; 2 packed 2 B/pair
- * into host staging, expanded by host threads; 0, HBM, only in ovl_score_device), the pairs and the launch's
+ * into host staging, expanded by host threads after the launch; 3 streamed tile records into host staging,
+ * expanded by host threads while the launch runs; 0, HBM, only in ovl_score_device), the pairs and the launch's
  * duration in ms (HIP events recorded by the kernel's own launch for ungapped chunks, else on its stream).
  * Any output pointer may be NULL. */
 int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs, double* ms,
                       int32_t* out_n);
 /* Link traffic of the last host-array scoring call (always recorded): link_bytes = pair-list bytes the
  * devices read from host memory + result bytes they stored there (ovl_last_results: 2 per pair in packed
- * chunks, 72 per 64 pairs plus 2 per escape in tile records, 8 per pair otherwise; the few packed pairs whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose results crossed packed and
- * were expanded on the host. */
+ * chunks and tile records, plus 4 per special pair of a tile record, 8 per pair otherwise; the few pairs of a
+ * 2 B/pair chunk whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose
+ * results crossed packed and were expanded on the host. */
 int ovl_last_transfer(const ovl_ctx* ctx, int64_t* link_bytes, int64_t* packed_pairs);
 /* The results' part of the last host-array call's link bytes (always recorded): result_bytes = what the kernels
- * stored into host memory for the results (8 per int32 pair, 2 per packed pair, 72 per tile record of 64 pairs
- * plus 2 per escaped pair); record_pairs = pairs that crossed as tile records (packed chunks in throughput mode);
- * escapes = those of them whose code could not hold their (end, mismatches) and crossed as 2-byte words. */
+ * stored into host memory for the results (8 per int32 pair, 2 per packed pair, 128 per streamed tile record of
+ * 64 pairs plus 4 per special pair); record_pairs = pairs that crossed as streamed tile records; escapes = the
+ * special pairs among them (a shorter read a inside b's window, or a bad pair), whose word travels apart. */
 int ovl_last_results(const ovl_ctx* ctx, int64_t* result_bytes, int64_t* record_pairs, int64_t* escapes);
 /* How the last host-array call's pair list reached the kernels (always recorded): in_place_pairs = pairs of
  * chunks the scoring kernel read in their compact encoding (b as uint16, a as tile deltas); decoded_pairs =

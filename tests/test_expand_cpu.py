@@ -22,14 +22,16 @@ def test_expand_variants_match_scalar(tmp_path):
 
 
 def test_tile_records_decode(tmp_path):
-    """The tile records of ovl_kernels.hip put_tile9 (sink 3: 9-bit codes around a mismatch-rate model, escapes
-    as OM 2 words): tests/c/expand9_test.cpp encodes random results with the host restatement of put_tile9 and
-    checks the scalar decoder and the widest this CPU runs give every (score, end) back."""
-    exe = tmp_path / "expand9_test"
+    """The streamed tile records of ovl_kernels.hip put_tile_rec (sink 3: 15-bit codes j(j + 1)/2 + X and a phase
+    bit per dword, special words apart): tests/c/rec_test.cpp checks every code, random tiles in both phases
+    through the scalar and (where this CPU runs it) AVX-512 decoders, the readiness test on incomplete records,
+    the zeroing of special words and a special word that never arrives."""
+    exe = tmp_path / "rec_test"
     r = subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(PKG, "csrc"),
-                        "-o", str(exe), os.path.join(ROOT, "tests", "c", "expand9_test.cpp")],
+                        "-o", str(exe), os.path.join(ROOT, "tests", "c", "rec_test.cpp")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.splitlines()[-1] == "ok"
+    lines = r.stdout.splitlines()
+    assert lines[-1] == "ok" and lines[0] == "checked codes", lines

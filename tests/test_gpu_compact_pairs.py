@@ -145,15 +145,16 @@ def test_one_shot_abi_call(oracle_mod, target):
         np.testing.assert_array_equal(e, re_)
 
 
-def test_compact_adaptive_share(oracle_mod, target):
-    """Host-list calls into pinned arrays keep their own adaptive direct share (the host also encodes the
-    list): exact results call after call, the packed part within 20-98 % of the pairs."""
-    from ovlgraph import OverlapEngine
+@pytest.mark.parametrize("pack", ["1", "2"])
+def test_compact_adaptive_share(oracle_mod, target, pack):
+    """Host-list calls into pinned arrays: 2-byte packing (OVL_PACK=1) keeps its own adaptive direct share (the
+    host also encodes the list), the packed part within 20-98 % of the pairs; streamed records (the default)
+    take every pair as records.  Exact results call after call."""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = target
     ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
     n = a.shape[0]
-    with OverlapEngine(0) as eng:
+    with _engine_env({"OVL_PACK": pack}) as eng:
         eng.set_reads(reads)
         out = (pinned_empty(n), pinned_empty(n))
         shares = []
@@ -163,7 +164,10 @@ def test_compact_adaptive_share(oracle_mod, target):
             np.testing.assert_array_equal(out[0], ref_s)
             np.testing.assert_array_equal(out[1], ref_e)
             shares.append(eng.last_transfer()["packed_pairs"] / n)
-        assert all(0.19 <= x <= 0.99 for x in shares), shares
+        if pack == "1":
+            assert all(0.19 <= x <= 0.99 for x in shares), shares
+        else:
+            assert all(x == 1.0 for x in shares), shares
 
 
 def _pair_link_bytes(eng, n):
@@ -236,18 +240,27 @@ def test_ix_tile_jumps_fall_back(oracle_mod, target):
         eng.close()
 
 
-def test_ix_small_call_latency_mode(oracle_mod, target):
-    """100 K pairs (compact, but few enough for the latency-mode launch, which takes the decoded list)."""
+@pytest.mark.parametrize("pack", ["1", "2"])
+def test_ix_small_call_latency_mode(oracle_mod, target, pack):
+    """100 K pairs, compact: with 2-byte packing (OVL_PACK=1) few enough for the latency-mode launch, which takes
+    the decoded list (runs: < 3 B per pair); streamed records (the default) always launch in throughput mode,
+    which reads the list in place (3 B per pair + 4 B per tile)."""
     reads, a, b = target
     a, b = a[:100_000], b[:100_000]
+    n = a.shape[0]
     ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
-    eng = _engine_env({})
+    eng = _engine_env({"OVL_PACK": pack})
     try:
         eng.set_reads(reads)
         s, e = eng.score(a, b)
         np.testing.assert_array_equal(s, ref_s)
         np.testing.assert_array_equal(e, ref_e)
-        assert _pair_link_bytes(eng, a.shape[0]) < 3 * a.shape[0]
+        if pack == "1":
+            assert _pair_link_bytes(eng, n) < 3 * n
+            assert eng.last_pair_list() == {"in_place_pairs": 0, "decoded_pairs": n}
+        else:
+            assert eng.last_pair_list() == {"in_place_pairs": n, "decoded_pairs": 0}
+            assert _pair_link_bytes(eng, n) == 3 * n + 4 * ((n + 63) // 64)
     finally:
         eng.close()
 

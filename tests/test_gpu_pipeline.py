@@ -101,7 +101,8 @@ def test_pipeline_host_list_pinned_and_pageable(oracle_mod, cfg2, cfg2_ref, chun
         eng.close()
 
 
-@pytest.mark.parametrize("pack,pct", [("1", "25"), ("1", "0"), ("1", "60"), ("1", "100"), ("0", "25")])
+@pytest.mark.parametrize("pack,pct", [("1", "25"), ("1", "0"), ("1", "60"), ("1", "100"), ("0", "25"),
+                                      ("2", "25"), ("2", "0"), ("2", "100")])
 @pytest.mark.parametrize("chunk", ["0", "1000"])
 def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk):
     """Results cross the link packed (uint16 score | end << 8) and are expanded on the host: pinned,
@@ -139,7 +140,12 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
             else:
                 want = n
             assert x["packed_pairs"] == want, (name, x)
-            assert x["link_bytes"] == 8 * n + 2 * want + 8 * (n - want), (name, x)
+            if pack == "2":  # streamed records: 128 B per tile of each chunk plus 4 per special pair
+                r = eng.last_transfer()
+                assert r["record_pairs"] == want and r["result_bytes"] >= 2 * want + 8 * (n - want), (name, r)
+                assert x["link_bytes"] == 8 * n + r["result_bytes"], (name, x, r)
+            else:
+                assert x["link_bytes"] == 8 * n + 2 * want + 8 * (n - want), (name, x)
         # the resident candidate list into a misaligned pageable pair of arrays
         eng.candidates(5)
         out = (np.empty(a.shape[0] + 1, np.int32)[1:], np.empty(a.shape[0], np.int32))
@@ -165,13 +171,12 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
 @pytest.mark.parametrize("pack", ["1", "2"])
 @pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
 def test_tile_records(oracle_mod, cfg2, pack, scoring):
-    """Packed chunks in throughput mode cross the link as tile records (OVL_PACK=2, the default: ovl_kernels.hip
-    put_tile9, 9-bit codes around a mismatch-rate model, escapes as 2-byte words; OVL_PACK=1 keeps 2 bytes per
-    pair): cfg2's list tiled six times (731 K pairs, so the packed chunks run in throughput mode) with bad pairs,
-    scored under scorings that move the mismatch counts far from the model (every such pair an escape: match ==
-    mismatch, mismatch > match), into pinned, pageable and misaligned arrays, all packed and with a direct share;
-    every (score, end) equals the oracle's, and the call's link bytes are the records' (72 per tile + 2 per
-    escape) or OM 2's 2 per pair."""
+    """Packed chunks cross the link as streamed tile records (OVL_PACK=2, the default: ovl_kernels.hip
+    put_tile_rec, 15-bit codes and a phase bit per dword, expanded by host threads while the kernel runs;
+    OVL_PACK=1 keeps 2 bytes per pair expanded after each chunk): cfg2's list tiled six times (731 K pairs) with
+    bad pairs, under scorings with match == mismatch and mismatch > match, into pinned, pageable and misaligned
+    arrays, all packed and with a direct share; every (score, end) equals the oracle's, and the call's link
+    bytes are the records' (128 per tile + 4 per special pair) or 2 per pair."""
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a0, b0 = cfg2
@@ -193,34 +198,63 @@ def test_tile_records(oracle_mod, cfg2, pack, scoring):
                     "pageable": (np.empty(n, np.int32), np.empty(n, np.int32)),
                     "misaligned": (np.empty(n + 1, np.int32)[1:], np.empty(n + 3, np.int32)[3:])}
             for name, out in outs.items():
-                out[0][:] = 7
-                out[1][:] = 7
-                with pytest.raises(OvlError, match="OVL_E_INDEX"):
-                    eng.score(a[:n], b[:n], match, mismatch, out=out)
-                np.testing.assert_array_equal(out[0], ref_s[:n], err_msg=f"{name} pct {pct}")
-                np.testing.assert_array_equal(out[1], ref_e[:n], err_msg=f"{name} pct {pct}")
-                x = eng.last_transfer()
-                np_ = x["packed_pairs"]
-                assert np_ > 0 and x["link_bytes"] == 8 * n + x["result_bytes"], x
-                res = x["result_bytes"] - 8 * (n - np_)  # the packed part's result bytes
-                if pack == "1":
-                    assert res == 2 * np_ and x["record_pairs"] == 0, (name, x)
-                else:
-                    assert x["record_pairs"] == np_, (name, x)  # every packed chunk in throughput mode
-                    tiles = (np_ + 63) // 64
-                    assert res == 72 * tiles + 2 * x["escapes"], (name, x)
-                    if scoring == (10, -1):  # the model's own scoring: most pairs coded in 9 bits
-                        assert x["escapes"] < 0.25 * np_, (name, x)
+                for rep in range(2):  # (the second call reuses the slot in the other phase)
+                    out[0][:] = 7
+                    out[1][:] = 7
+                    with pytest.raises(OvlError, match="OVL_E_INDEX"):
+                        eng.score(a[:n], b[:n], match, mismatch, out=out)
+                    np.testing.assert_array_equal(out[0], ref_s[:n], err_msg=f"{name} pct {pct} rep {rep}")
+                    np.testing.assert_array_equal(out[1], ref_e[:n], err_msg=f"{name} pct {pct} rep {rep}")
+                    x = eng.last_transfer()
+                    np_ = x["packed_pairs"]
+                    assert np_ > 0 and x["link_bytes"] == 8 * n + x["result_bytes"], x
+                    res = x["result_bytes"] - 8 * (n - np_)  # the packed part's result bytes
+                    if pack == "1":
+                        assert res == 2 * np_ and x["record_pairs"] == 0, (name, x)
+                    else:
+                        assert x["record_pairs"] == np_, (name, x)
+                        tiles = (np_ + 63) // 64
+                        assert res == 128 * tiles + 4 * x["escapes"], (name, x)
+                        assert x["escapes"] >= len(bad) - 1, (name, x)  # (the bad pairs are specials)
+        finally:
+            eng.close()
+
+
+def test_tile_records_phases(oracle_mod, cfg2, cfg2_ref):
+    """The staging slots' phase invariant over calls of changing sizes (ovl_api.cpp issue_chunk /
+    stream_chunk): one engine scores prefixes of cfg2's list that grow, shrink and repeat, as one chunk and in
+    many chunks (slot reuse in both phases, partial last tiles), each call exact against the oracle; a call
+    that leaves stale records of a larger earlier call above its own tiles must not let the next larger call
+    read them as its own."""
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = cfg2
+    N = a.shape[0]
+    sizes = [N, N // 3 + 17, N, N // 2 + 1, 70_000, N - 64, N // 3 + 17, N, 65_536, N]
+    for chunk in ("0", "40000"):
+        eng = _engine_env({"OVL_PACK": "2", "OVL_PACK_MIN": "0", "OVL_PACK_DIRECT_PCT": "0", "OVL_PIPE_CHUNK": chunk,
+                           "OVL_PAIRS_COMPACT": "0"})
+        try:
+            eng.set_reads(reads)
+            out = (pinned_empty(N), pinned_empty(N))
+            for i, n in enumerate(sizes):
+                out[0][:] = -7
+                out[1][:] = -7
+                eng.score(a[:n], b[:n], out=(out[0][:n], out[1][:n]))
+                np.testing.assert_array_equal(out[0][:n], cfg2_ref[0][:n], err_msg=f"chunk {chunk} call {i}")
+                np.testing.assert_array_equal(out[1][:n], cfg2_ref[1][:n], err_msg=f"chunk {chunk} call {i}")
+                assert eng.last_transfer()["record_pairs"] == n, (chunk, i)
         finally:
             eng.close()
 
 
 def test_packed_adaptive_share(oracle_mod, cfg2, cfg2_ref):
-    """The direct share of packed calls into pinned arrays adapts call by call (no OVL_PACK_DIRECT_PCT):
-    every call's results stay exact and the packed part stays within its bounds (50-98 % of the pairs)."""
+    """The direct share of 2-byte packed calls into pinned arrays (OVL_PACK=1) adapts call by call (no
+    OVL_PACK_DIRECT_PCT): every call's results stay exact and the packed part stays within its bounds (50-98 % of
+    the pairs).  (Streamed records, the default, have no direct share unless OVL_PACK_DIRECT_PCT sets one:
+    test_step_transport_vs_oracle.)"""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
-    eng = _engine_env({"OVL_PACK_MIN": "0"})
+    eng = _engine_env({"OVL_PACK_MIN": "0", "OVL_PACK": "1"})
     try:
         eng.set_reads(reads)
         eng.candidates(5)
@@ -615,15 +649,17 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
 
 # ----------------------------------------------------------------------------- the step's transport
 @pytest.mark.parametrize("cfg", ["target", "cfg3"])
-def test_step_transport_vs_oracle(oracle_mod, cfg):
-    """Whole resident list into pinned arrays (the bench step: packed chunks expanded on the host plus a direct
-    int32 chunk) equals the oracle call after call, into reused and fresh arrays; ovl_last_transfer counts
-    2 B per packed pair and 8 B per direct pair."""
+@pytest.mark.parametrize("pct", [None, "15"])
+def test_step_transport_vs_oracle(oracle_mod, cfg, pct):
+    """Whole resident list into pinned arrays (the bench step: one launch whose streamed tile records host threads
+    expand while it runs; with OVL_PACK_DIRECT_PCT its last tiles stored as int32 straight into the arrays) equals
+    the oracle call after call, into reused and fresh arrays; ovl_last_transfer counts 128 B per record tile, 4 B
+    per special pair and 8 B per direct pair."""
     from ovlgraph.candidates import dedup_reads
     from ovlgraph.hostmem import pinned_empty
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
-    eng = _engine_env({})
+    eng = _engine_env({"OVL_PACK_DIRECT_PCT": pct} if pct else {})
     try:
         eng.set_reads(reads)
         a, b = eng.candidates(5)
@@ -637,12 +673,12 @@ def test_step_transport_vs_oracle(oracle_mod, cfg):
             np.testing.assert_array_equal(out[0], ref_s, err_msg=f"call {it}")
             np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
             x = eng.last_transfer()
-            assert 0 < x["packed_pairs"] < n, x
-            # (no pair list crosses: the link bytes are the results', tile records for the packed chunks in
-            # throughput mode -- 72 B per 64 pairs and 2 B per escape -- 2 B per other packed pair, 8 B per direct)
+            assert (0 < x["packed_pairs"] < n) if pct else x["packed_pairs"] == n, x
+            # (no pair list crosses: the link bytes are the results', tile records for the packed pairs -- 128 B
+            # per 64 pairs and 4 B per special pair -- and 8 B per direct pair)
             assert x["link_bytes"] == x["result_bytes"], x
             q = x["record_pairs"]
-            assert x["result_bytes"] == 72 * ((q + 63) // 64) + 2 * x["escapes"] + 2 * (x["packed_pairs"] - q) + \
+            assert x["result_bytes"] == 128 * ((q + 63) // 64) + 4 * x["escapes"] + 2 * (x["packed_pairs"] - q) + \
                 8 * (n - x["packed_pairs"]), x
         fresh = eng.score_candidates()
         np.testing.assert_array_equal(fresh[0], ref_s)
