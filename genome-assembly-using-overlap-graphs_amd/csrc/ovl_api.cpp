@@ -124,7 +124,9 @@ constexpr int64_t kResidentCopyMax = int64_t(256) << 20;
 // streamed tile records: tiles per group of the expansion (groups go round-robin to the pool's parts, so every
 // part has records arriving while the kernel runs), and pairs per pipeline chunk at most
 constexpr int64_t kRecGroupTiles = 8;
-constexpr size_t kRecSkip = 32;  // incomplete records a pass of the expansion skips before it polls again
+// incomplete records a pass of the expansion skips before it polls again (4 / 32 / all of a part's: N = 1 step
+// 0.168 / 0.155 / 0.167 ms, N = 8 0.050 / 0.049 / 0.052, profiles/r05_rec_skip_ab.json)
+constexpr size_t kRecSkip = 32;
 constexpr int64_t kRecChunk = int64_t(1) << 22;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
