@@ -649,8 +649,8 @@ def pair_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 SINKS = {0: "int32 results in HBM (copy-engine transfer after)", 1: "int32 results stored into pinned host memory",
          2: "packed 2 B/pair results stored into pinned host staging (host threads expand)",
-         3: "streamed tile records (10-bit codes relative to the tile, a phase bit per dword: 92 B per 64 pairs + 4 B "
-            "per escape) stored into pinned host staging, expanded by host threads while the kernel runs"}
+         3: "streamed tile records (15-bit codes + a phase bit per dword: 128 B per 64 pairs + 4 B per special pair) "
+            "stored into pinned host staging, expanded by host threads while the kernel runs"}
 
 
 def kernel_name(w, sink: int, pairs: int) -> str:
@@ -666,7 +666,7 @@ def kernel_name(w, sink: int, pairs: int) -> str:
 
 
 # result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed; 3
-# streamed tile records: 92 B per 64 pairs plus 4 B per escape, measured per call -- in_step_rooflines)
+# streamed tile records: 128 B per 64 pairs plus 4 B per special pair, measured per call -- in_step_rooflines)
 LINK_BYTES_PER_PAIR = {0: 0, 1: 8, 2: 2}
 # a kernel's stores into pinned host memory, measured on the box (profiles/r02_pcie_write.txt)
 LINK_PEAK_GBS = 55.3

@@ -84,10 +84,13 @@ struct Knobs {
     int32_t lane_prof = 1;        // OVL_LANE_PROF=0: compare/select scores instead of the byte profile (tests)
     int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
-    int32_t pack = 2;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
-                                  // form holds; 1 packed as 2 bytes per pair, expanded chunk by chunk after each
-                                  // chunk's kernel; 2 (default) as streamed tile records (ovl_kernels.hip
-                                  // put_tile_rec), expanded by host threads while the kernel still runs (tests)
+    int32_t pack = 1;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
+                                  // form holds; 1 (default) packed as 2 bytes per pair, expanded chunk by chunk
+                                  // after each chunk's kernel, a last chunk stored as int32 meanwhile; 2 as
+                                  // streamed tile records (ovl_kernels.hip put_tile_rec), one launch whose records
+                                  // host threads expand while it runs.  Same box, per-rank steps of the target list
+                                  // at N = 1 / 2 / 8, 1 against 2: 0.135 / 0.088 / 0.045 against 0.144 / 0.081 /
+                                  // 0.050 ms; cfg4 and cfg3 within 3 % (profiles/r05_stream_vs_packed_ab.json)
     int64_t pack_min = 1 << 16;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
                                   // (64 K: a 250 K-pair shard -- N = 8 at the target point -- 0.057 -> 0.054 ms)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
@@ -174,7 +177,7 @@ struct Dev {
     // [0, rec_hw) carries it; the dwords above are still zero from the allocation) and its high-water mark
     uint8_t rec_phase[kSlots] = {};
     int64_t rec_hw[kSlots] = {};
-    // ... whether its escape words are known zero (false after a chunk of another sink used its staging), the escape
+    // ... whether its special words are known zero (false after a chunk of another sink used its staging), the special
     // words its last record chunk read (zeroed once that chunk's kernel has ended, stream_chunk), and the rotation
     // of record chunks over the slots (consecutive record chunks take consecutive slots)
     bool rec_clean[kSlots] = {true, true, true};
@@ -953,11 +956,11 @@ struct Job {
     std::vector<uint8_t> kexact; // timing: chunk k's kernel recorded its own start / end (k_ev)
     std::vector<uint8_t> om;     // chunk k's result sink (OvlUngappedArgs::host_out): 1 int32, 2 packed, 3 records
     std::vector<uint8_t> slot;   // chunk k's staging slot: k % kSlots, or the next in Dev::rec_next's rotation (records)
-    int64_t n_esc = 0;           // escapes seen by the expansion of the record chunks
+    int64_t n_esc = 0;           // special pairs seen by the expansion of the record chunks
     int64_t drained = 0;         // chunks [0, drained) are drained (run_pipeline)
     int64_t rec_end = 0;         // packed pairs [0, rec_end); streamed records: the pairs from rec_end on are
                                  // stored as int32 by the last chunk's launch (its tiles from rec_end / 64)
-    int64_t n_bad = 0;           // bad pairs seen by the expansion of the record chunks (their escape words)
+    int64_t n_bad = 0;           // bad pairs seen by the expansion of the record chunks (their special words)
     bool ended = true;           // every launch of the job is known finished (false: a streamed chunk returned
                                  // on its records alone; run_pipeline then needs no stream synchronisation)
 };
@@ -1070,7 +1073,7 @@ int setup_job(const Call& C, Job& J) {
     if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
     if (need_out && !d->st_out) {
         HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
-        // (streamed records: every record dword, escape slot and special word starts at zero, phase 0)
+        // (streamed records: every record dword and special word starts at zero, phase 0)
         memset(d->st_out, 0, (size_t)kSlots * 2 * (size_t)d->st_cap * sizeof(int32_t));
         for (int i = 0; i < kSlots; ++i) {
             d->rec_phase[i] = 0;
@@ -1311,7 +1314,7 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     d->out_mode = J.om[(size_t)k];
     if (staged_out && d->out_mode != 3) d->rec_clean[slot] = false;  // (its stores leave values in the slot)
     if (d->out_mode == 3 && (!d->rec_clean[slot] || !d->rec_dirty[slot].empty())) {
-        // the slot's escape words are not known zero -- another sink's chunk used it, or the record chunk before
+        // the slot's special words are not known zero -- another sink's chunk used it, or the record chunk before
         // found no later chunk to clear them (stream_chunk): once its writers have ended, zero them here
         HIPCHK(d, hipStreamSynchronize(d->stream));
         if (!d->rec_clean[slot]) {
@@ -1330,8 +1333,7 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
         const int64_t nt = (std::max<int64_t>(0, std::min(n, J.rec_end - off)) + 63) / 64;
         uint32_t* rec = reinterpret_cast<uint32_t*>(d->st_out + so);
         if (nt > d->rec_hw[slot]) {
-            if (d->rec_phase[slot])  // (the phase dwords 0..22 of each record; its escape slots stay zero)
-                for (int64_t t = d->rec_hw[slot]; t < nt; ++t) std::fill(rec + 32 * t, rec + 32 * t + 23, 0x80000000u);
+            if (d->rec_phase[slot]) std::fill(rec + 32 * d->rec_hw[slot], rec + 32 * nt, 0x80000000u);
             d->rec_hw[slot] = nt;
         }
         d->rec_phase_next = d->rec_phase[slot] ^ 1u;
@@ -1369,15 +1371,16 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
 // one round of waves land in any order), and poll when a pass found nothing.
 //   The call needs the kernel's end only when the chunk has direct tiles (int32 stores the host cannot see
 // arrive) or timing is on (`need_end`): then part 0 -- the calling thread -- waits for the chunk's event after
-// its own tiles.  Otherwise the results are complete once every record is read: bad pairs arrive as escape
+// its own tiles.  Otherwise the results are complete once every record is read: bad pairs arrive as special
 // words (the kernel sets no host flag for record tiles), nothing of this call is left to land in host memory,
 // and the stream orders the next call's launches after this kernel, so the call returns ~5 us before the
 // kernel's completion signal could be seen (tools/launch_probe.hip).
 //   A kernel that fails must not leave a part polling forever: part 0 queries the event while it polls, any
 // part queries it after kLostPolls fruitless polls, and a record still incomplete well after the kernel has
-// finished -- which the kernel's end makes impossible -- ends the call with OVL_E_INTERNAL.  The escape words
-// read are zeroed again, and tiles above this chunk's that an earlier, larger chunk left in this slot get this
-// launch's phase, so the slot's next launch finds every dword it does not write yet in the other phase.
+// finished -- which the kernel's end makes impossible -- ends the call with OVL_E_INTERNAL.  The special words
+// read are zeroed during the next record chunk's drain (below), and tiles above this chunk's that an earlier,
+// larger chunk left in this slot get this launch's phase, so the slot's next launch finds every dword it does not
+// write yet in the other phase.
 int stream_chunk(const Call& C, Job& J, int64_t k) {
     constexpr uint32_t kLostPolls = 1u << 14;
     Dev* d = J.d;
@@ -1401,7 +1404,7 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
     const hipEvent_t ev = d->ev_k[slot];
     // 0 the kernel may still run, 1 it has finished, 2 error (kernel failure or an incomplete record)
     std::atomic<int> state{0};
-    std::atomic<int64_t> escapes{0}, bad{0};
+    std::atomic<int64_t> specials{0}, bad{0};
     std::atomic<hipError_t> herr{hipSuccess};
     const auto query = [&] {  // the kernel's event; false on a failure
         const hipError_t q = hipEventQuery(ev);
@@ -1419,7 +1422,7 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
     const std::vector<size_t> parts = pool.cut(64 * 64, 64);
     const int64_t P = (int64_t)parts.size() - 1;
     const int64_t ngroups = (nt + kRecGroupTiles - 1) / kRecGroupTiles;
-    // The escape words the record chunk before this one read (the previous slot of the rotation) are zeroed here,
+    // The special words the record chunk before this one read (the previous slot of the rotation) are zeroed here,
     // once this chunk's kernel is seen running (a record of it complete, or its end): the stream ran that chunk's
     // kernel to its end first, and the slot is not written again until the chunk after the next, issued after this
     // drain.  A host store into a line of a kernel that still runs can be lost (ovl_expand.h).
@@ -1431,7 +1434,7 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
     pool.parallel_parts(parts, [&](size_t i, size_t, size_t) {
         uint32_t polls = 0;  // fruitless polls in a row
         int64_t after = 0;   // polls since the kernel was seen finished
-        // one poll of an incomplete record or escape word: false ends the part (error)
+        // one poll of an incomplete record or special word: false ends the part (error)
         const auto wait = [&]() -> bool {
             _mm_pause();
             const int st = state.load(std::memory_order_acquire);
@@ -1457,10 +1460,12 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
         int64_t m = 0;
         int nbad = 0;
         bool first = i == 0 && g_trace;
-        std::vector<uint32_t*>& taken = taken_by[i];
+        // (the special words read, in a part-local vector handed over at the end: the parts' vector objects share
+        // cache lines, and updating them per tile from every thread measured ~5x slower expansion)
+        std::vector<uint32_t*> taken;
         uint32_t* tk[64];
         bool cleared = !clear_prev;
-        const auto clear_share = [&] {  // (this part's share of the previous chunk's escape words)
+        const auto clear_share = [&] {  // (this part's share of the previous chunk's special words)
             const size_t len = clear.size(), lo = len * i / (size_t)P, hi = len * (i + 1) / (size_t)P;
             for (size_t q = lo; q < hi; ++q) *(volatile uint32_t*)clear[q] = 0u;
             cleared = true;
@@ -1475,15 +1480,11 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
                 if (a512 && cnt == 64) {
                     bool ready = false;
                     got = ovl_expand::rec_tile_avx512(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, phase, al, &ready,
-                                                      &nbad, tk, wait);
+                                                      &nbad, tk);
                     if (!ready) got = -2;
                 } else {
-                    got = ovl_expand::rec_tile_ready_scalar(r, phase)
-                              ? ovl_expand::rec_tile_scalar(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, cnt, &nbad,
-                                                            tk, wait)
-                              : -2;
+                    got = ovl_expand::rec_tile_scalar(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, cnt, phase, &nbad, tk);
                 }
-                if (got == -1) return;  // (state 2: the caller reports it)
                 if (got >= 0) {
                     m += got;
                     ++took;
@@ -1515,8 +1516,9 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
                 return;
             }
         }
-        escapes.fetch_add(m, std::memory_order_relaxed);
+        specials.fetch_add(m, std::memory_order_relaxed);
         bad.fetch_add(nbad, std::memory_order_relaxed);
+        taken_by[i] = std::move(taken);
         if (i == 0 && need_end) {  // the kernel's end (its event): direct tiles, timing
             if (g_trace) g_trace->mark('p', k);
             while (state.load(std::memory_order_acquire) == 0 && query()) _mm_pause();
@@ -1524,7 +1526,7 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
     });
     _mm_sfence();
     if (state.load() == 2) {
-        // the slot's dwords and escape words are in no known state: reallocated (zeroed) by the next call
+        // the slot's dwords and special words are in no known state: reallocated (zeroed) by the next call
         (void)hipStreamSynchronize(d->stream);
         free_staging(d->st_out);
         d->st_cap = 0;
@@ -1533,12 +1535,11 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
                                          hipGetErrorString(e));
         return fail(d, OVL_E_INTERNAL, "a result record was incomplete after its kernel finished");
     }
-    for (int64_t t = nt; t < d->rec_hw[slot]; ++t)  // (the phase dwords only: the escape slots stay zero)
-        for (int w = 0; w < 23; ++w) rec[32 * t + w] ^= 0x80000000u;
+    for (int64_t w = 32 * nt; w < 32 * d->rec_hw[slot]; ++w) rec[w] ^= 0x80000000u;
     d->rec_phase[slot] = (uint8_t)phase;
     if (clear_prev) clear.clear();
     for (auto& v : taken_by) d->rec_dirty[slot].insert(d->rec_dirty[slot].end(), v.begin(), v.end());
-    J.n_esc += escapes.load();
+    J.n_esc += specials.load();
     J.n_bad += bad.load();
     J.ended = need_end;  // (the stream's earlier launches end before this chunk's)
     return OVL_OK;
@@ -1710,10 +1711,10 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         if (n <= 0) continue;
         const int64_t np = J.n_packed ? std::min(J.rec_end, J.cb[(size_t)J.n_packed]) : 0;
         packed += np;
-        int64_t res = 8 * (n - np);  // results: int32 pairs, 2 bytes per packed pair, 92 per record + escapes
+        int64_t res = 8 * (n - np);  // results: int32 pairs, 2 bytes per packed pair, 128 per record + specials
         for (int64_t k = 0; k < J.n_packed; ++k) {
             const int64_t nk = std::min(J.cb[(size_t)k + 1], np) - std::min(J.cb[(size_t)k], np);
-            res += J.om[(size_t)k] == 3 ? 92 * ((nk + 63) / 64) : 2 * nk;
+            res += J.om[(size_t)k] == 3 ? 128 * ((nk + 63) / 64) : 2 * nk;
             if (J.om[(size_t)k] == 3) rec += nk;
         }
         res += 4 * J.n_esc;

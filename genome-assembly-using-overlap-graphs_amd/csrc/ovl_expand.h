@@ -12,8 +12,6 @@
 #pragma once
 
 #include <immintrin.h>
-
-#include <algorithm>
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -182,161 +180,134 @@ __attribute__((target("avx512f,avx512bw"))) inline void expand_avx512(int32_t* s
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Streamed tile records (ovl_kernels.hip put_tile_rec, sink 3): tile t's record is the 128-byte slot r = rec + 32 t,
-//   r[0]       phase << 31 | nesc << 16 | rho << 8 | jmax
-//   r[1 + w]   phase << 31 | c[w + 44] << 20 | c[w + 22] << 10 | c[w]       (w < 22: pair l's code in dword
-//              1 + l % 22, field l / 22)
-//   r[23 + e]  escape e (e < 9, in lane order); escapes from the tenth on in the special word sp[l]
-// Code c != 1023: j = jmax - (c >> 5), X = ((j * rho) >> 8) + (c & 31) - 16, score = match*j + (mismatch - match)*X.
-// c = 1023: the escape word v -- 0xFFFFFFFF a bad pair (-1, -1); else j = v >> 16 & 0xFF, X = v >> 8 & 0xFF,
-// n = v & 0xFF, L = min(j, n), score = match*L + (mismatch - match)*X.  Escape words are zero until they land: the
-// decoders report every escape word they read (`taken`), and the caller zeroes them once the kernel that wrote them
-// has ended (ovl_api.cpp stream_chunk) -- a host store into a line of a running kernel's records was measured to
-// come back with the device's value (escape slots zeroed on the box while their kernel ran were found nonzero
-// again afterwards, ~1 in 2,000 escapes at cfg3).  A record's codes are complete when dwords 0..22 carry the
-// launch's phase (rec_tile_ready_scalar).
+// Streamed tile records (ovl_kernels.hip put_tile_rec, sink 3): tile t's record is 32 dwords at r = rec + 32 t,
+//   r[w] = phase << 31 | c[w + 32] << 15 | c[w]    (c[l]: the 15-bit code of the tile's pair l)
+// c = j(j + 1)/2 + X (end j, X mismatches over L = j compared bases): score = match*j + (mismatch - match)*X.
+// c = 0x7FFF: the pair's special word sp[l] holds it --
+//   1 << 31 | j << 16 | X << 8 | n: score = match*n + (mismatch - match)*X, end j;  0xFFFFFFFF: (-1, -1).
+// A record is complete when every dword's bit 31 is the launch's phase (rec_tile_ready_scalar).  A special word is
+// zero until it lands: the decoders take a tile only once all of its special words have landed, report the words
+// they read (`taken`), and the caller zeroes them once the kernel that wrote them has ended (ovl_api.cpp
+// stream_chunk) -- a host store into a line that a running kernel writes was measured to come back with the
+// device's value (escape words zeroed on the box while their kernel ran were found nonzero again, ~1 in 2,000 at
+// cfg3, round 5).  j from c: the largest j with j(j + 1)/2 <= c is floor((sqrt(8c + 1) - 1) / 2), exact in float for
+// c < 2^15 (8c + 1 is a perfect square exactly when X = 0, and otherwise lies >= 1 from one, far above float's
+// error at 2^18).
+
+constexpr uint32_t kRecSpecial = 0x7FFFu;
 
 struct RecK {
     int32_t match, mismatch;
 };
 
-inline void rec_decode_code(uint32_t c, uint32_t jmax, uint32_t rho, const RecK& k, int32_t& s, int32_t& e) {
-    const int32_t j = (int32_t)jmax - (int32_t)(c >> 5);
-    const int32_t x = (int32_t)(((uint32_t)j * rho) >> 8) + (int32_t)(c & 31u) - 16;
-    s = k.match * j + (k.mismatch - k.match) * x;
-    e = j;
+inline void rec_decode_code(uint32_t c, const RecK& k, int32_t& s, int32_t& e) {
+    const uint32_t j = (uint32_t)(int32_t)((__builtin_sqrtf((float)(8 * c + 1)) - 1.0f) * 0.5f);
+    const int32_t x = (int32_t)(c - (j * (j + 1) >> 1));
+    s = k.match * (int32_t)j + (k.mismatch - k.match) * x;
+    e = (int32_t)j;
 }
 
-// an escape word (non-zero) -> (score, end)
-inline void rec_decode_escape(uint32_t v, const RecK& k, int32_t& s, int32_t& e) {
+// a special word (non-zero) -> (score, end)
+inline void rec_decode_special(uint32_t v, const RecK& k, int32_t& s, int32_t& e) {
     if (v == 0xFFFFFFFFu) {
         s = e = -1;
         return;
     }
     const int32_t j = (int32_t)(v >> 16 & 0xFFu), x = (int32_t)(v >> 8 & 0xFFu), n = (int32_t)(v & 0xFFu);
-    s = k.match * (j < n ? j : n) + (k.mismatch - k.match) * x;
+    s = k.match * n + (k.mismatch - k.match) * x;
     e = j;
 }
 
-// dwords 0..22 of the record carry `phase` in bit 31
+// all 32 dwords of the record carry `phase` in bit 31
 inline bool rec_tile_ready_scalar(const uint32_t* r, uint32_t phase) {
     const volatile uint32_t* v = r;
-    for (int w = 0; w < 23; ++w)
+    for (int w = 0; w < 32; ++w)
         if ((v[w] >> 31) != phase) return false;
     return true;
 }
 
-// Waits for escape word *w (spinning while `wait` says to) and decodes it; a bad pair adds 1 to *bad.  False if
-// `wait` gave up first.
-template <typename Wait>
-inline bool rec_take_escape(uint32_t* w, const RecK& k, int32_t& s, int32_t& e, int* bad, Wait&& wait) {
-    volatile uint32_t* v = w;
-    uint32_t x;
-    while ((x = *v) == 0u)
-        if (!wait()) return false;
-    rec_decode_escape(x, k, s, e);
-    *bad += x == 0xFFFFFFFFu;
-    return true;
-}
-
-
-// escape e of a tile whose lane is l: an inline slot of the record, or the lane's special word
-inline uint32_t* rec_escape_slot(uint32_t* r, uint32_t* sp, int e, int l) { return e < 9 ? r + 23 + e : sp + l; }
-
-// one complete record's pairs [0, cnt) (cnt <= 64) into s / e (scalar); the escapes' count (their words in
-// taken[0 ..), the bad pairs among them added to *bad), or -1 if one never came
-template <typename Wait>
-inline int rec_tile_scalar(int32_t* s, int32_t* e, uint32_t* r, uint32_t* sp, const RecK& k, size_t cnt, int* bad,
-                           uint32_t** taken, Wait&& wait) {
+// One record's pairs [0, cnt) (cnt <= 64) into s / e (scalar) once the record and all its special words have
+// landed: the specials' count (their words in taken[0 ..), the bad pairs among them added to *bad), or -2 (nothing
+// written) while something has not.
+inline int rec_tile_scalar(int32_t* s, int32_t* e, const uint32_t* r, uint32_t* sp, const RecK& k, size_t cnt,
+                           uint32_t phase, int* bad, uint32_t** taken) {
+    if (!rec_tile_ready_scalar(r, phase)) return -2;
     const volatile uint32_t* v = r;
-    const uint32_t hdr = v[0], jmax = hdr & 0xFFu, rho = hdr >> 8 & 0xFFu;
+    uint32_t wv[64];
     int m = 0;
+    for (size_t l = 0; l < cnt; ++l) {  // (every special word first: a tile is taken whole or not at all)
+        if (((v[l & 31] >> (l < 32 ? 0 : 15)) & 0x7FFFu) != kRecSpecial) continue;
+        taken[m] = sp + l;
+        if ((wv[m] = *(volatile uint32_t*)taken[m]) == 0u) return -2;
+        ++m;
+    }
+    int q = 0;
     for (size_t l = 0; l < cnt; ++l) {
-        const uint32_t c = (v[1 + l % 22] >> (10 * (l / 22))) & 0x3FFu;
-        if (c == 1023u) {
-            uint32_t* w = rec_escape_slot(r, sp, m, (int)l);
-            if (!rec_take_escape(w, k, s[l], e[l], bad, wait)) return -1;
-            taken[m++] = w;
+        const uint32_t c = (v[l & 31] >> (l < 32 ? 0 : 15)) & 0x7FFFu;
+        if (c == kRecSpecial) {
+            rec_decode_special(wv[q], k, s[l], e[l]);
+            *bad += wv[q++] == 0xFFFFFFFFu;
         } else {
-            rec_decode_code(c, jmax, rho, k, s[l], e[l]);
+            rec_decode_code(c, k, s[l], e[l]);
         }
     }
     return m;
 }
 
-// pair l = 16 q + i of a record: its code in dword 1 + l % 22 (kRecIdx, an index into the two 16-dword halves), field
-// l / 22 (kRecShift, the bit offset)
-alignas(64) constexpr int32_t kRecIdx[4][16] = {
-    {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16},
-    {17, 18, 19, 20, 21, 22, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10},
-    {11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 1, 2, 3, 4},
-    {5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20}};
-alignas(64) constexpr int32_t kRecShift[4][16] = {
-    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {0, 0, 0, 0, 0, 0, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10},
-    {10, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10, 20, 20, 20, 20},
-    {20, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20, 20}};
-
-// AVX-512: readiness check and decode of one full record (64 pairs) from the same two loads; *ready = false
-// (nothing written) when the record is incomplete.  Stores non-temporally when `al` (s and e 64-byte aligned).
-// Returns the escapes' count (their words in taken[0 ..)), or -1 if `wait` gave up on one.
-template <typename Wait>
-__attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(int32_t* s, int32_t* e, uint32_t* r,
-                                                                                  uint32_t* sp, const RecK& k,
-                                                                                  uint32_t phase, bool al, bool* ready,
-                                                                                  int* bad, uint32_t** taken,
-                                                                                  Wait&& wait) {
+// AVX-512: readiness check and decode of one full record (64 pairs) from the same two loads; *ready = false (nothing
+// written) while the record or one of its special words has not landed.  Stores non-temporally when `al` (s and e
+// 64-byte aligned).  Returns the specials' count (their words in taken[0 ..)).
+__attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(int32_t* s, int32_t* e,
+                                                                                  const uint32_t* r, uint32_t* sp,
+                                                                                  const RecK& k, uint32_t phase,
+                                                                                  bool al, bool* ready, int* bad,
+                                                                                  uint32_t** taken) {
     const __m512i w0 = _mm512_load_si512(r), w1 = _mm512_load_si512(r + 16);
     const __m512i sign = _mm512_set1_epi32((int)0x80000000u);
-    const __mmask16 m0 = _mm512_test_epi32_mask(w0, sign), m1 = _mm512_test_epi32_mask(w1, sign) & 0x7F;
-    if (m0 != (phase ? (__mmask16)0xFFFF : (__mmask16)0) || m1 != (phase ? (__mmask16)0x7F : (__mmask16)0)) {
-        *ready = false;
-        return 0;
-    }
-    *ready = true;
-    const uint32_t hdr = (uint32_t)_mm_cvtsi128_si32(_mm512_castsi512_si128(w0));
-    const uint32_t nesc = hdr >> 16 & 0x7Fu;
-    const __m512i vj = _mm512_set1_epi32((int)(hdr & 0xFFu)), vr = _mm512_set1_epi32((int)(hdr >> 8 & 0xFFu));
-    const __m512i m10 = _mm512_set1_epi32(0x3FF), m5 = _mm512_set1_epi32(31), v16 = _mm512_set1_epi32(16);
+    const __mmask16 want = phase ? (__mmask16)0xFFFF : (__mmask16)0;
+    *ready = false;
+    if (_mm512_test_epi32_mask(w0, sign) != want || _mm512_test_epi32_mask(w1, sign) != want) return 0;
+    const __m512i m15 = _mm512_set1_epi32(0x7FFF), one = _mm512_set1_epi32(1);
     const __m512i vm = _mm512_set1_epi32(k.match), vd = _mm512_set1_epi32(k.mismatch - k.match);
+    const __m512 f8 = _mm512_set1_ps(8.0f), f1 = _mm512_set1_ps(1.0f), fh = _mm512_set1_ps(0.5f);
     __m512i S[4], E[4];
-    __mmask16 em[4];
-    for (int q = 0; q < 4; ++q) {  // pairs 16q .. 16q + 15: dword 1 + l % 22, field l / 22 (kRecIdx, kRecShift)
-        const __m512i d = _mm512_permutex2var_epi32(w0, _mm512_load_si512(kRecIdx[q]), w1);
-        const __m512i c = _mm512_and_si512(_mm512_srlv_epi32(d, _mm512_load_si512(kRecShift[q])), m10);
-        const __m512i j = _mm512_sub_epi32(vj, _mm512_srli_epi32(c, 5));
-        const __m512i xc = _mm512_srli_epi32(_mm512_mullo_epi32(j, vr), 8);
-        const __m512i x = _mm512_sub_epi32(_mm512_add_epi32(xc, _mm512_and_si512(c, m5)), v16);
+    __mmask16 spm[4];
+    const __m512i cs[4] = {_mm512_and_si512(w0, m15), _mm512_and_si512(w1, m15),
+                           _mm512_and_si512(_mm512_srli_epi32(w0, 15), m15),
+                           _mm512_and_si512(_mm512_srli_epi32(w1, 15), m15)};
+    for (int q = 0; q < 4; ++q) {  // pairs 16q .. 16q + 15
+        const __m512i c = cs[q];
+        const __m512 f = _mm512_sqrt_ps(_mm512_fmadd_ps(_mm512_cvtepi32_ps(c), f8, f1));
+        const __m512i j = _mm512_cvttps_epi32(_mm512_mul_ps(_mm512_sub_ps(f, f1), fh));
+        const __m512i tri = _mm512_srli_epi32(_mm512_mullo_epi32(j, _mm512_add_epi32(j, one)), 1);
+        const __m512i x = _mm512_sub_epi32(c, tri);
         S[q] = _mm512_add_epi32(_mm512_mullo_epi32(j, vm), _mm512_mullo_epi32(x, vd));
         E[q] = j;
-        em[q] = nesc ? _mm512_cmpeq_epi32_mask(c, m10) : (__mmask16)0;
+        spm[q] = _mm512_cmpeq_epi32_mask(c, m15);
     }
-    if (nesc) {
-        alignas(64) int32_t ts[64], te[64];
-        for (int q = 0; q < 4; ++q) {
-            _mm512_store_si512(ts + 16 * q, S[q]);
-            _mm512_store_si512(te + 16 * q, E[q]);
+    // each special's (score, end) into its lane of the vectors (a masked broadcast: no trip through memory); a
+    // special word not landed yet leaves the tile untaken (the vectors are dropped, nothing stored)
+    int m = 0, nb = 0;
+    for (int q = 0; q < 4; ++q)
+        for (uint32_t b = spm[q]; b; b &= b - 1, ++m) {
+            uint32_t* w = sp + 16 * q + __builtin_ctz(b);
+            const uint32_t v = *(volatile uint32_t*)w;
+            if (v == 0u) return 0;
+            taken[m] = w;
+            int32_t sv, ev;
+            rec_decode_special(v, k, sv, ev);
+            nb += v == 0xFFFFFFFFu;
+            const __mmask16 bit = (__mmask16)(b & (0u - b));
+            S[q] = _mm512_mask_set1_epi32(S[q], bit, sv);
+            E[q] = _mm512_mask_set1_epi32(E[q], bit, ev);
         }
-        int m = 0;
-        for (int q = 0; q < 4; ++q)
-            for (uint32_t b = em[q]; b; b &= b - 1, ++m) {
-                const int l = 16 * q + __builtin_ctz(b);
-                // (the device stores it beside the record's dwords, but nothing orders their arrival)
-                uint32_t* w = rec_escape_slot(r, sp, m, l);
-                if (!rec_take_escape(w, k, ts[l], te[l], bad, wait)) return -1;
-                taken[m] = w;
-            }
-        for (int q = 0; q < 4; ++q) {
-            put512(s + 16 * q, _mm512_load_si512(ts + 16 * q), al);
-            put512(e + 16 * q, _mm512_load_si512(te + 16 * q), al);
-        }
-        return m;
-    }
     for (int q = 0; q < 4; ++q) {
         put512(s + 16 * q, S[q], al);
         put512(e + 16 * q, E[q], al);
     }
-    return 0;
+    *bad += nb;
+    *ready = true;
+    return m;
 }
 
 // this CPU runs rec_tile_avx512
@@ -351,41 +322,29 @@ inline bool rec_avx512() {
 }
 
 // The record encoder (put_tile_rec restated on the host), for the CPU tests of the decoders: pairs [0, cnt) of a tile
-// from (sc, en, n) -- n read a's length (j > n: a window pair), en -1 a bad pair; escapes beyond the record's nine
-// slots into sp.  Returns the escapes' count.
+// from (sc, en, n) -- n read a's length (j > n: a window pair), en -1 a bad pair; specials into sp.  Returns the
+// specials' count.
 inline int encode_rec_tile(uint32_t* r, uint32_t* sp, const RecK& k, const int32_t* sc, const int32_t* en,
                            const int32_t* n, size_t cnt, uint32_t phase) {
-    uint32_t x[64] = {0}, c[66] = {0};
-    bool normal[64] = {false};
-    uint32_t jm = 0, sj = 0, sx = 0;
-    for (size_t l = 0; l < cnt; ++l) {
-        const int32_t L = en[l] <= n[l] ? en[l] : n[l];
-        x[l] = en[l] < 0 || k.match == k.mismatch ? 0u : (uint32_t)((k.match * L - sc[l]) / (k.match - k.mismatch));
-        normal[l] = en[l] >= 0 && en[l] <= n[l];
-        if (normal[l]) {
-            jm = jm > (uint32_t)en[l] ? jm : (uint32_t)en[l];
-            sj += (uint32_t)en[l];
-            sx += x[l];
-        }
-    }
-    const uint32_t rho = sj ? std::min(255u, (256u * sx + sj / 2) / sj) : 0u;
+    uint32_t c[64] = {0};
     int m = 0;
     for (size_t l = 0; l < cnt; ++l) {
-        const int32_t dj = (int32_t)jm - en[l], dx = (int32_t)x[l] - (int32_t)(((uint32_t)en[l] * rho) >> 8) + 16;
-        const uint32_t cc = (uint32_t)(32 * dj + dx);
-        if (normal[l] && (uint32_t)dj < 32u && (uint32_t)dx < 32u && cc != 1023u) {
-            c[l] = cc;
-        } else {
-            c[l] = 1023u;
-            const uint32_t w = en[l] < 0 ? 0xFFFFFFFFu
-                                         : 0x80000000u | (uint32_t)en[l] << 16 | x[l] << 8 |
-                                               (en[l] > n[l] ? (uint32_t)n[l] : 255u);
-            *rec_escape_slot(r, sp, m, (int)l) = w;
+        const int32_t j = en[l];
+        if (j < 0) {
+            c[l] = kRecSpecial;
+            sp[l] = 0xFFFFFFFFu;
             ++m;
+        } else if (j > n[l]) {
+            const int32_t x = k.match == k.mismatch ? 0 : (k.match * n[l] - sc[l]) / (k.match - k.mismatch);
+            c[l] = kRecSpecial;
+            sp[l] = 0x80000000u | (uint32_t)j << 16 | (uint32_t)x << 8 | (uint32_t)n[l];
+            ++m;
+        } else {
+            const int32_t x = k.match == k.mismatch ? 0 : (k.match * j - sc[l]) / (k.match - k.mismatch);
+            c[l] = ((uint32_t)j * (uint32_t)(j + 1) >> 1) + (uint32_t)x;
         }
     }
-    r[0] = phase << 31 | (uint32_t)m << 16 | rho << 8 | jm;
-    for (int w = 0; w < 22; ++w) r[1 + w] = phase << 31 | c[w + 44] << 20 | c[w + 22] << 10 | c[w];
+    for (int w = 0; w < 32; ++w) r[w] = phase << 31 | c[w + 32] << 15 | c[w];
     return m;
 }
 

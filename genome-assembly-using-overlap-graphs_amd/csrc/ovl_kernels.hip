@@ -107,67 +107,44 @@ __device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
     return match != mismatch ? 1.0f / (float)(match - mismatch) : 0.f;
 }
 
-// OM 3: streamed tile records.  A 64-pair tile's results as one record in a 128-byte slot at out_score + 32 * tile
-// (dwords), which host threads read while the kernel still runs (ovl_expand.h rec_tile_*):
-//   dword 0           phase << 31 | nesc << 16 | rho << 8 | jmax        (the tile's header)
-//   dword 1 + w       phase << 31 | c[w + 44] << 20 | c[w + 22] << 10 | c[w]   (w < 22; c[64], c[65] = 0)
-//   dword 23 + r      escape r of the tile (r < 9), in lane order; escapes from the tenth on go to out_end[p]
-// The phase bit (the host flips it each time it reuses the staging slot) tells the host which of dwords 0..22 this
-// launch has written: every dword is one aligned 32-bit store, so a dword whose phase bit is the launch's holds the
-// launch's payload.  No fence, no counter, no acknowledgement wait on the device (the rejected one-grid transport
-// paid an L2 write-back per wave for its counters).  An escape word has bit 31 set and is zero until it lands: the
-// host zeroes each one it reads, so a slot holds nothing stale.
-//   Codes are relative to the tile: a pair with end j <= n (read a's length; L = j compared bases,
-// aligners.py:27-48 with gaps that cannot win, so score = match*j + (mismatch - match)*X) has the 10-bit code
-// c = 32 (jmax - j) + (X - xc(j) + 16) with xc(j) = (j * rho) >> 8, where jmax is the largest such j of the tile
-// and rho / 256 its mismatch rate (sum X / sum j) -- when both parts fit 5 bits and c != 1023.  Every other pair
-// is an escape (c = 1023) with the word 1 << 31 | j << 16 | X << 8 | n (L = min(j, n): n = 255 for an ordinary
-// pair, read a's length for a shorter read a inside b's window) or 0xFFFFFFFF for a bad pair.  The tile model
-// decides only which pairs escape, never a result: the host inverts every code exactly.  92 link bytes per tile
-// plus 4 per escape (~1.5 per pair at the target point, against 8 for two int32).  Every lane of the wavefront
-// calls it (the reductions and exchanges); lanes with !mine code 0, which the host never reads.
+// OM 3: streamed tile records.  A 64-pair tile's results as one 128-byte record at out_score + 32 * tile
+// (dwords), which host threads read while the kernel still runs (ovl_expand.h rec_tile_ready / expand_rec):
+//   dword w (w < 32) = phase << 31 | c[w + 32] << 15 | c[w]   (c[l]: lane l's 15-bit code)
+// The phase bit (the host flips it each time it reuses the staging slot) tells the host which dwords this
+// launch has written: every dword is one aligned 32-bit store, so a dword whose phase bit is the launch's
+// holds the launch's payload, and a record is complete when all 32 are.  No fence, no counter, no
+// acknowledgement wait on the device (the rejected one-grid transport paid an L2 write-back per wave for its
+// counters).  Code c of a pair with end j <= n (read a's length; L = j compared bases, aligners.py:27-48 with
+// gaps that cannot win, so score = match*j + (mismatch - match)*X) is j(j + 1)/2 + X, X <= j <= 254 (< 0x7FFF).
+// Every other pair has c = 0x7FFF and a special word in out_end[p] (zero until it lands; the host zeroes the words it
+// read once this kernel has ended, ovl_api.cpp stream_chunk):
+//   1 << 31 | j << 16 | X << 8 | n   a shorter read a inside b's window (j > n: L = n, score = match*n +
+//                                    (mismatch - match)*X);
+//   0xFFFFFFFF                       a bad pair (-1, -1).
+// 2 link bytes per pair (+ 4 per special), a fixed layout whatever the mismatch counts.  Every lane of the
+// wavefront calls it (the cross-half exchange); lanes with !mine code 0, which the host never reads.
 __device__ __forceinline__ void put_tile_rec(int32_t* out_score, int32_t* out_end, int64_t tile, int64_t p, bool mine,
                                              int32_t sc, int32_t en, int32_t n, int32_t match, float inv,
                                              uint32_t phase, int lane) {
-    const bool normal = mine && en >= 0 && en <= n;
-    // X = (match*L - score) / (match - mismatch), an exact quotient below 2^8: float is exact
-    const int32_t L = en <= n ? en : n;
-    const uint32_t x = mine && en >= 0 ? (uint32_t)__builtin_rintf((float)(match * L - sc) * inv) : 0u;
-    int32_t jm = normal ? en : 0;
-    uint32_t sum = normal ? ((uint32_t)en | x << 16) : 0u;  // (sum j < 2^14, sum X <= sum j)
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        jm = max(jm, __shfl_xor(jm, o, 64));
-        sum += (uint32_t)__shfl_xor((int)sum, o, 64);
-    }
-    const uint32_t sj = sum & 0xFFFFu, sx = sum >> 16;
-    const uint32_t rho = sj ? min(255u, (256u * sx + sj / 2) / sj) : 0u;
     uint32_t c = 0;
-    bool esc = false;
-    uint32_t ew = 0;
     if (mine) {
-        const int32_t dj = jm - en, dx = (int32_t)x - (int32_t)(((uint32_t)en * rho) >> 8) + 16;
-        const uint32_t cc = (uint32_t)(32 * dj + dx);
-        if (normal && (uint32_t)dj < 32u && (uint32_t)dx < 32u && cc != 1023u) {
-            c = cc;
+        if (en < 0) {
+            c = 0x7FFFu;
+            __builtin_nontemporal_store(0xFFFFFFFFu, reinterpret_cast<uint32_t*>(out_end) + p);
+        } else if (en > n) {
+            // X = (match*n - score) / (match - mismatch), an exact quotient below 2^8: float is exact
+            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * n - sc) * inv);
+            c = 0x7FFFu;
+            __builtin_nontemporal_store(0x80000000u | (uint32_t)en << 16 | x << 8 | (uint32_t)n,
+                                        reinterpret_cast<uint32_t*>(out_end) + p);
         } else {
-            esc = true;
-            c = 1023u;
-            ew = en < 0 ? 0xFFFFFFFFu : 0x80000000u | (uint32_t)en << 16 | x << 8 | (en > n ? (uint32_t)n : 255u);
+            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * en - sc) * inv);
+            c = ((uint32_t)en * (uint32_t)(en + 1) >> 1) + x;
         }
     }
-    const uint64_t em = __ballot(esc);
-    const uint32_t c1 = (uint32_t)__shfl(c, lane + 22, 64), c2 = (uint32_t)__shfl(c, lane + 44 < 64 ? lane + 44 : 0, 64);
-    uint32_t* rec = reinterpret_cast<uint32_t*>(out_score) + tile * 32;
-    // lanes 0..22: the header and the 22 code dwords in one store
-    const uint32_t cw = c | c1 << 10 | (lane + 44 < 64 ? c2 : 0u) << 20;
-    const uint32_t hw = (uint32_t)__popcll(em) << 16 | rho << 8 | (uint32_t)jm;
-    const uint32_t prev = (uint32_t)__shfl_up((int)cw, 1, 64);  // (lane l stores code dword l - 1)
-    if (lane <= 22) __builtin_nontemporal_store(phase << 31 | (lane == 0 ? hw : prev), rec + lane);
-    if (esc) {
-        const int r = __popcll(em & ((1ull << lane) - 1ull));
-        __builtin_nontemporal_store(ew, r < 9 ? rec + 23 + r : reinterpret_cast<uint32_t*>(out_end) + p);
-    }
+    const uint32_t hi = (uint32_t)__shfl_xor((int)c, 32, 64);
+    if (lane < 32)
+        __builtin_nontemporal_store(phase << 31 | hi << 15 | c, reinterpret_cast<uint32_t*>(out_score) + tile * 32 + lane);
 }
 
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler

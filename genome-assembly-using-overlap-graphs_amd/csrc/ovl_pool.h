@@ -132,14 +132,14 @@ class CpuShare {
 };
 
 // Threads of the host pool for `cpus` CPUs shared by `sharers` processes: OVL_POOL_THREADS (or the older
-// OVL_HOST_THREADS) when set, else the process's part of the CPUs less one, at most 15, at least 1.  (Round 2,
-// 2-byte packing, three processes on a 16-CPU share: 6 / 8 / 12 threads each 0.156-0.217 / 0.181-0.229 /
-// 0.157-0.162 ms, profiles/r02_pool_threads_*.json.  Round 5, streamed records, one process: 15 threads against
-// 12 faster at every shard size, N = 1 / 2 / 4 / 8 of the target list 0.155 / 0.083 / 0.062 / 0.049 ->
-// 0.149 / 0.078 / 0.059 / 0.049 ms, profiles/r05_pool_threads_ab.json.)
+// OVL_HOST_THREADS) when set, else the process's part of the CPUs less one, at most 12, at least 1.  (Round 2,
+// three processes on a 16-CPU share: 6 / 8 / 12 threads each 0.156-0.217 / 0.181-0.229 / 0.157-0.162 ms,
+// profiles/r02_pool_threads_*.json.  Round 5, one process, per-rank steps at N = 1 / 2 / 4 / 8 of the target list:
+// 12 threads 0.138 / 0.089 / 0.060 / 0.045 ms against 15 threads 0.150 / 0.095 / 0.065 / 0.050, same box; streamed
+// records (OVL_PACK=2) preferred 15 by 1-7 %, profiles/r05_pool_threads_ab.json.)
 int pool_rule(int cpus, int sharers, int env_threads) {
     if (env_threads > 0) return std::min(64, env_threads);
-    return std::max(1, std::min(15, cpus / std::max(1, sharers) - 1));
+    return std::max(1, std::min(12, cpus / std::max(1, sharers) - 1));
 }
 
 int env_pool_threads() {

@@ -140,11 +140,11 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
             else:
                 want = n
             assert x["packed_pairs"] == want, (name, x)
-            if pack == "2":  # streamed records: 92 B per tile of each chunk plus 4 per escape
+            if pack == "2":  # streamed records: 128 B per tile of each chunk plus 4 per special pair
                 r = eng.last_transfer()
                 rec = r["result_bytes"] - 8 * (n - want) - 4 * r["escapes"]
                 tiles = (want + 63) // 64
-                assert r["record_pairs"] == want and 92 * tiles <= rec <= 92 * (tiles + n // 1000 + 2), (name, r)
+                assert r["record_pairs"] == want and 128 * tiles <= rec <= 128 * (tiles + n // 1000 + 2), (name, r)
                 assert x["link_bytes"] == 8 * n + r["result_bytes"], (name, x, r)
             else:
                 assert x["link_bytes"] == 8 * n + 2 * want + 8 * (n - want), (name, x)
@@ -174,11 +174,11 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
 @pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
 def test_tile_records(oracle_mod, cfg2, pack, scoring):
     """Packed chunks cross the link as streamed tile records (OVL_PACK=2, the default: ovl_kernels.hip
-    put_tile_rec, 10-bit codes relative to the tile and a phase bit per dword, expanded by host threads while the
-    kernel runs; OVL_PACK=1 keeps 2 bytes per pair expanded after each chunk): cfg2's list tiled six times (731 K
-    pairs) with bad pairs, under scorings with match == mismatch and mismatch > match, into pinned, pageable and
-    misaligned arrays, all packed and with a direct share; every (score, end) equals the oracle's, and the call's
-    link bytes are the records' (92 per tile + 4 per escape) or 2 per pair."""
+    put_tile_rec, 15-bit codes and a phase bit per dword, expanded by host threads while the kernel runs;
+    OVL_PACK=1 keeps 2 bytes per pair expanded after each chunk): cfg2's list tiled six times (731 K pairs) with
+    bad pairs, under scorings with match == mismatch and mismatch > match, into pinned, pageable and misaligned
+    arrays, all packed and with a direct share; every (score, end) equals the oracle's, and the call's link bytes
+    are the records' (128 per tile + 4 per special pair) or 2 per pair."""
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a0, b0 = cfg2
@@ -216,10 +216,8 @@ def test_tile_records(oracle_mod, cfg2, pack, scoring):
                     else:
                         assert x["record_pairs"] == np_, (name, x)
                         tiles = (np_ + 63) // 64
-                        assert res == 92 * tiles + 4 * x["escapes"], (name, x)
-                        assert x["escapes"] >= len(bad) - 1, (name, x)  # (the bad pairs are escapes)
-                        if scoring == (10, -1):  # most pairs near their tile's model
-                            assert x["escapes"] < 0.1 * np_, (name, x)
+                        assert res == 128 * tiles + 4 * x["escapes"], (name, x)
+                        assert x["escapes"] >= len(bad) - 1, (name, x)  # (the bad pairs are specials)
         finally:
             eng.close()
 
@@ -256,8 +254,7 @@ def test_tile_records_across_read_sets(oracle_mod):
     list read in place), permuted (decoded) and from the resident candidate list, twice each, every call exact
     against the oracle.  Covers the staging slots' rotation and the zeroing of the escape words each record chunk
     read, which waits until that chunk's kernel has ended (a host store into a line of a running kernel's records
-    was measured to come back with the device's value: stale escape words then decoded into later calls)."""
-    from ovlgraph import OverlapEngine
+    was measured to come back with the device's value: stale words then decoded into later calls)."""
     from ovlgraph.candidates import dedup_reads, enumerate_candidates
     from ovlgraph.reads import config_reads
     sets = {}
@@ -266,7 +263,7 @@ def test_tile_records_across_read_sets(oracle_mod):
         a, b = enumerate_candidates(reads, 5)
         rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
         sets[cfg] = (reads, a, b, rs, re_, np.random.default_rng(1).permutation(a.shape[0]))
-    with OverlapEngine(0) as eng:
+    with _engine_env({"OVL_PACK": "2"}) as eng:
         for rnd in range(2):
             for cfg in ("cfg2", "cfg3"):
                 reads, a, b, rs, re_, perm = sets[cfg]
@@ -692,15 +689,16 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
 @pytest.mark.parametrize("cfg", ["target", "cfg3"])
 @pytest.mark.parametrize("pct", [None, "15"])
 def test_step_transport_vs_oracle(oracle_mod, cfg, pct):
-    """Whole resident list into pinned arrays (the bench step: one launch whose streamed tile records host threads
-    expand while it runs; with OVL_PACK_DIRECT_PCT its last tiles stored as int32 straight into the arrays) equals
-    the oracle call after call, into reused and fresh arrays; ovl_last_transfer counts 92 B per record tile, 4 B
-    per escape and 8 B per direct pair."""
+    """Whole resident list into pinned arrays through streamed tile records (OVL_PACK=2: one launch whose records
+    host threads expand while it runs; with OVL_PACK_DIRECT_PCT its last tiles stored as int32 straight into the
+    arrays) equals the oracle call after call, into reused and fresh arrays; ovl_last_transfer counts 128 B per
+    record tile, 4 B per special pair and 8 B per direct pair.  (The default 2-byte transport of the bench step:
+    test_packed_adaptive_share, test_gpu_bench_dist.py.)"""
     from ovlgraph.candidates import dedup_reads
     from ovlgraph.hostmem import pinned_empty
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
-    eng = _engine_env({"OVL_PACK_DIRECT_PCT": pct} if pct else {})
+    eng = _engine_env({"OVL_PACK": "2", "OVL_PACK_DIRECT_PCT": pct} if pct else {"OVL_PACK": "2"})
     try:
         eng.set_reads(reads)
         a, b = eng.candidates(5)
@@ -715,11 +713,11 @@ def test_step_transport_vs_oracle(oracle_mod, cfg, pct):
             np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
             x = eng.last_transfer()
             assert (0 < x["packed_pairs"] < n) if pct else x["packed_pairs"] == n, x
-            # (no pair list crosses: the link bytes are the results', tile records for the packed pairs -- 92 B
-            # per 64 pairs and 4 B per escape -- and 8 B per direct pair)
+            # (no pair list crosses: the link bytes are the results', tile records for the packed pairs -- 128 B
+            # per 64 pairs and 4 B per special pair -- and 8 B per direct pair)
             assert x["link_bytes"] == x["result_bytes"], x
             q = x["record_pairs"]
-            assert x["result_bytes"] == 92 * ((q + 63) // 64) + 4 * x["escapes"] + 2 * (x["packed_pairs"] - q) + \
+            assert x["result_bytes"] == 128 * ((q + 63) // 64) + 4 * x["escapes"] + 2 * (x["packed_pairs"] - q) + \
                 8 * (n - x["packed_pairs"]), x
         fresh = eng.score_candidates()
         np.testing.assert_array_equal(fresh[0], ref_s)

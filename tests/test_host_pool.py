@@ -9,10 +9,10 @@ from ovlgraph.engine import host_pool
 
 def test_rule():
     rule = _lib.load().ovl_host_pool_rule
-    assert rule(16, 1, 0) == 15           # the box's 16-CPU share, one process: 15 threads
-    assert rule(256, 1, 0) == 15
+    assert rule(16, 1, 0) == 12           # the box's 16-CPU share, one process: 12 threads
+    assert rule(256, 1, 0) == 12
     assert rule(16, 4, 0) == 3            # four joblib workers on 16 CPUs: 16 / 4 - 1
-    assert rule(128, 8, 0) == 15          # eight ranks on a 128-CPU node quota
+    assert rule(128, 8, 0) == 12          # eight ranks on a 128-CPU node quota
     assert rule(16, 8, 0) == 1            # never below one thread
     assert rule(8, 1, 0) == 7
     assert rule(16, 4, 5) == 5            # OVL_POOL_THREADS wins
@@ -49,7 +49,7 @@ def test_four_processes_share_the_cpus():
         # this test process holds a slot too (host_pool above), so at least the four workers + 1
         assert r["sharers"] >= 5, res
         assert r["threads"] <= max(1, r["cpus"] // 4), res
-        assert r["threads"] == max(1, min(15, r["cpus"] // r["sharers"] - 1)), res
+        assert r["threads"] == max(1, min(12, r["cpus"] // r["sharers"] - 1)), res
         if r["threads"] < 6:
             assert r["packed"] == 0
     # the workers' slots are gone with them: the count drops back
