@@ -831,6 +831,26 @@ def max_over_ranks(el: float, world: int, dev, backend: str) -> float:
     return max(r[0] for r in gather_floats([el], world, dev, backend))
 
 
+def per_rank_projection(name: str):
+    """The per-rank steps of `name`'s list measured on one GPU (tools/shard_step_ab.py: rank 0's shard of the list
+    sharded by sum n*m over N ranks, scored alone; the committed profile named in `source`), and the speed-ups over
+    one GPU they project for N ranks on N GPUs -- each rank on its own GPU, link and CPU share, so this prices the
+    per-rank step, not the host memory all ranks of one node share.  None when no profile is committed."""
+    src = os.path.join("profiles", "r05_cfg4_shard_steps.json" if name == "cfg4" else "r05_shard_steps.json")
+    try:
+        with open(os.path.join(ROOT, src)) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ms = {int(r["ranks"]): float(r["median_ms"]) for r in d.get("results", [])
+          if r.get("setting", "default") in ("default", "def")}
+    if 1 not in ms:
+        return None
+    return {"source": src, "config": d.get("config"), "ms_per_rank_step": ms,
+            "projected_speedup": {n: round(ms[1] / v, 2) for n, v in sorted(ms.items())},
+            "projected_efficiency": {n: round(ms[1] / v / n, 2) for n, v in sorted(ms.items())}}
+
+
 def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: int, warmup: int):
     """One read set of `name`, its candidate list sharded by sum n*m over the ranks, every rank's results into
     rank 0's shared pinned host buffer (ShardedStep, dest="host"); then rank 0 alone scores the whole list
@@ -865,7 +885,7 @@ def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: i
             "ms_per_step": el_max / steps * 1e3, "pairs_per_s": st.n_pairs * steps / el_max,
             "one_gpu_ms_per_step": one / steps * 1e3, "one_gpu_pairs_per_s": st.n_pairs * steps / one,
             "speedup_vs_one_gpu": one / el_max, "matches_one_gpu": ok, "setup_s": round(setup, 2),
-            "scaling": "strong",
+            "scaling": "strong", "per_rank_projection": per_rank_projection(name),
             "what": "one shared list sharded by sum n*m, each rank's (score, end) into rank 0's shared pinned host "
                     "buffer (step fence in shared memory); one_gpu: rank 0 alone scores the whole list in the "
                     "same run (others idle)"}
@@ -927,6 +947,7 @@ def sharded_list(name: str, world: int, rank: int, dev, backend: str, args):
     if rank == 0:
         res.update(one_gpu_ms_per_step=one / args.steps * 1e3, one_gpu_pairs_per_s=w.n_pairs * args.steps / one,
                    speedup_vs_one_gpu=one / el_max, matches_one_gpu=ok,
+                   per_rank_projection=per_rank_projection(name),
                    rccl_gather={"dest": "rank0", "backend": backend, "ms_per_step": el_g / args.steps * 1e3,
                                 "pairs_per_s": w.n_pairs * args.steps / el_g, "matches_one_gpu": g_ok,
                                 "bytes_per_step": g.gather_bytes(),
@@ -984,6 +1005,7 @@ def multi_line(args, world: int, ident: dict, top: dict, extras: dict) -> dict:
         "one_gpu_pairs_per_s": top.get("one_gpu_pairs_per_s"),
         "speedup_vs_one_gpu": top.get("speedup_vs_one_gpu"),
         "matches_one_gpu": top.get("matches_one_gpu"),
+        "per_rank_projection": top.get("per_rank_projection"),
         "per_rank_ms_per_step": top.get("per_rank_ms_per_step"),
         "roofline": top.get("roofline"),
         "in_step_kernels": top.get("in_step_kernels"),
