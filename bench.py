@@ -560,8 +560,27 @@ def band_sweep(w: Workload, bands, indel: int, steps: int, dev):
         out["points"].append({"band": band, "kernel": w.kernel, "ms_per_step": el / steps * 1e3,
                               "kernel_ms": km, "pairs_per_s": w.n_pairs * steps / el,
                               "cells_per_pair_upper": round(cells, 1),
-                              "cells_per_s": w.n_pairs * cells / (km * 1e-3)})
+                              "cells_per_s": w.n_pairs * cells / (km * 1e-3), "pmc": band_pmc(band)})
     return out
+
+
+def band_pmc(band: int):
+    """The band kernel's counters at this sweep point from the committed PMC profile (tools/gpu_r05_cfg5_pmc.sh,
+    tools/cfg5_pmc_summary.py: each counter in its own rocprofv3 pass of the same bench command, so not live):
+    valu_isa_frac (VALU pipe issue share at 4 cycles per wave64 instruction), waves_per_simd (mean resident),
+    lds_bank_conflict_frac (conflict cycles over LDS-array cycles).  None when the profile lacks the band."""
+    src = os.path.join("profiles", "r05_cfg5_pmc.json")
+    try:
+        with open(os.path.join(ROOT, src)) as f:
+            ks = json.load(f)["bands"][str(band)]["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    if not ks:
+        return None
+    k, e = max(ks.items(), key=lambda kv: (kv[1].get("kernel_trace") or {}).get("average_ns", 0.0))
+    return {"kernel": k, "valu_isa_frac": e.get("valu_isa_frac"), "waves_per_simd": e.get("waves_per_simd"),
+            "lds_bank_conflict_frac": e.get("lds_bank_conflict_frac"),
+            "rocprof_kernel_ms": (e.get("kernel_trace") or {}).get("average_ns", 0.0) / 1e6, "source": src}
 
 
 def sharded_band_sweep(world: int, rank: int, dev, eng, bands, indel: int, steps: int, backend: str):
@@ -1333,9 +1352,12 @@ def main() -> int:
     if not args.no_cpu_baseline and w.a is not None:
         cb = cpu_baseline(w.reads, w.a, w.b, gpu_sc, gpu_en, args.cpu_budget)
         line["cpu_baseline"] = cb
-        line["vs_cpu_baseline"] = {"all_cores_full_dp": value / cb["value"],
+        # "share": the threads the port ran on (cpu_baseline.cores: OMP_NUM_THREADS, else the affinity mask -- the
+        # box's 16-CPU share, not the machine's cores)
+        line["vs_cpu_baseline"] = {"share_threads": cb["cores"],
+                                   "share_threads_full_dp": value / cb["value"],
                                    "one_core_full_dp": value / cb["one_core"]["value"],
-                                   "all_cores_closed_form": value / cb["closed_form"]["value"]}
+                                   "share_threads_closed_form": value / cb["closed_form"]["value"]}
     else:
         line["cpu_baseline"] = None
     print(json.dumps(line), flush=True)

@@ -76,13 +76,19 @@ thread_local std::string g_err;
 // planner would otherwise pick by size or scoring, so the tests reach every form on small inputs.  (The A/B
 // knobs of rounds 1-3 -- lane split, copy-engine transfers, spin waits, ordinary-store expansion, grid cap, heavy
 // tiles, lane strip width and hand-off forms, read packing, pool spin, coarse-grained host memory -- are gone
-// with the forms they measured; DESIGN.md records each measurement.)
+// with the forms they measured; DESIGN.md records each measurement.  Round 5 merged the pairs of switches over one
+// choice into one knob each -- OVL_DP_FORM, OVL_LANE_FORM, OVL_PAIRS_FORM -- and dropped the settled vector-width
+// knobs of the host expansion and encoding: both run the widest form the CPU has.)
 struct Knobs {
     int32_t band_form = -1;       // OVL_BAND_FORM env (lane|diag|rows|fast|strip): band knob kernel (tests)
-    int32_t dp_classic = 0;       // OVL_DP_CLASSIC=1 env: full-DP scoring through dp_kernel (tests)
-    int32_t dp_lane = -1;         // OVL_DP_LANE env: lane-per-pair full DP (-1 auto by list size, 0 off, 1 forced)
-    int32_t lane_prof = 1;        // OVL_LANE_PROF=0: compare/select scores instead of the byte profile (tests)
-    int32_t lane_sfx = 1;         // OVL_LANE_SFX=0: row symbols by byte gathers instead of the bit planes (tests)
+    // OVL_DP_FORM env, full-DP scoring (tests): auto (default: lane-per-pair from kLaneMinPairs pairs, else
+    // dp_fast_kernel), lane (lane-per-pair forced), fast (dp_fast_kernel), classic (dp_kernel)
+    int32_t dp_classic = 0;
+    int32_t dp_lane = -1;         // -1 auto by list size, 0 off, 1 forced
+    // OVL_LANE_FORM env, the lane kernels' inner form (tests), a bit mask, default 3: bit 0 scores by the byte
+    // profile (else compare/select), bit 1 takes row symbols from the bit planes (else byte gathers)
+    int32_t lane_prof = 1;
+    int32_t lane_sfx = 1;
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
     int32_t pack = 1;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
                                   // form holds; 1 (default) packed as 2 bytes per pair, expanded chunk by chunk
@@ -95,10 +101,11 @@ struct Knobs {
                                   // (64 K: a 250 K-pair shard -- N = 8 at the target point -- 0.057 -> 0.054 ms)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
                                   // OVL_PACK_DIRECT_PCT fixes it
-    int32_t compact = 1;          // OVL_PAIRS_COMPACT=0: host pair lists cross the link as the caller's int32 arrays
-                                  // instead of the compact encoding (encode_chunk; tests)
-    int32_t pairs_ix = 1;         // OVL_PAIRS_IX=0: compact lists always decode into HBM (widen / runs kernels)
-                                  // instead of uniform_kernel reading b16 + tile deltas in place (tests)
+    // OVL_PAIRS_FORM env, host pair lists over the link (tests): ix (default: the compact encoding, encode_chunk,
+    // read in place by uniform_kernel as b16 + tile deltas where it can), decode (compact, always decoded into HBM
+    // by the widen / runs kernels), plain (the caller's int32 arrays)
+    int32_t compact = 1;
+    int32_t pairs_ix = 1;
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -728,19 +735,26 @@ Knobs read_knobs() {
         else if (!strcmp(e, "lane1")) k.band_form = OVL_BAND_FORM_LANE1;
         else if (!strcmp(e, "lane2")) k.band_form = OVL_BAND_FORM_LANE2;
     }
-    if (const char* e = getenv("OVL_DP_CLASSIC")) k.dp_classic = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_DP_LANE")) k.dp_lane = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_PROF")) k.lane_prof = atoi(e) ? 1 : 0;
-    if (const char* e = getenv("OVL_LANE_SFX")) k.lane_sfx = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_DP_FORM")) {
+        if (!strcmp(e, "lane")) k.dp_lane = 1;
+        else if (!strcmp(e, "fast")) k.dp_lane = 0;
+        else if (!strcmp(e, "classic")) k.dp_classic = 1;
+    }
+    if (const char* e = getenv("OVL_LANE_FORM")) {
+        const int v = atoi(e);
+        k.lane_prof = v & 1;
+        k.lane_sfx = (v >> 1) & 1;
+    }
     if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
         k.pack_adapt = 0;  // a fixed share
     }
-    if (const char* e = getenv("OVL_PAIRS_COMPACT")) k.compact = atoi(e) ? 1 : 0;
-
-    if (const char* e = getenv("OVL_PAIRS_IX")) k.pairs_ix = atoi(e) ? 1 : 0;
+    if (const char* e = getenv("OVL_PAIRS_FORM")) {
+        if (!strcmp(e, "plain")) k.compact = 0;
+        else if (!strcmp(e, "decode")) k.pairs_ix = 0;
+    }
     if (const char* e = getenv("OVL_PIPE_CHUNK")) {
         const long long v = atoll(e);
         if (v >= 64) k.pipe_chunk = v;
@@ -751,14 +765,10 @@ Knobs read_knobs() {
 void host_copy(void* dst, const void* src, size_t bytes) { CopyPool::get().copy(dst, src, bytes); }
 
 // Packed results (ovl_kernels.hip put_pair, sink 2) into the caller's int32 arrays (ovl_expand.h), split
-// over the host pool.  The vector width is the widest this CPU runs unless OVL_EXPAND_ISA names one
-// (scalar, sse2, avx2, avx512; A/B knob).
+// over the host pool, at the widest vector width this CPU runs.
 void host_expand(int32_t* s, int32_t* e, const uint16_t* pk, const int32_t* esc, int32_t match, int32_t mismatch,
                  bool nt, size_t n, size_t min_part) {
-    static const ovl_expand::Fn f = [] {
-        const ovl_expand::Fn g = ovl_expand::pick(getenv("OVL_EXPAND_ISA"));
-        return g ? g : ovl_expand::pick(nullptr);
-    }();
+    static const ovl_expand::Fn f = ovl_expand::pick(nullptr);
     CopyPool::get().parallel(n, min_part,
                              [=](size_t lo, size_t hi) { f(s, e, pk, esc, match, mismatch, nt, lo, hi); });
 }
@@ -1158,8 +1168,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
     char* ha = hb + b_bytes;                       // a area: tile deltas + bases, runs, or a like b
     CopyPool& pool = CopyPool::get();
     const std::vector<size_t> parts = pool.cut((size_t)n, size_t(1) << 15);
-    static const ovl_encode::Fns enc = ovl_encode::pick(getenv("OVL_ENCODE_ISA"));
-    if (!enc.narrow) return fail(d, OVL_E_ARG, "OVL_ENCODE_ISA names an ISA this CPU does not run");
+    static const ovl_encode::Fns enc = ovl_encode::pick(nullptr);  // the widest this CPU runs
     J.ixk.resize((size_t)J.nchunks, 0);
     J.ixk[(size_t)k] = 0;
     // In place (uniform_kernel IX): b as uint16 and a as tile deltas (d8[p] = a[p] - a[64t], bases int32),

@@ -180,7 +180,7 @@ def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes, lanes):
     diagonals left and right of the table) and scorings inside and outside their int8 byte scores
     (those fall back to the anti-diagonal form): one lane per pair (lanes=1) and two lanes per pair one
     row apart (lanes=2; band 0 has one cell and stays on one lane).  planes=1 reads row symbols and t
-    codes from the resident bit planes, planes=0 gathers code bytes (OVL_LANE_SFX)."""
+    codes from the resident bit planes, planes=0 gathers code bytes (OVL_LANE_FORM bit 1)."""
     rng = random.Random(band * 31 + sum(params) % 97)
     lens = [0, 1, 2, 3, 7, 16, 31, 33, 64, 100, 180, 250]
     reads = ["".join(rng.choice("ACGT") for _ in range(rng.choice(lens))) for _ in range(160)]
@@ -189,6 +189,6 @@ def test_band_lane_kernel_vs_oracle(oracle_mod, params, band, planes, lanes):
     a = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
     b = np.array([rng.randrange(n) for _ in range(2500)], np.int32)
     rs, re_ = oracle_mod.batch_banded(reads, a, b, *params, band)
-    sc, en = _score_with_env({"OVL_BAND_FORM": "lane" + lanes, "OVL_LANE_SFX": planes}, reads, a, b, params, band)
+    sc, en = _score_with_env({"OVL_BAND_FORM": "lane" + lanes, "OVL_LANE_FORM": str(1 + 2 * int(planes))}, reads, a, b, params, band)
     np.testing.assert_array_equal(sc, rs)
     np.testing.assert_array_equal(en, re_)

@@ -3,7 +3,7 @@
 ovl_score_host / ovl_score_pairs encode the caller's int32 pairs per pipeline chunk -- b as uint16 when
 n_reads <= 65,535; a, when the list is a-major (overlapGraphs.py:43-52), as tile deltas that uniform_kernel
 reads in place (IX: a = base[p / 64] + d8[p]) or as runs that kernels decode into HBM.  Every result is
-compared with the oracle and with the uncompressed path (OVL_PAIRS_COMPACT=0): a-major and shuffled lists
+compared with the oracle and with the uncompressed path (OVL_PAIRS_FORM=plain): a-major and shuffled lists
 (in place / runs / no runs), uint16 and int32 widths, pinned and pageable lists, odd chunk sizes, tiles whose
 a jumps past the delta range, calls small enough for the latency-mode launch, and bad indices (OVL_E_INDEX,
 -1 results, the rest exact).
@@ -55,7 +55,7 @@ def test_compact_vs_oracle_and_plain(oracle_mod, target, order, pinned, chunk):
         a, b = pa, pb
     env = {"OVL_PIPE_CHUNK": chunk} if chunk else {}
     comp = _engine_env(env)
-    plain = _engine_env(dict(env, OVL_PAIRS_COMPACT="0"))
+    plain = _engine_env(dict(env, OVL_PAIRS_FORM="plain"))
     try:
         for e in (comp, plain):
             e.set_reads(reads)
@@ -179,7 +179,7 @@ def _pair_link_bytes(eng, n):
 
 @pytest.mark.parametrize("pinned", [False, True])
 def test_ix_in_place_vs_decode(oracle_mod, target, pinned):
-    """The a-major target list is read in place (3 B per pair + 4 B per tile); OVL_PAIRS_IX=0 decodes the
+    """The a-major target list is read in place (3 B per pair + 4 B per tile); OVL_PAIRS_FORM=decode decodes the
     same encoding's runs into HBM first.  Same results; the path each call took is asserted from
     ovl_last_pair_list (pairs read in place / decoded), not inferred from its link bytes."""
     from ovlgraph.hostmem import pinned_empty
@@ -191,7 +191,7 @@ def test_ix_in_place_vs_decode(oracle_mod, target, pinned):
         pa[:], pb[:] = a, b
         a, b = pa, pb
     ix = _engine_env({})
-    dec = _engine_env({"OVL_PAIRS_IX": "0"})
+    dec = _engine_env({"OVL_PAIRS_FORM": "decode"})
     try:
         for e in (ix, dec):
             e.set_reads(reads)

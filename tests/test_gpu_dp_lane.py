@@ -1,7 +1,7 @@
 """GPU parity of the lane-per-pair full DP (csrc/ovl_dp_lane.hip) for gapped scoring.
 
 aligners.py:27-57 with a finite indel: every (score, end) must equal the oracle's C
-restatement bit for bit.  OVL_DP_LANE=1 forces the lane kernel for small lists (the
+restatement bit for bit.  OVL_DP_FORM=lane forces the lane kernel for small lists (the
 planner picks it automatically only for >= 65,536 pairs).
 Wavefronts mix read lengths (virtual leading rows), lengths cross the 32-column strips,
 and the list length is not a multiple of 64.
@@ -52,7 +52,7 @@ def mixed_set(request):
 # byte score profile x bit-plane row symbols; the hand-off column form follows the scoring (4-bit steps in LDS
 # when the profile and planes are on, the steps are bounded by 15 and lmax <= 256; else int16 or int32 in HBM),
 # so the 13 scorings below reach every form
-VARIANTS = {f"prof{pr}-sfx{sx}": {"OVL_LANE_PROF": pr, "OVL_LANE_SFX": sx}
+VARIANTS = {f"prof{pr}-sfx{sx}": {"OVL_LANE_FORM": str(int(pr) + 2 * int(sx))}
             for pr in ("0", "1") for sx in ("0", "1") if pr == "1" or sx == "0"}
 
 
@@ -66,7 +66,7 @@ def test_lane_vs_oracle_mixed_lengths(oracle_mod, mixed_set, params, variant):
     and int32 inside the same kernel family."""
     reads, a, b = mixed_set
     rs, re_ = oracle_mod.batch_dp(reads, a, b, *params)
-    with _engine_env(dict(VARIANTS[variant], OVL_DP_LANE="1")) as eng:
+    with _engine_env(dict(VARIANTS[variant], OVL_DP_FORM="lane")) as eng:
         eng.set_reads(reads)
         # (0, 0, -1) over bit-plane reads is the closed form (gaps cannot win): still checked
         assert eng.plan(*params) == "dp" or params == (0, 0, -1)
@@ -85,7 +85,7 @@ def test_lane_uniform_reads_with_truncated_tail(oracle_mod, variant):
     a, b = enumerate_candidates(reads, 5)
     a, b = a[:4000], b[:4000]
     rs, re_ = oracle_mod.batch_dp(reads, a, b, 10, -1, -2)
-    with _engine_env(dict(VARIANTS[variant], OVL_DP_LANE="1")) as eng:
+    with _engine_env(dict(VARIANTS[variant], OVL_DP_FORM="lane")) as eng:
         eng.set_reads(reads)
         sc, en = eng.score(a, b, 10, -1, -2)
     np.testing.assert_array_equal(sc, rs)
@@ -99,7 +99,7 @@ def test_lane_wide_alphabet_vs_oracle(oracle_mod):
     a = np.array([rng.randrange(200) for _ in range(1300)], dtype=np.int32)
     b = np.array([rng.randrange(200) for _ in range(1300)], dtype=np.int32)
     rs, re_ = oracle_mod.batch_dp(reads, a, b, 10, -1, -2)
-    with _engine_env({"OVL_DP_LANE": "1"}) as eng:
+    with _engine_env({"OVL_DP_FORM": "lane"}) as eng:
         eng.set_reads(reads)
         sc, en = eng.score(a, b, 10, -1, -2)
     np.testing.assert_array_equal(sc, rs)
@@ -108,7 +108,7 @@ def test_lane_wide_alphabet_vs_oracle(oracle_mod):
 
 def test_lane_and_fast_kernels_agree_at_scale(oracle_mod):
     """>= 65,536 pairs: the planner's automatic choice (lane kernel) equals dp_fast_kernel
-    (OVL_DP_LANE=0) on every pair, and the oracle on a strided sample."""
+    (OVL_DP_FORM=fast) on every pair, and the oracle on a strided sample."""
     from ovlgraph.candidates import dedup_reads, enumerate_candidates
     from ovlgraph.reads import read_genome_from_fasta, simulate_reads
     reads, _ = dedup_reads(simulate_reads(read_genome_from_fasta(), 150, 8000, 0.02, seed=1))
@@ -117,7 +117,7 @@ def test_lane_and_fast_kernels_agree_at_scale(oracle_mod):
     with _engine_env({}) as eng:
         eng.set_reads(reads)
         sc, en = eng.score(a, b, 10, -1, -2)
-    with _engine_env({"OVL_DP_LANE": "0"}) as eng:
+    with _engine_env({"OVL_DP_FORM": "fast"}) as eng:
         eng.set_reads(reads)
         fs, fe = eng.score(a, b, 10, -1, -2)
     np.testing.assert_array_equal(sc, fs)
@@ -133,7 +133,7 @@ def test_lane_falls_back_on_large_magnitudes(oracle_mod, mixed_set):
     reads, a, b = mixed_set
     params = (2 ** 20, -(2 ** 20), -(2 ** 19))
     rs, re_ = oracle_mod.batch_dp(reads, a[:500], b[:500], *params)
-    with _engine_env({"OVL_DP_LANE": "1"}) as eng:
+    with _engine_env({"OVL_DP_FORM": "lane"}) as eng:
         eng.set_reads(reads)
         sc, en = eng.score(a[:500], b[:500], *params)
     np.testing.assert_array_equal(sc, rs)
@@ -143,7 +143,7 @@ def test_lane_falls_back_on_large_magnitudes(oracle_mod, mixed_set):
 def test_lane_flags_bad_index(mixed_set):
     import torch
     reads, a, b = mixed_set
-    with _engine_env({"OVL_DP_LANE": "1"}) as eng:
+    with _engine_env({"OVL_DP_FORM": "lane"}) as eng:
         eng.set_reads(reads)
         da = torch.as_tensor(np.array([0, 1, len(reads) + 5, 2], dtype=np.int32), device="cuda")
         db = torch.as_tensor(np.array([1, 2, 3, -1], dtype=np.int32), device="cuda")

@@ -421,7 +421,7 @@ def test_t_truncated_pairs_in_sweep(oracle_mod, lw, split):
 
 @pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (2 ** 28, -(2 ** 28), -(2 ** 27))])
 def test_dp_fast_and_classic_agree_with_oracle(oracle_mod, params):
-    """Scores-only full DP runs dp_fast_kernel (chunked, unrolled); OVL_DP_CLASSIC=1 forces dp_kernel.
+    """Scores-only full DP runs dp_fast_kernel (chunked, unrolled); OVL_DP_FORM=classic forces dp_kernel.
     Lengths cross 64-row strips and 64-column chunks on both axes; the last set wraps int32 stores."""
     import os
     from ovlgraph import OverlapEngine
@@ -432,15 +432,15 @@ def test_dp_fast_and_classic_agree_with_oracle(oracle_mod, params):
     a = np.array([rng.randrange(n) for _ in range(900)], dtype=np.int32)
     b = np.array([rng.randrange(n) for _ in range(900)], dtype=np.int32)
     rs, re_ = oracle_mod.batch_dp(reads, a, b, *params)
-    for classic in ("0", "1"):
-        os.environ["OVL_DP_CLASSIC"] = classic
+    for form in ("fast", "classic"):
+        os.environ["OVL_DP_FORM"] = form
         try:
             with OverlapEngine(0) as eng:
                 eng.set_reads(reads)
                 assert eng.plan(*params) == "dp"
                 sc, en = eng.score(a, b, *params)
         finally:
-            del os.environ["OVL_DP_CLASSIC"]
+            del os.environ["OVL_DP_FORM"]
         np.testing.assert_array_equal(sc, rs)
         np.testing.assert_array_equal(en, re_)
 

@@ -110,13 +110,13 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
     slot reuse (many chunks, 1000-pair chunks that are not a multiple of the 64-pair rounding), bad pairs
     expanded to (-1, -1); pinned arrays with 0-100 % of the pairs in
     direct int32 chunks after the packed ones; OVL_PACK=0 is the int32 transport.  (OVL_PACK_MIN=0: packed
-    below the default 1 M-pair threshold; OVL_PAIRS_COMPACT=0: the pair list crosses as int32, 8 B/pair --
+    below the default 1 M-pair threshold; OVL_PAIRS_FORM=plain: the pair list crosses as int32, 8 B/pair --
     the compact encoding has its own tests, test_gpu_compact_pairs.py.)"""
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
     eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_MIN": "0", "OVL_PACK_DIRECT_PCT": pct,
-                       "OVL_PIPE_CHUNK": chunk, "OVL_PAIRS_COMPACT": "0"})
+                       "OVL_PIPE_CHUNK": chunk, "OVL_PAIRS_FORM": "plain"})
     try:
         eng.set_reads(reads)
         n = a.shape[0] - 3
@@ -193,7 +193,7 @@ def test_tile_records(oracle_mod, cfg2, pack, scoring):
     ref_s, ref_e = ref_s.copy(), ref_e.copy()
     ref_s[bad] = ref_e[bad] = -1
     for pct in ("0", "25"):
-        eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_DIRECT_PCT": pct, "OVL_PAIRS_COMPACT": "0"})
+        eng = _engine_env({"OVL_PACK": pack, "OVL_PACK_DIRECT_PCT": pct, "OVL_PAIRS_FORM": "plain"})
         try:
             eng.set_reads(reads)
             outs = {"pinned": (pinned_empty(n), pinned_empty(n)),
@@ -234,7 +234,7 @@ def test_tile_records_phases(oracle_mod, cfg2, cfg2_ref):
     sizes = [N, N // 3 + 17, N, N // 2 + 1, 70_000, N - 64, N // 3 + 17, N, 65_536, N]
     for chunk in ("0", "40000"):
         eng = _engine_env({"OVL_PACK": "2", "OVL_PACK_MIN": "0", "OVL_PACK_DIRECT_PCT": "0", "OVL_PIPE_CHUNK": chunk,
-                           "OVL_PAIRS_COMPACT": "0"})
+                           "OVL_PAIRS_FORM": "plain"})
         try:
             eng.set_reads(reads)
             out = (pinned_empty(N), pinned_empty(N))
@@ -611,7 +611,7 @@ def test_lane_kernel_on_two_streams(oracle_mod, cfg2):
     """dp_lane_kernel launches on different streams are ordered on the shared hand-off buffer."""
     import torch
     reads, a, b = cfg2
-    eng = _engine_env({"OVL_DP_LANE": "1"})
+    eng = _engine_env({"OVL_DP_FORM": "lane"})
     try:
         eng.set_reads(reads)
         ta = torch.as_tensor(a, device="cuda")
@@ -664,11 +664,11 @@ def test_cfg5_full_default_scoring_vs_oracle(engine, oracle_mod, cfg5):
 
 def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
     """Gapped (indel -2) on the whole cfg5 list: dp_lane_kernel (the planner's choice) ==
-    dp_fast_kernel (OVL_DP_LANE=0) pair for pair; both == the oracle's full DP on a strided
+    dp_fast_kernel (OVL_DP_FORM=fast) pair for pair; both == the oracle's full DP on a strided
     50k-pair sample."""
     reads, a, b = cfg5
-    lane = _engine_env({"OVL_DP_LANE": "1"})
-    fast = _engine_env({"OVL_DP_LANE": "0"})
+    lane = _engine_env({"OVL_DP_FORM": "lane"})
+    fast = _engine_env({"OVL_DP_FORM": "fast"})
     try:
         lane.set_reads(reads)
         fast.set_reads(reads)

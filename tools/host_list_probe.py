@@ -23,7 +23,7 @@ def main():
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
     enc = encode_reads(reads)
     res = {}
-    for label, env in (("compact", {}), ("plain", {"OVL_PAIRS_COMPACT": "0"})):
+    for label, env in (("compact", {}), ("plain", {"OVL_PAIRS_FORM": "plain"})):
         os.environ.update(env)
         eng = OverlapEngine(0)
         for k in env:
