@@ -812,9 +812,12 @@ typedef struct {
     PyObject** ints;
     PyObject *tmpl, *kw, *ke;
     Py_ssize_t iw, ie;
+    PyObject** spec;        /* per edge: its attribute dict made ahead of its row (spec_advance), or NULL */
     int64_t n_rows;         /* complete rows */
     int64_t n_dec;          /* decided edges */
     int64_t n_ins;          /* live edges inserted */
+    int64_t n_spec;         /* attribute dicts made ahead */
+    int64_t n_spec_used;    /* ... and inserted */
 } RowCtx;
 
 /* advance u's row; `all`: u is published (every edge decided).  1 if it moved, 0 if not, -1 on error */
@@ -841,11 +844,17 @@ static int row_advance(RowCtx* R, int64_t u, int all) {
             }
             if (live) {
                 if (!R->rows[u] && !(R->rows[u] = _PyDict_NewPresized(R->outdeg[u]))) return -1;
-                PyObject* wv = int_of(R->ints, R->sc[p]);
-                PyObject* ev = int_of(R->ints, R->en[p]);
-                PyObject* d = wv && ev ? new_attr(R->tmpl, R->kw, R->ke, R->iw, R->ie, wv, ev) : NULL;
-                Py_XDECREF(wv);
-                Py_XDECREF(ev);
+                PyObject* d = R->spec[e];
+                if (d) {
+                    R->spec[e] = NULL;
+                    ++R->n_spec_used;
+                } else {
+                    PyObject* wv = int_of(R->ints, R->sc[p]);
+                    PyObject* ev = int_of(R->ints, R->en[p]);
+                    d = wv && ev ? new_attr(R->tmpl, R->kw, R->ke, R->iw, R->ie, wv, ev) : NULL;
+                    Py_XDECREF(wv);
+                    Py_XDECREF(ev);
+                }
                 const int bad = !d || PyDict_SetItem(R->rows[u], PyList_GET_ITEM(R->P->names, vb + cb), d);
                 if (bad) {
                     Py_XDECREF(d);
@@ -870,6 +879,43 @@ static int row_advance(RowCtx* R, int64_t u, int all) {
     return 1;
 }
 
+/* Idle work while the replay runs: the attribute dicts of the still-undecided live out-edges of the nodes from *su on,
+   made ahead of their rows (row_advance takes them), up to `budget` of them.  Making an edge's dict is about half of
+   what inserting it costs, and the edges whose fate the replay decides last -- the graph's last cycles -- are
+   otherwise all built after it has ended; an edge removed after its dict was made only costs that dict (released at
+   the end).  Each node once, in node order.  Returns the dicts made (0: every node passed), -1 on error. */
+static int64_t spec_advance(RowCtx* R, int64_t* su, int64_t n_nodes, int64_t budget) {
+    const Layout* L = R->P->L;
+    int64_t made = 0;
+    while (*su < n_nodes && made < budget) {
+        const int64_t u = (*su)++;
+        int64_t g = R->rg[u];
+        if (g < 0 || R->pub[u]) continue;  /* (row complete, or published: built next) */
+        const Py_ssize_t r = (Py_ssize_t)R->P->rread[u];
+        const int64_t gend = L->goff[r + 1];
+        int32_t cb = R->rc[u];
+        for (; g < gend; ++g, cb = 0) {
+            const int64_t p = L->plist[g];
+            const int64_t e0 = L->off[u] + L->pstart[p];
+            const int32_t nb = R->counts[R->b[p]];
+            for (; cb < nb; ++cb) {
+                const int64_t e = e0 + cb;
+                if (R->spec[e] || !__atomic_load_n(&R->alive[e], __ATOMIC_ACQUIRE)) continue;
+                PyObject* wv = int_of(R->ints, R->sc[p]);
+                PyObject* ev = int_of(R->ints, R->en[p]);
+                PyObject* d = wv && ev ? new_attr(R->tmpl, R->kw, R->ke, R->iw, R->ie, wv, ev) : NULL;
+                Py_XDECREF(wv);
+                Py_XDECREF(ev);
+                if (!d) return -1;
+                R->spec[e] = d;
+                ++made;
+            }
+        }
+    }
+    R->n_spec += made;
+    return made;
+}
+
 /* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
  *     -> (node, succ, pred, removed, n_removed)
  * remove_cycles_from_graph on a graph that is still columns, with the replay and the dicts overlapped: the replay
@@ -883,6 +929,10 @@ static int row_advance(RowCtx* R, int64_t u, int all) {
 /* OVL_TRACE_STREAM=1 (diagnostics): one stderr line per build_overlap_stream with the millisecond offsets of its
    phases (s setup done, r replay finished as seen here, with the share of the nodes whose rows were built by
    then, b dicts built, t top-level dicts), the replay thread's own time and the CPUs both threads ran on */
+/* the streamed builder's sweeps of its open rows, at most one per this many ms (target point, this container's CPU,
+   three runs each: 0 -> 1 ms, build_overlap_stream 1.69-1.79 -> 1.49-1.60 s) */
+static const double kSweepMs = 1.0;
+
 static double now_ms(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -955,7 +1005,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     double t_setup = 0.0, t_replay = -1.0, t_built = 0.0;
     int64_t k_at_replay = 0, dec_at_replay = 0, ins_at_replay = 0;
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
-    PyObject **rows = NULL, **dptr = NULL, **pin = NULL;
+    PyObject **rows = NULL, **dptr = NULL, **pin = NULL, **spec = NULL;
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t* rread = NULL;
     int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL, *pg = NULL, *pt = NULL, *rg = NULL;
@@ -996,12 +1046,13 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         rows = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
         pin = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
         dptr = (PyObject**)PyMem_Calloc((size_t)(E ? E : 1), sizeof(PyObject*));
+        spec = (PyObject**)PyMem_Calloc((size_t)(E ? E : 1), sizeof(PyObject*));
         rread = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(N ? N : 1));
         /* in-edges in insertion order: the kept pairs grouped by b (list order within a group) */
         bgoff = (int64_t*)PyMem_Calloc((size_t)L.R + 1, sizeof(int64_t));
         blist = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(L.P ? L.P : 1));
         pending = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
-        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !rread || !bgoff ||
+        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !spec || !rread || !bgoff ||
             !blist || !pending) {
             PyErr_NoMemory();
             goto done;
@@ -1091,7 +1142,9 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         }
         int64_t n_open = N;
         RowCtx R = {&X, counts, b, sc, en, job.alive, pubd, outdeg, rows, dptr, dec, rg, rc, ints, tmpl, kw, ke, iw, ie,
-                    0, 0, 0};
+                    spec, 0, 0, 0, 0, 0};
+        int64_t spec_u = 0;     /* spec_advance's next node */
+        double t_sweep = -1e9;  /* the last sweep's start (ms) */
         for (int64_t v = 0; v < N; ++v)
             if (pred_advance(&X, v)) goto done;  /* (completes the nodes without in-edges) */
         for (;;) {
@@ -1119,7 +1172,20 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                 if (__atomic_load_n(&job.n_final, __ATOMIC_ACQUIRE) > k_done) continue;
                 break;
             }
-            /* nothing newly published: advance the openl rows as far as their heads allow */
+            /* nothing newly published: advance the openl rows as far as their heads allow -- at most once per
+               kSweepMs (a sweep calls row_advance on every open row, hundreds of millions of calls over a run when
+               repeated back to back); in between, and after a sweep that moved nothing, make attribute dicts ahead */
+            if (now_ms() - t_sweep < kSweepMs) {
+                const int64_t m = spec_advance(&R, &spec_u, N, 256);
+                if (m < 0) goto done;
+                if (m == 0) {
+                    Py_BEGIN_ALLOW_THREADS
+                    sched_yield();
+                    Py_END_ALLOW_THREADS
+                }
+                continue;
+            }
+            t_sweep = now_ms();
             int moved = 0;
             int64_t keep_n = 0;
             for (int64_t i = 0; i < n_open; ++i) {
@@ -1137,10 +1203,14 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             }
             n_open = keep_n;
             ++n_sweeps;
-            if (!moved) {
-                Py_BEGIN_ALLOW_THREADS
-                sched_yield();
-                Py_END_ALLOW_THREADS
+            if (!moved) {  /* nothing to insert yet: make attribute dicts ahead, else yield */
+                const int64_t m = spec_advance(&R, &spec_u, N, 256);
+                if (m < 0) goto done;
+                if (m == 0) {
+                    Py_BEGIN_ALLOW_THREADS
+                    sched_yield();
+                    Py_END_ALLOW_THREADS
+                }
             }
         }
         const int64_t n_rows = R.n_rows;
@@ -1174,11 +1244,11 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
         if (trace)
             fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows, %.0f%% edges, %lld inserted) b=%.1f t=%.1f sweeps=%lld scc=%d passes=%d first=%lld "
-                    "replay=%.1f cpus main %d/%d replay %d/%d\n", t_setup, t_replay,
+                    "replay=%.1f cpus main %d/%d replay %d/%d spec %lld used %lld\n", t_setup, t_replay,
                     N ? 100.0 * (double)k_at_replay / (double)N : 100.0,
                     E ? 100.0 * (double)dec_at_replay / (double)E : 100.0, (long long)ins_at_replay, t_built, now_ms() - t0, (long long)n_sweeps,
                     scc_on, scc.passes,
-                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end);
+                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end, (long long)R.n_spec, (long long)R.n_spec_used);
     }
 done:
     if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */
@@ -1215,6 +1285,10 @@ done:
     if (dptr) {
         for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(dptr[e]);
         PyMem_Free(dptr);
+    }
+    if (spec) {  /* (the dicts made ahead for edges the replay then removed) */
+        for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(spec[e]);
+        PyMem_Free(spec);
     }
     PyMem_Free(rread);
     PyMem_Free(bgoff);

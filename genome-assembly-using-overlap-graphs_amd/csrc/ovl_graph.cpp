@@ -79,16 +79,6 @@ class HugeArray {
     std::vector<T> heap_;
 };
 
-// One undo-log record per iterator advance of `node` (its old position).  A yield that reaches a node for the
-// first time also carries that node (`first`; -1 otherwise): its first visit and 'seen' insertion happen at
-// that yield (a yielded head becomes the next current node unless the edge closes a cycle, which rewinds past
-// the yield), so one record undoes all three.
-struct Event {
-    int32_t node;
-    int32_t old;
-    int32_t first;
-};
-
 // Nodes whose out-edges are final, published as they become so (ovl_remove_cycles_stream): a node that is
 // settled (below) or explored (reached by a start whose walk found no cycle) can reach no cycle, so none of its
 // out-edges is ever removed.  nodes[0 .. *count) are published with a release store of *count; a consumer on
@@ -182,9 +172,9 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
              int64_t* n_removed, uint8_t* alive_out, Publish& pub) {
     const int64_t n_edges = off[n_nodes];
 
-    // Per edge, what one yield touches, in one record: the head, the skip delta to the next edge that may
-    // still be yielded (0: this one; edges removed or into explored / settled nodes are spliced out), the
-    // weight.  A sentinel record ends the array.
+    // Per edge: the head, the skip delta to the next edge that may still be yielded (0: this one; edges removed
+    // or into explored / settled nodes are spliced out), the weight.  A sentinel record ends the array.  Read only
+    // to find a node's next live edge after a yield, not by the yield itself (Node below).
     struct Edge {
         int32_t head;
         int32_t skip;
@@ -197,16 +187,41 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                                                                                             // settled (only grow)
     uint8_t* alive = alive_out ? alive_out : alive_own.data();
     if (alive_out) memset(alive_out, 1, (size_t)n_edges);
-    // per node, what a yield touches, in one record: the out-edge iterator position (CSR index) of a visited
-    // node, the index of the path edge leaving it (valid while active), visited (= seen: both happen at the
-    // yield that first reaches it) and on the active path
+    // Per node, what a yield touches, in one record (20 bytes: the target point's 50,000 nodes fit a core's L2).
+    // The out-edge iterator is held as the edge it yields next: cq, its CSR index, and when `cv` also its head ch
+    // and weight cw, so a yield reads no edge record -- the edge array (45 MB at the target point) is read only to
+    // find the next live edge after a yield (cv = 0: scan from cq), off the walk's critical path.  "Live" only ever
+    // turns false (removal, head explored / settled), so a cached edge whose head is not done is still the next
+    // live one, except the removed edge itself (its tail's cache is dropped at the removal).  Also: the index of
+    // the path edge leaving the node (valid while active), visited (= seen: both happen at the yield that first
+    // reaches it) and on the active path.  A node starts with its row's first edge cached.
     struct Node {
-        int32_t pos;
+        int32_t cq, ch;
+        WT cw;
         int32_t tail_pos;
-        uint8_t visited;
-        uint8_t active;
+        uint8_t visited, active, cv;
     };
-    std::vector<Node> nd((size_t)n_nodes, Node{0, 0, 0, 0});
+    std::vector<Node> nd((size_t)n_nodes);
+    for (int32_t v = 0; v < n_nodes; ++v) {
+        Node& x = nd[(size_t)v];
+        x = Node{};
+        x.cq = (int32_t)off[v];
+        if (off[v] < off[v + 1]) {
+            x.ch = head[off[v]];
+            x.cw = (WT)weight[off[v]];
+        }
+        x.cv = 1;
+    }
+    // One undo-log record per yield: the yielding node and the edge it yielded (index, head, weight: undoing the
+    // yield puts that edge back as the node's cached next edge), and, when the yield reached its head for the
+    // first time, that head (`first`; -1 otherwise): its first visit and 'seen' insertion happen at that yield
+    // (a yielded head becomes the next current node unless the edge closes a cycle, which rewinds past the
+    // yield), so one record undoes all three.  Undoing a node's yields restores its cache as of its first visit,
+    // so a first visit after an undone one needs no reset.  (Scans that only move past dead edges are not logged.)
+    struct Event {
+        int32_t node, q, first, h;
+        WT w;
+    };
     // find_cycle's `edges`: the active path, one record per path edge: the undo-log size just before it was
     // yielded, its weight, CSR index, tail (the node whose iterator yielded it), head, and `link`: the last
     // earlier path edge whose weight is <= this one's (-1: none).  From the path's end, the link chain visits
@@ -231,6 +246,23 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
 
     Edge* E = ed.data();
     Node* N = nd.data();
+    const uint8_t* D = done.data();
+    // the first live edge at or after q (end if none).  Edges into explored or settled nodes are walked by
+    // edge_dfs without any effect on find_cycle, and both sets only grow, so such an edge is spliced out of
+    // every later iteration (skip deltas, shared with the removed edges) instead of being yielded.
+    auto next_live = [E, D](int64_t q, int64_t end) -> int64_t {
+        for (;;) {
+            while (E[q].skip) {  // (path halving)
+                const int64_t p1 = q + E[q].skip;
+                const int64_t p2 = p1 + E[p1].skip;
+                E[q].skip = (int32_t)(p2 - q);
+                q = p2;
+            }
+            if (q >= end) return end;
+            if (!D[E[q].head]) return q;
+            E[q].skip = 1;
+        }
+    };
     for (int32_t s = 0; s < n_nodes; ++s) {
         if (done[s]) continue;
         log.clear();
@@ -240,7 +272,6 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
         int32_t root = s;  // find_cycle's path root (the start node; a reset re-roots at the tail)
         // the start node's first visit is never rewound (every rewind target is a later yield's checkpoint)
         N[s].visited = 1;
-        N[s].pos = (int32_t)off[s];
         N[s].active = 1;
         seen_list.push_back(s);
         int32_t prev_head = -1;
@@ -256,43 +287,30 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                 break;
             }
             const int32_t cur = stack.back();
-            // next yield of cur's iterator.  Edges into explored or settled nodes are walked by edge_dfs
-            // without any effect on find_cycle, and both sets only grow, so such an edge is spliced out
-            // of every later iteration (skip deltas, shared with the removed edges) instead of being
-            // yielded; the iterator advance over a run of them is logged once with the yield after it.
+            Node& c = N[cur];
             const int64_t end = off[cur + 1];
-            int64_t q = N[cur].pos;
-            for (;;) {
-                while (E[q].skip) {  // first live edge at or after q (path halving)
-                    const int64_t p1 = q + E[q].skip;
-                    const int64_t p2 = p1 + E[p1].skip;
-                    E[q].skip = (int32_t)(p2 - q);
-                    q = p2;
+            if (!c.cv || (c.cq < end && D[c.ch])) {  // next live edge of cur's iterator from the edge records
+                const int64_t q = next_live(c.cq, end);
+                c.cq = (int32_t)q;
+                if (q < end) {
+                    c.ch = E[q].head;
+                    c.cw = E[q].w;
                 }
-                if (q >= end) {
-                    q = end;
-                    break;
-                }
-                if (!done[E[q].head]) break;
-                E[q].skip = 1;
+                c.cv = 1;
             }
+            const int64_t q = c.cq;
             if (q == end) {  // iterator exhausted: pop
-                if (N[cur].pos != q) {
-                    log.push_back({cur, N[cur].pos, -1});
-                    N[cur].pos = (int32_t)q;
-                }
                 stack.pop_back();
                 continue;
             }
             // yield edge q = (cur, h)
             const int64_t mark = (int64_t)log.size();
-            log.push_back({cur, N[cur].pos, -1});
-            N[cur].pos = (int32_t)(q + 1);
-            const int32_t h = E[q].head;
-            // h is the next node to walk (unless the edge closes a cycle): start the fetch of its next edge
-            // record now, ahead of the path bookkeeping below (a random row of the edge array; -7..12 % on
-            // the target point's replay, tools/replay_ab.py)
-            __builtin_prefetch(&E[N[h].visited ? N[h].pos : off[h]]);
+            const int32_t h = c.ch;
+            const WT w = c.cw;
+            log.push_back({cur, (int32_t)q, -1, h, w});
+            c.cq = (int32_t)(q + 1);
+            c.cv = 0;
+            __builtin_prefetch(&E[q + 1]);  // (for cur's next yield, after the walk below h returns to it)
             stack.push_back(h);
             if (prev_head >= 0 && cur != prev_head) {
                 // backtracking: pop the path back to the edge whose head is cur (or empty it)
@@ -308,15 +326,15 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                     if (!path.empty() && path.back().head == cur) break;
                 }
             }
-            const int64_t w = E[q].w;
             int32_t link = (int32_t)path.size() - 1;
-            while (link >= 0 && path[(size_t)link].w > w) link = path[(size_t)link].link;
-            N[cur].tail_pos = (int32_t)path.size();
-            path.push_back({mark, w, (int32_t)q, cur, h, link});
-            if (N[h].active) {
+            while (link >= 0 && path[(size_t)link].w > (int64_t)w) link = path[(size_t)link].link;
+            c.tail_pos = (int32_t)path.size();
+            path.push_back({mark, (int64_t)w, (int32_t)q, cur, h, link});
+            Node& hn = N[h];
+            if (hn.active) {
                 // cycle: the path suffix from the first edge leaving h (the path is simple, so that edge is
                 // tail_pos[h]); remove its weakest edge, the first minimum in cycle order
-                const int32_t i0 = N[h].tail_pos;
+                const int32_t i0 = hn.tail_pos;
                 const PathEdge* pp = path.data();
                 int32_t kmin = (int32_t)path.size() - 1;
                 while (pp[kmin].link >= i0) kmin = pp[kmin].link;
@@ -334,12 +352,17 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                 while ((int64_t)log.size() > target) {
                     const Event ev = log.back();
                     log.pop_back();
-                    N[ev.node].pos = ev.old;
+                    Node& x = N[ev.node];
+                    x.cq = ev.q;
+                    x.ch = ev.h;
+                    x.cw = ev.w;
+                    x.cv = 1;
                     if (ev.first >= 0) {
                         N[ev.first].visited = 0;
                         seen_list.pop_back();
                     }
                 }
+                N[tail_of_dead].cv = 0;  // (its cached next edge is now the removed one)
                 // heads leaving the path (not the closing edge's: that node is on the surviving path)
                 for (size_t k = (size_t)kmin; k + 1 < path.size(); ++k) N[pp[k].head].active = 0;
                 N[root].active = 1;  // (the root is unchanged since path[kmin] was yielded)
@@ -356,13 +379,12 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                 prev_head = kmin > 0 ? path[(size_t)kmin - 1].head : -1;
                 continue;
             }
-            if (!N[h].visited) {  // first visit (and 'seen' insertion) of h, undone with this yield
-                N[h].visited = 1;
-                N[h].pos = (int32_t)off[h];
+            if (!hn.visited) {  // first visit (and 'seen' insertion) of h, undone with this yield
+                hn.visited = 1;
                 seen_list.push_back(h);
                 log.back().first = h;
             }
-            N[h].active = 1;
+            hn.active = 1;
             prev_head = h;
         }
     }
