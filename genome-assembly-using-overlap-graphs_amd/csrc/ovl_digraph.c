@@ -813,6 +813,7 @@ typedef struct {
     PyObject *tmpl, *kw, *ke;
     Py_ssize_t iw, ie;
     PyObject** spec;        /* per edge: its attribute dict made ahead of its row (spec_advance), or NULL */
+    int own;                /* dptr holds a reference (only when some (a, b) pair is listed twice, below) */
     int64_t n_rows;         /* complete rows */
     int64_t n_dec;          /* decided edges */
     int64_t n_ins;          /* live edges inserted */
@@ -860,8 +861,11 @@ static int row_advance(RowCtx* R, int64_t u, int all) {
                     Py_XDECREF(d);
                     return -1;
                 }
-                /* owned (released in build_overlap_stream's exit): a duplicated (a, b) pair replaces the row's
-                   entry, freeing the first dict while its head's predecessor cursor may still be short of it */
+                /* dptr[e] is read by the head's predecessor cursor, which may still be short of e.  The row holds
+                   the dict, so dptr borrows it -- unless some (a, b) pair is listed twice (not a list
+                   overlapGraphs.py:43-52 makes, but OverlapEdges accepts it): the second replaces the row's entry
+                   and would free the first dict, so then dptr keeps a reference, released at the exit */
+                if (!R->own) Py_DECREF(d);
                 R->dptr[e] = d;
                 ++R->n_ins;
             }
@@ -884,7 +888,11 @@ static int row_advance(RowCtx* R, int64_t u, int all) {
    what inserting it costs, and the edges whose fate the replay decides last -- the graph's last cycles -- are
    otherwise all built after it has ended; an edge removed after its dict was made only costs that dict (released at
    the end).  Each node once, in node order.  Returns the dicts made (0: every node passed), -1 on error. */
+#ifndef OVL_SPEC_AHEAD
+#define OVL_SPEC_AHEAD 1 /* (0: no dicts made ahead -- an A/B build, tools/stream_ab.py) */
+#endif
 static int64_t spec_advance(RowCtx* R, int64_t* su, int64_t n_nodes, int64_t budget) {
+    if (!OVL_SPEC_AHEAD) return 0;
     const Layout* L = R->P->L;
     int64_t made = 0;
     while (*su < n_nodes && made < budget) {
@@ -914,6 +922,24 @@ static int64_t spec_advance(RowCtx* R, int64_t* su, int64_t n_nodes, int64_t bud
     }
     R->n_spec += made;
     return made;
+}
+
+/* Idle work once every node has had its dicts made ahead: release the made-ahead dicts of edges the replay has
+   removed since, `budget` entries of the edge array per call, cycling over it, so that few are left to release after
+   the replay.  Returns the dicts released. */
+static int64_t spec_reap(RowCtx* R, int64_t* re, int64_t n_edges, int64_t budget) {
+    int64_t freed = 0;
+    for (int64_t k = 0; k < budget && n_edges > 0; ++k) {
+        const int64_t e = (*re)++;
+        if (*re >= n_edges) *re = 0;
+        PyObject* d = R->spec[e];
+        if (d && !__atomic_load_n(&R->alive[e], __ATOMIC_ACQUIRE)) {
+            R->spec[e] = NULL;
+            Py_DECREF(d);
+            ++freed;
+        }
+    }
+    return freed;
 }
 
 /* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
@@ -1006,6 +1032,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     int64_t k_at_replay = 0, dec_at_replay = 0, ins_at_replay = 0;
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
     PyObject **rows = NULL, **dptr = NULL, **pin = NULL, **spec = NULL;
+    int own_refs = 1;  /* dptr's entries are references (until the columns are known free of repeated pairs) */
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t* rread = NULL;
     int64_t *bgoff = NULL, *blist = NULL, *pending = NULL, *ready = NULL, *pg = NULL, *pt = NULL, *rg = NULL;
@@ -1141,9 +1168,24 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             openl[v] = v;
         }
         int64_t n_open = N;
+        /* some read's kept pairs list the same b twice? (then dptr owns its references, RowCtx.own) */
+        int dup = 0;
+        {
+            int32_t* stamp = (int32_t*)PyMem_Calloc((size_t)(L.R ? L.R : 1), sizeof(int32_t));
+            if (!stamp) { PyErr_NoMemory(); goto done; }
+            for (Py_ssize_t r = 0; r < L.R && !dup; ++r)
+                for (int64_t g = L.goff[r]; g < L.goff[r + 1]; ++g) {
+                    const int32_t bb = b[L.plist[g]];
+                    if (stamp[bb] == (int32_t)r + 1) { dup = 1; break; }
+                    stamp[bb] = (int32_t)r + 1;
+                }
+            PyMem_Free(stamp);
+        }
+        own_refs = dup;
         RowCtx R = {&X, counts, b, sc, en, job.alive, pubd, outdeg, rows, dptr, dec, rg, rc, ints, tmpl, kw, ke, iw, ie,
-                    spec, 0, 0, 0, 0, 0};
+                    spec, dup, 0, 0, 0, 0, 0};
         int64_t spec_u = 0;     /* spec_advance's next node */
+        int64_t reap_e = 0;     /* spec_reap's next edge */
         double t_sweep = -1e9;  /* the last sweep's start (ms) */
         for (int64_t v = 0; v < N; ++v)
             if (pred_advance(&X, v)) goto done;  /* (completes the nodes without in-edges) */
@@ -1178,6 +1220,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             if (now_ms() - t_sweep < kSweepMs) {
                 const int64_t m = spec_advance(&R, &spec_u, N, 256);
                 if (m < 0) goto done;
+                if (m == 0 && OVL_SPEC_AHEAD) (void)spec_reap(&R, &reap_e, E, 16384);
                 if (m == 0) {
                     Py_BEGIN_ALLOW_THREADS
                     sched_yield();
@@ -1282,14 +1325,19 @@ done:
         for (Py_ssize_t i = 0; i < L_N; ++i) Py_XDECREF(pin[i]);
         PyMem_Free(pin);
     }
+    const double tc0 = trace ? now_ms() : 0.0;
     if (dptr) {
-        for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(dptr[e]);
+        if (own_refs)
+            for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(dptr[e]);
         PyMem_Free(dptr);
     }
+    const double tc1 = trace ? now_ms() : 0.0;
     if (spec) {  /* (the dicts made ahead for edges the replay then removed) */
         for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(spec[e]);
         PyMem_Free(spec);
     }
+    if (trace) fprintf(stderr, "ovl_stream exit: references %.1f ms, dicts made ahead and unused %.1f ms\n", tc1 - tc0,
+                       now_ms() - tc1);
     PyMem_Free(rread);
     PyMem_Free(bgoff);
     PyMem_Free(blist);
