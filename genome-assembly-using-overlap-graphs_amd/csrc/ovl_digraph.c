@@ -952,13 +952,23 @@ static int64_t spec_reap(RowCtx* R, int64_t* re, int64_t n_edges, int64_t budget
  * order (pairs with b = its read in list order, then the copies of a: overlapGraphs.py:43-60); then the
  * node-ordered top-level dicts.  The result is build_overlap's for the alive mask of the replay; removed holds
  * the replay's removed CSR indices (int64) in removal order. */
-/* OVL_TRACE_STREAM=1 (diagnostics): one stderr line per build_overlap_stream with the millisecond offsets of its
-   phases (s setup done, r replay finished as seen here, with the share of the nodes whose rows were built by
-   then, b dicts built, t top-level dicts), the replay thread's own time and the CPUs both threads ran on */
+/* The collector.  The builder runs with the collector off (millions of new objects), so the first allocation after it
+   is back on collects the young generation: every row and predecessor dict built, traversing their millions of
+   entries (~0.12 s at the target point on the box, the caller's time).  The builder instead collects the young
+   generations itself (gc.collect(1): generations 0 and 1, so the next automatic collection stays a generation-0
+   one) in idle time while the replay still runs, when these shares of the edges are decided, leaving only the
+   dicts built after the last one for that first collection.  At most kGcMid times: each adds one to generation 2's
+   count, whose threshold (10) arms a full collection. */
+static const int kGcMid = 3;
+static const double kGcAt[3] = {0.30, 0.50, 0.65};
+
 /* the streamed builder's sweeps of its open rows, at most one per this many ms (target point, this container's CPU,
    three runs each: 0 -> 1 ms, build_overlap_stream 1.69-1.79 -> 1.49-1.60 s) */
 static const double kSweepMs = 1.0;
 
+/* OVL_TRACE_STREAM=1 (diagnostics): one stderr line per build_overlap_stream with the millisecond offsets of its
+   phases (s setup done, r replay finished as seen here, with the share of the nodes whose rows were built by
+   then, b dicts built, t top-level dicts), the replay thread's own time and the CPUs both threads ran on */
 static double now_ms(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -1032,6 +1042,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     int64_t k_at_replay = 0, dec_at_replay = 0, ins_at_replay = 0;
     PyObject *node = NULL, *succ = NULL, *pred = NULL, *kw = NULL, *ke = NULL, *tmpl = NULL, *out = NULL;
     PyObject **rows = NULL, **dptr = NULL, **pin = NULL, **spec = NULL;
+    PyObject* gc_collect = NULL;
     int own_refs = 1;  /* dptr's entries are references (until the columns are known free of repeated pairs) */
     PyObject** ints = (PyObject**)PyMem_Calloc((size_t)(kIntHi - kIntLo), sizeof(PyObject*));
     int64_t* rread = NULL;
@@ -1046,6 +1057,38 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
     if (bs.len != C.a.len || be.len != C.a.len) {
         PyErr_SetString(PyExc_ValueError, "score and end must have one entry per pair");
         goto done;
+    }
+    /* the replay needs only the CSR: start it first, and lay out the columns while it runs (the CSR is checked
+       against them below; on a mismatch the replay of the caller's CSR still ends, is joined and the call fails) */
+    if (boff.len < 8 || bh.len / 4 != bw.len / 8 || boff.len / 8 - 1 >= ((Py_ssize_t)1 << 31)) {
+        PyErr_SetString(PyExc_ValueError, "names / CSR do not match the columns' graph");
+        goto done;
+    }
+    {
+        const int64_t E = (int64_t)(bh.len / 4), N = (int64_t)(boff.len / 8 - 1);
+        job.fn = (replay_stream_fn)(uintptr_t)fn_addr;
+        job.off = (const int64_t*)boff.buf;
+        job.heads = (const int32_t*)bh.buf;
+        job.w = (const int64_t*)bw.buf;
+        job.n = (int32_t)N;
+        job.removed = (int64_t*)PyMem_RawMalloc(sizeof(int64_t) * (size_t)(E ? E : 1));
+        job.alive = (uint8_t*)PyMem_RawMalloc((size_t)(E ? E : 1));
+        job.final_nodes = (int32_t*)PyMem_RawMalloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+        if (!job.removed || !job.alive || !job.final_nodes) {
+            PyErr_NoMemory();
+            goto done;
+        }
+        /* all ones before either thread starts (the replay sets it too, but on its own thread, where the component
+           helper could read it first) */
+        memset(job.alive, 1, (size_t)E);
+        job.cpu_main = sched_getcpu();
+        job.gate = scc_on != 2;
+        if (pthread_create(&th, NULL, replay_main, &job) != 0) {
+            PyErr_SetString(PyExc_RuntimeError, "cannot start the replay thread");
+            goto done;
+        }
+        started = 1;
+        if (trace) t_setup = now_ms() - t0;
     }
     {
         const int32_t* counts = (const int32_t*)C.c.buf;
@@ -1062,14 +1105,6 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
             goto done;
         }
         const int64_t E = L.E, N = L.N;
-        job.fn = (replay_stream_fn)(uintptr_t)fn_addr;
-        job.off = (const int64_t*)boff.buf;
-        job.heads = (const int32_t*)bh.buf;
-        job.w = (const int64_t*)bw.buf;
-        job.n = (int32_t)N;
-        job.removed = (int64_t*)PyMem_RawMalloc(sizeof(int64_t) * (size_t)(E ? E : 1));
-        job.alive = (uint8_t*)PyMem_RawMalloc((size_t)(E ? E : 1));
-        job.final_nodes = (int32_t*)PyMem_RawMalloc(sizeof(int32_t) * (size_t)(N ? N : 1));
         rows = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
         pin = (PyObject**)PyMem_Calloc((size_t)(N ? N : 1), sizeof(PyObject*));
         dptr = (PyObject**)PyMem_Calloc((size_t)(E ? E : 1), sizeof(PyObject*));
@@ -1079,14 +1114,10 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         bgoff = (int64_t*)PyMem_Calloc((size_t)L.R + 1, sizeof(int64_t));
         blist = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(L.P ? L.P : 1));
         pending = (int64_t*)PyMem_Calloc((size_t)(N ? N : 1), sizeof(int64_t));
-        if (!job.removed || !job.alive || !job.final_nodes || !rows || !pin || !dptr || !spec || !rread || !bgoff ||
-            !blist || !pending) {
+        if (!rows || !pin || !dptr || !spec || !rread || !bgoff || !blist || !pending) {
             PyErr_NoMemory();
             goto done;
         }
-        /* all ones before either thread starts (the replay sets it too, but on its own thread, where the component
-           helper could read it first) */
-        memset(job.alive, 1, (size_t)E);
         for (Py_ssize_t r = 0; r < L.R; ++r)
             for (int64_t u = L.first[r]; u < L.first[r + 1]; ++u) rread[u] = r;
         for (Py_ssize_t p = 0; p < L.P; ++p)
@@ -1120,15 +1151,13 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         Py_ssize_t iw, ie;
         attr_slots(tmpl, kw, ke, &iw, &ie);
         {
-            job.cpu_main = sched_getcpu();
-            job.gate = scc_on != 2;
+            PyObject* gcm = PyImport_ImportModule("gc");
+            if (!gcm) goto done;
+            gc_collect = PyObject_GetAttrString(gcm, "collect");
+            Py_DECREF(gcm);
+            if (!gc_collect) goto done;
         }
-        if (pthread_create(&th, NULL, replay_main, &job) != 0) {
-            PyErr_SetString(PyExc_RuntimeError, "cannot start the replay thread");
-            goto done;
-        }
-        started = 1;
-        if (trace) t_setup = now_ms() - t0;
+        if (trace) t_setup = now_ms() - t0;  /* (s: the builder's setup done, the replay running since the start) */
         /* successors of each node as its out-edges become final (row order: kept pairs with a == its read in
            list order, then the copies of b) -- published by the replay (settled or explored nodes) or by the
            component helper (scc_main), whichever comes first; predecessors of each node once every tail of its
@@ -1186,6 +1215,8 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                     spec, dup, 0, 0, 0, 0, 0};
         int64_t spec_u = 0;     /* spec_advance's next node */
         int64_t reap_e = 0;     /* spec_reap's next edge */
+        int n_gc = 0;           /* collections of the young generations run so far (kGcMid) */
+        double t_gc = 0.0;
         double t_sweep = -1e9;  /* the last sweep's start (ms) */
         for (int64_t v = 0; v < N; ++v)
             if (pred_advance(&X, v)) goto done;  /* (completes the nodes without in-edges) */
@@ -1221,6 +1252,16 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                 const int64_t m = spec_advance(&R, &spec_u, N, 256);
                 if (m < 0) goto done;
                 if (m == 0 && OVL_SPEC_AHEAD) (void)spec_reap(&R, &reap_e, E, 16384);
+                if (m == 0 && gc_collect && n_gc < kGcMid && R.n_dec >= (int64_t)(kGcAt[n_gc] * (double)E)) {
+                    /* the collector's pass over the dicts built so far, now, beside the replay (see kGcMid) */
+                    const double tg = now_ms();
+                    PyObject* res = PyObject_CallFunction(gc_collect, "i", 1);
+                    if (!res) goto done;
+                    Py_DECREF(res);
+                    t_gc += now_ms() - tg;
+                    ++n_gc;
+                    continue;
+                }
                 if (m == 0) {
                     Py_BEGIN_ALLOW_THREADS
                     sched_yield();
@@ -1287,11 +1328,11 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
         if (trace)
             fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows, %.0f%% edges, %lld inserted) b=%.1f t=%.1f sweeps=%lld scc=%d passes=%d first=%lld "
-                    "replay=%.1f cpus main %d/%d replay %d/%d spec %lld used %lld\n", t_setup, t_replay,
+                    "replay=%.1f cpus main %d/%d replay %d/%d spec %lld used %lld gc %d in %.1f ms\n", t_setup, t_replay,
                     N ? 100.0 * (double)k_at_replay / (double)N : 100.0,
                     E ? 100.0 * (double)dec_at_replay / (double)E : 100.0, (long long)ins_at_replay, t_built, now_ms() - t0, (long long)n_sweeps,
                     scc_on, scc.passes,
-                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end, (long long)R.n_spec, (long long)R.n_spec_used);
+                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end, (long long)R.n_spec, (long long)R.n_spec_used, n_gc, t_gc);
     }
 done:
     if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */
@@ -1336,6 +1377,7 @@ done:
         for (Py_ssize_t e = 0; e < L_E; ++e) Py_XDECREF(spec[e]);
         PyMem_Free(spec);
     }
+    Py_XDECREF(gc_collect);
     if (trace) fprintf(stderr, "ovl_stream exit: references %.1f ms, dicts made ahead and unused %.1f ms\n", tc1 - tc0,
                        now_ms() - tc1);
     PyMem_Free(rread);

@@ -192,20 +192,24 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
     // and weight cw, so a yield reads no edge record -- the edge array (45 MB at the target point) is read only to
     // find the next live edge after a yield (cv = 0: scan from cq), off the walk's critical path.  "Live" only ever
     // turns false (removal, head explored / settled), so a cached edge whose head is not done is still the next
-    // live one, except the removed edge itself (its tail's cache is dropped at the removal).  Also: the index of
-    // the path edge leaving the node (valid while active), visited (= seen: both happen at the yield that first
-    // reaches it) and on the active path.  A node starts with its row's first edge cached.
+    // live one, except the removed edge itself (its tail's cache is dropped at the removal).  Also the row's end
+    // (so a yield reads no offset either), visited (= seen: both happen at the yield that first reaches it) and on
+    // the active path.  A node starts with its row's first edge cached.  The index of the path edge leaving a node
+    // (valid while it is active, read only when a cycle closes) is kept apart, in tail_pos.  (Box, alternating
+    // builds: row end in the record and tail_pos apart 0.374 -> 0.354 s; 16-byte records with the flags in a byte
+    // array 0.383 -> 0.408 s, not kept; profiles/r05_replay_ab.json.)
     struct Node {
-        int32_t cq, ch;
+        int32_t cq, end, ch;
         WT cw;
-        int32_t tail_pos;
         uint8_t visited, active, cv;
     };
     std::vector<Node> nd((size_t)n_nodes);
+    std::vector<int32_t> tail_pos((size_t)n_nodes, 0);
     for (int32_t v = 0; v < n_nodes; ++v) {
         Node& x = nd[(size_t)v];
         x = Node{};
         x.cq = (int32_t)off[v];
+        x.end = (int32_t)off[v + 1];
         if (off[v] < off[v + 1]) {
             x.ch = head[off[v]];
             x.cw = (WT)weight[off[v]];
@@ -288,7 +292,7 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
             }
             const int32_t cur = stack.back();
             Node& c = N[cur];
-            const int64_t end = off[cur + 1];
+            const int64_t end = c.end;
             if (!c.cv || (c.cq < end && D[c.ch])) {  // next live edge of cur's iterator from the edge records
                 const int64_t q = next_live(c.cq, end);
                 c.cq = (int32_t)q;
@@ -328,13 +332,13 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
             }
             int32_t link = (int32_t)path.size() - 1;
             while (link >= 0 && path[(size_t)link].w > (int64_t)w) link = path[(size_t)link].link;
-            c.tail_pos = (int32_t)path.size();
+            tail_pos[(size_t)cur] = (int32_t)path.size();
             path.push_back({mark, (int64_t)w, (int32_t)q, cur, h, link});
             Node& hn = N[h];
             if (hn.active) {
                 // cycle: the path suffix from the first edge leaving h (the path is simple, so that edge is
                 // tail_pos[h]); remove its weakest edge, the first minimum in cycle order
-                const int32_t i0 = hn.tail_pos;
+                const int32_t i0 = tail_pos[(size_t)h];
                 const PathEdge* pp = path.data();
                 int32_t kmin = (int32_t)path.size() - 1;
                 while (pp[kmin].link >= i0) kmin = pp[kmin].link;
