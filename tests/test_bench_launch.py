@@ -91,3 +91,21 @@ def test_world_size_mismatch_is_an_error():
                        timeout=120, env=_env(WORLD_SIZE="4", RANK="0"))
     assert r.returncode == 2
     assert "WORLD_SIZE" in r.stderr
+
+
+def test_committed_profiles_on_the_line():
+    """The committed profiles bench.py puts on its line (no GPU): every cfg5 band-sweep point's kernel counters
+    (profiles/r05_cfg5_pmc.json) and the per-rank projections of the target list and of cfg4
+    (profiles/r05_shard_steps.json, profiles/r05_cfg4_shard_steps.json) load and are in range."""
+    for band in (4, 8, 16, 32, 64, -1):
+        p = bench.band_pmc(band)
+        assert p is not None, band
+        assert 0.0 < p["valu_isa_frac"] <= 1.2 and 0.0 < p["waves_per_simd"] <= 8.0, p
+        assert p["lds_bank_conflict_frac"] is not None and 0.0 <= p["lds_bank_conflict_frac"] <= 1.0, p
+        assert ("dp_lane" if band < 0 else "band_lane") in p["kernel"] and p["rocprof_kernel_ms"] > 0
+    assert bench.band_pmc(12345) is None
+    for name in ("target", "cfg4"):
+        pr = bench.per_rank_projection(name)
+        assert pr is not None and pr["source"].startswith("profiles/r05_"), name
+        sp = pr["projected_speedup"]
+        assert sp[1] == 1.0 and 1.0 < sp[2] < sp[4] < sp[8] <= 8.0, sp
