@@ -1,4 +1,4 @@
-"""Summarise tools/gpu_r04_profile.sh into profiles/<round>_<config>_{kernel_stats.csv,pmc.json} (a shard run,
+"""Summarise tools/gpu_profile.sh into profiles/<round>_<config>_{kernel_stats.csv,pmc.json} (a shard run,
 SHARD=r/N: workload "<config>/shard<r>of<N>", files <round>_<config>_shard<r>of<N>_*).
 
 One entry per uniform_kernel instantiation (their names differ by the result sink: <W, 0, false, 2> packed chunks
@@ -11,7 +11,7 @@ breakdown: SQ_WAIT_ANY (parked on s_waitcnt: loads, and the stores to host memor
 SQ_WAIT_INST_ANY (issue stalls), SQ_ACTIVE_INST_ANY (issuing), each a fraction of SQ_WAVE_CYCLES.
 ``headline_kernel`` is the bench line's roofline.kernel (the in-step kernel scoring most of the pairs).
 
-    python tools/profile_summary_r04.py gpurun_out/r04prof r04 target [shard_tag]
+    python tools/profile_summary.py gpurun_out/r04prof r04 target [shard_tag]
 """
 import csv
 import glob
@@ -118,7 +118,7 @@ def main():
         cmd += " --shard " + shard.replace("shard", "").replace("of", "/")
     out = {"workload": workload, "headline_kernel": bench["roofline"]["kernel"], "command": cmd,
            "bench_roofline_same_run": bench["roofline"], "kernels": kernels,
-           "source": "tools/gpu_r04_profile.sh, tools/profile_summary_r04.py"}
+           "source": "tools/gpu_profile.sh, tools/profile_summary.py"}
     json.dump(out, open(os.path.join(root, "profiles", f"{stem}_pmc.json"), "w"), indent=1)
     print(json.dumps(out, indent=1)[:4000])
 
