@@ -605,6 +605,8 @@ def sharded_band_sweep(world: int, rank: int, dev, eng, bands, indel: int, steps
             ref = eng.score_candidates(10, -1, indel, band)
             ok = bool(np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]))
         out["pairs"] = st.n_pairs
+        if rank == 0:
+            print(f"bench.py: sharded band sweep, band {band} done", file=sys.stderr, flush=True)
         out["points"].append({"band": band, "kernel": eng.plan(10, -1, indel, band), "ms_per_step": el / steps * 1e3,
                               "pairs_per_s": st.n_pairs * steps / el,
                               **({"matches_single_gpu": ok} if ok is not None else {})})
@@ -1068,7 +1070,14 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
     if shared:
         ident["note"] = ("more ranks than visible GPUs: ranks share devices (flow rehearsal, gloo barriers) -- "
                          "not a scaling number")
+    t_run = time.perf_counter()
+
+    def progress(what):  # (rank 0, stderr: the line on stdout stays the only output there)
+        if rank == 0:
+            print(f"bench.py: {what} done at {time.perf_counter() - t_run:.1f} s", file=sys.stderr, flush=True)
+
     top = sharded_list(name, world, rank, dev, backend, args)
+    progress("sharded list")
     w = top["w"]
     extras = {}
     for item in extra_plan(args, world):
@@ -1082,6 +1091,7 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
         elif item == "single_process_all_gpus":
             extras[item] = single_process_all_gpus(rank, world, shared, w.reads, w.cfg["k"], args.steps, w.eng)
         dist.barrier()
+        progress(item)
     line = multi_line(args, world, ident, top, extras) if rank == 0 else None
     w.close()
     return line
