@@ -116,7 +116,10 @@ struct Knobs {
 constexpr int64_t kLaneMinPairs = 65536;
 // uniform_kernel grid cap, blocks of 256 per CU: ~1 tile per wavefront at the target point, the dispatcher
 // balances the tail (measured -2.3 % against 8 per CU; 16 / 32 / 64: 69.2 / 68.6 / 68.4 us)
-constexpr int64_t kBlocksPerCu = 32;
+#ifndef OVL_BLOCKS_PER_CU
+#define OVL_BLOCKS_PER_CU 32  // (a build macro for A/B builds, not a runtime knob)
+#endif
+constexpr int64_t kBlocksPerCu = OVL_BLOCKS_PER_CU;
 // band knob: two lanes per pair (band_lane2_kernel) from this half-width.  Measured at cfg5 (tools/band_ab.py,
 // profiles/r04_band_lane_ab.json, ms one lane / two lanes): 40: 6.07 / 6.99, 48: 7.13 / 8.04, 56: 8.29 / 9.09,
 // 64: 10.50 / 10.17 -- two lanes only pay where one lane's 129 band cells leave one wavefront per SIMD.  With
