@@ -190,3 +190,32 @@ def test_streamed_removal_duplicated_pairs(monkeypatch):
     assert ts["overlapped"] and not tr["overlapped"] and ts["removed"] == tr["removed"]
     _same_views(Ls, Lr)
     assert nx.is_directed_acyclic_graph(Ls)
+
+
+def test_streamed_build_rejects_a_mismatched_csr():
+    """build_overlap_stream starts the replay on the caller's CSR before it lays out the columns; a CSR that does not
+    belong to the columns' graph (one node too many, or a heads array from a smaller graph) still fails with
+    ValueError once the replay it started has ended, and a correct call afterwards works."""
+    import ctypes
+    from ovlgraph import _lib
+    mod = og._digraph()
+    if mod is None or not hasattr(mod, "build_overlap_stream"):
+        pytest.skip("ovlgraph._digraph is not built")
+    fn = ctypes.cast(_lib.load().ovl_remove_cycles_stream, ctypes.c_void_p).value
+    d, c, a, b, sc, en = _case(31, n_reads=300)
+    E = og.OverlapEdges(d, c, a, b, sc, en)
+    off, heads, w = E.csr()
+    off = np.ascontiguousarray(off, np.int64)
+    heads = np.ascontiguousarray(heads, np.int32)
+    w = np.ascontiguousarray(w, np.int64)
+    args = (E.node_names(), np.ascontiguousarray(E.counts, dtype=np.int32), E.a, E.b, E.score, E.end, E._keep_mask(),
+            og._attr_template(), fn)
+    extra = np.concatenate([off, off[-1:]])  # one node more, with no edges
+    with pytest.raises(ValueError):
+        mod.build_overlap_stream(*args, extra, heads, w)
+    n = int(off[-1]) // 2
+    cut = np.minimum(off, n)  # the first n edges only
+    with pytest.raises(ValueError):
+        mod.build_overlap_stream(*args, cut, np.ascontiguousarray(heads[:n]), np.ascontiguousarray(w[:n]))
+    node, succ, pred, _rem, n_removed = mod.build_overlap_stream(*args, off, heads, w)
+    assert len(node) == len(succ) == len(pred) == E.n_nodes() and n_removed >= 0

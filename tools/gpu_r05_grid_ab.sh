@@ -7,8 +7,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/${1:-r05grid}
 mkdir -p $OUT
 B=genome-assembly-using-overlap-graphs_amd/build
-for pass in 1 2; do
-  for v in default bpc8 bpc16 bpc64; do
+for pass in ${PASSES:-1 2}; do
+  for v in ${VARIANTS:-default bpc8 bpc16 bpc64}; do
     if [ $v = default ]; then LIB=$B/libovl.so; else LIB=$B/ablate_$v/libovl.so; fi
     OVL_LIB_PATH=$LIB SHARD_AB_NS=1,8 timeout -k 10 200 python3 -u tools/shard_step_ab.py 3 30 > $OUT/${v}_$pass.json \
       2> $OUT/${v}_$pass.err || { echo "$v failed"; tail -20 $OUT/${v}_$pass.err; exit 1; }
