@@ -239,7 +239,6 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
         int32_t link;
     };
     std::vector<PathEdge> path;
-    std::vector<int32_t> stack;  // edge_dfs stack: the start node, then the path heads
     std::vector<int32_t> seen_list;
     std::vector<Event> log;
     int64_t nrem = 0;
@@ -272,25 +271,16 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
         log.clear();
         path.clear();
         seen_list.clear();
-        stack.assign(1, s);
-        int32_t root = s;  // find_cycle's path root (the start node; a reset re-roots at the tail)
+        // the edge_dfs stack is implicit: s, then the heads of path[0 .. depth) -- every stack entry but s is the
+        // head of a path edge, in order, and find_cycle's path also keeps, until the next yield pops them, the
+        // edges whose heads the stack has popped (path[depth ..)).  So s is the root of every path.
+        int32_t depth = 0;
         // the start node's first visit is never rewound (every rewind target is a later yield's checkpoint)
         N[s].visited = 1;
         N[s].active = 1;
         seen_list.push_back(s);
-        int32_t prev_head = -1;
         for (;;) {
-            if (stack.empty()) {
-                // no cycle reachable from s: everything seen is explored for the later starts
-                for (int32_t v : seen_list)
-                    if (!done[v]) {
-                        done[v] = 1;
-                        pub.push(v);
-                    }
-                N[root].active = 0;
-                break;
-            }
-            const int32_t cur = stack.back();
+            const int32_t cur = depth ? path[(size_t)depth - 1].head : s;
             Node& c = N[cur];
             const int64_t end = c.end;
             if (!c.cv || (c.cq < end && D[c.ch])) {  // next live edge of cur's iterator from the edge records
@@ -304,8 +294,18 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
             }
             const int64_t q = c.cq;
             if (q == end) {  // iterator exhausted: pop
-                stack.pop_back();
-                continue;
+                if (depth > 0) {
+                    --depth;
+                    continue;
+                }
+                // s popped: no cycle reachable from it, everything seen is explored for the later starts
+                for (int32_t v : seen_list)
+                    if (!done[v]) {
+                        done[v] = 1;
+                        pub.push(v);
+                    }
+                N[s].active = 0;
+                break;
             }
             // yield edge q = (cur, h)
             const int64_t mark = (int64_t)log.size();
@@ -315,20 +315,10 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
             c.cq = (int32_t)(q + 1);
             c.cv = 0;
             __builtin_prefetch(&E[q + 1]);  // (for cur's next yield, after the walk below h returns to it)
-            stack.push_back(h);
-            if (prev_head >= 0 && cur != prev_head) {
-                // backtracking: pop the path back to the edge whose head is cur (or empty it)
-                while (true) {
-                    if (path.empty()) {  // popped everything: active_nodes = {tail}
-                        N[root].active = 0;
-                        root = cur;
-                        N[root].active = 1;
-                        break;
-                    }
-                    N[path.back().head].active = 0;
-                    path.pop_back();
-                    if (!path.empty() && path.back().head == cur) break;
-                }
+            if ((size_t)depth < path.size()) {
+                // backtracking: pop the path back to the edge whose head is cur (emptied: active_nodes = {s})
+                for (size_t k = (size_t)depth; k < path.size(); ++k) N[path[k].head].active = 0;
+                path.resize((size_t)depth);
             }
             int32_t link = (int32_t)path.size() - 1;
             while (link >= 0 && path[(size_t)link].w > (int64_t)w) link = path[(size_t)link].link;
@@ -369,18 +359,8 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                 N[tail_of_dead].cv = 0;  // (its cached next edge is now the removed one)
                 // heads leaving the path (not the closing edge's: that node is on the surviving path)
                 for (size_t k = (size_t)kmin; k + 1 < path.size(); ++k) N[pp[k].head].active = 0;
-                N[root].active = 1;  // (the root is unchanged since path[kmin] was yielded)
                 path.resize((size_t)kmin);
-                // the edge_dfs stack at that moment: the root (= the start node: only it can be on the
-                // stack without being a path head) and the surviving path heads
-                stack.resize((size_t)kmin + 1);
-                if (kmin == 0) {
-                    // the path root was the yielding node itself: active_nodes = {tail}
-                    N[root].active = 0;
-                    root = tail_of_dead;
-                    N[root].active = 1;
-                }
-                prev_head = kmin > 0 ? path[(size_t)kmin - 1].head : -1;
+                depth = kmin;  // (the stack at that moment: s and the surviving path heads)
                 continue;
             }
             if (!hn.visited) {  // first visit (and 'seen' insertion) of h, undone with this yield
@@ -389,7 +369,7 @@ int replay_t(const int64_t* off, const int32_t* head, const int64_t* weight, int
                 log.back().first = h;
             }
             hn.active = 1;
-            prev_head = h;
+            depth = (int32_t)path.size();
         }
     }
     *n_removed = nrem;
