@@ -942,6 +942,38 @@ static int64_t spec_reap(RowCtx* R, int64_t* re, int64_t n_edges, int64_t budget
     return freed;
 }
 
+/* The dicts the result is made of, ahead of their contents: every node's successor and predecessor dict not made yet
+   (presized to its out- and in-edges, live or not) and the node-ordered top-level dicts (node attributes, succ,
+   pred) holding them -- the rows and predecessor dicts are then filled in place.  Idle work while the replay runs
+   (otherwise the last step after it), and made before the builder's collections of the young generations, which then
+   take these 150 K dicts out of the final one's way.  0, or -1 with an exception set. */
+static int make_tops(PyObject* names, int64_t n, PyObject** rows, PyObject** pin, const int64_t* outdeg,
+                     const int64_t* indeg, PyObject** node, PyObject** succ, PyObject** pred) {
+    PyObject* nd = PyDict_New();
+    PyObject* sd = PyDict_New();
+    PyObject* pd = PyDict_New();
+    if (!nd || !sd || !pd) goto fail;
+    for (Py_ssize_t i = 0; i < (Py_ssize_t)n; ++i) {
+        if (!rows[i] && !(rows[i] = _PyDict_NewPresized(outdeg[i]))) goto fail;
+        if (!pin[i] && !(pin[i] = _PyDict_NewPresized(indeg[i]))) goto fail;
+        PyObject* name = PyList_GET_ITEM(names, i);
+        PyObject* x = PyDict_New();
+        const int bad = !x || PyDict_SetItem(nd, name, x) || PyDict_SetItem(sd, name, rows[i]) ||
+                        PyDict_SetItem(pd, name, pin[i]);
+        Py_XDECREF(x);
+        if (bad) goto fail;
+    }
+    *node = nd;
+    *succ = sd;
+    *pred = pd;
+    return 0;
+fail:
+    Py_XDECREF(nd);
+    Py_XDECREF(sd);
+    Py_XDECREF(pd);
+    return -1;
+}
+
 /* build_overlap_stream(names, counts, a, b, score, end, keep, shared, replay_fn, off, heads, weights)
  *     -> (node, succ, pred, removed, n_removed)
  * remove_cycles_from_graph on a graph that is still columns, with the replay and the dicts overlapped: the replay
@@ -1216,6 +1248,7 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
         int64_t spec_u = 0;     /* spec_advance's next node */
         int64_t reap_e = 0;     /* spec_reap's next edge */
         int n_gc = 0;           /* collections of the young generations run so far (kGcMid) */
+        double t_tops = -1.0;
         double t_gc = 0.0;
         double t_sweep = -1e9;  /* the last sweep's start (ms) */
         for (int64_t v = 0; v < N; ++v)
@@ -1249,10 +1282,12 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                kSweepMs (a sweep calls row_advance on every open row, hundreds of millions of calls over a run when
                repeated back to back); in between, and after a sweep that moved nothing, make attribute dicts ahead */
             if (now_ms() - t_sweep < kSweepMs) {
-                const int64_t m = spec_advance(&R, &spec_u, N, 256);
-                if (m < 0) goto done;
-                if (m == 0 && OVL_SPEC_AHEAD) (void)spec_reap(&R, &reap_e, E, 16384);
-                if (m == 0 && gc_collect && n_gc < kGcMid && R.n_dec >= (int64_t)(kGcAt[n_gc] * (double)E)) {
+                if (!node) {  /* first: every row and predecessor dict and the top-level dicts, once */
+                    if (make_tops(names, N, rows, pin, outdeg, pending, &node, &succ, &pred)) goto done;
+                    if (trace) t_tops = now_ms() - t0;
+                    continue;
+                }
+                if (gc_collect && n_gc < kGcMid && R.n_dec >= (int64_t)(kGcAt[n_gc] * (double)E)) {
                     /* the collector's pass over the dicts built so far, now, beside the replay (see kGcMid) */
                     const double tg = now_ms();
                     PyObject* res = PyObject_CallFunction(gc_collect, "i", 1);
@@ -1262,7 +1297,10 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                     ++n_gc;
                     continue;
                 }
+                const int64_t m = spec_advance(&R, &spec_u, N, 256);
+                if (m < 0) goto done;
                 if (m == 0) {
+                    if (OVL_SPEC_AHEAD) (void)spec_reap(&R, &reap_e, E, 16384);
                     Py_BEGIN_ALLOW_THREADS
                     sched_yield();
                     Py_END_ALLOW_THREADS
@@ -1311,28 +1349,17 @@ static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
                          "%lld predecessor dicts)", job.rc, (long long)k_done, (long long)N, (long long)n_pred);
             goto done;
         }
-        node = PyDict_New();
-        succ = PyDict_New();
-        pred = PyDict_New();
-        if (!node || !succ || !pred) goto done;
-        for (Py_ssize_t i = 0; i < N; ++i) {
-            PyObject* name = PyList_GET_ITEM(names, i);
-            PyObject* x = PyDict_New();
-            const int bad = !x || PyDict_SetItem(node, name, x) || PyDict_SetItem(succ, name, rows[i]) ||
-                            PyDict_SetItem(pred, name, pin[i]);
-            Py_XDECREF(x);
-            if (bad) goto done;
-        }
+        if (!node && make_tops(names, N, rows, pin, outdeg, pending, &node, &succ, &pred)) goto done;
         PyObject* rem = PyBytes_FromStringAndSize((const char*)job.removed, (Py_ssize_t)(8 * job.n_removed));
         if (!rem) goto done;
         out = Py_BuildValue("(OOONL)", node, succ, pred, rem, (long long)job.n_removed);
         if (trace)
             fprintf(stderr, "ovl_stream: s=%.1f r=%.1f (%.0f%% rows, %.0f%% edges, %lld inserted) b=%.1f t=%.1f sweeps=%lld scc=%d passes=%d first=%lld "
-                    "replay=%.1f cpus main %d/%d replay %d/%d spec %lld used %lld gc %d in %.1f ms\n", t_setup, t_replay,
+                    "replay=%.1f cpus main %d/%d replay %d/%d spec %lld used %lld gc %d in %.1f ms tops at %.1f dec %.0f%%\n", t_setup, t_replay,
                     N ? 100.0 * (double)k_at_replay / (double)N : 100.0,
                     E ? 100.0 * (double)dec_at_replay / (double)E : 100.0, (long long)ins_at_replay, t_built, now_ms() - t0, (long long)n_sweeps,
                     scc_on, scc.passes,
-                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end, (long long)R.n_spec, (long long)R.n_spec_used, n_gc, t_gc);
+                    (long long)n_from_scc, job.ms, job.cpu_main, sched_getcpu(), job.cpu_start, job.cpu_end, (long long)R.n_spec, (long long)R.n_spec_used, n_gc, t_gc, t_tops, E ? 100.0 * (double)dec_at_replay / (double)E : 0.0);
     }
 done:
     if (started) {  /* an error while the replay runs: let it finish (it owns no Python objects) */
