@@ -21,7 +21,7 @@ grep '^{"metric"' "$OUT/bench.log" > "$OUT/bench.json"
 python3 -c "
 import json; d = json.load(open('$OUT/bench.json'))
 print('value', d['value'], 'ms/step', d['ms_per_step'], 'frac', d['roofline']['frac'])
-e = d['end_to_end']; print('end_to_end remove_cycles_s', e['remove_cycles_s'], e['remove_cycles_stages_s'])"
+e = d['end_to_end']; print('end_to_end remove_cycles_s', e['remove_cycles_s'], e['remove_cycles_runs_s'], e['remove_cycles_stages_s'])"
 echo "== bench N = 2 rehearsal (two ranks on one GPU)"
 timeout -k 10 600 python3 -u bench.py --gpus 2 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_n2.log" 2>&1 \
   || { echo "bench N=2 failed"; tail -30 "$OUT/bench_n2.log"; exit 1; }
