@@ -85,10 +85,12 @@ struct Knobs {
     // dp_fast_kernel), lane (lane-per-pair forced), fast (dp_fast_kernel), classic (dp_kernel)
     int32_t dp_classic = 0;
     int32_t dp_lane = -1;         // -1 auto by list size, 0 off, 1 forced
-    // OVL_LANE_FORM env, the lane kernels' inner form (tests), a bit mask, default 3: bit 0 scores by the byte
-    // profile (else compare/select), bit 1 takes row symbols from the bit planes (else byte gathers)
+    // OVL_LANE_FORM env, the lane kernels' inner form (tests), a bit mask, default 7: bit 0 scores by the byte
+    // profile (else compare/select), bit 1 takes row symbols from the bit planes (else byte gathers), bit 2 lets
+    // the full DP hold two pairs per lane as packed f16 cells (dp_lane_h2_kernel) where the scoring allows
     int32_t lane_prof = 1;
     int32_t lane_sfx = 1;
+    int32_t lane_h2 = 1;
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
     int32_t pack = 1;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
                                   // form holds; 1 (default) packed as 2 bytes per pair, expanded chunk by chunk
@@ -166,6 +168,7 @@ struct Dev {
     int32_t& dp_lane = k.dp_lane;
     int32_t& lane_prof = k.lane_prof;
     int32_t& lane_sfx = k.lane_sfx;
+    int32_t& lane_h2 = k.lane_h2;
     // resident reads
     int32_t n_reads = -1;
     int32_t lmax = 0;
@@ -652,6 +655,8 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
             if (k.sfx && indel <= 0 && std::max<int64_t>(match, mismatch) >= indel &&
                 step_max <= 15 && g.mcap <= 256)
                 k.ho = 2;
+            k.h2 = k.ho == 2 && c->lane_h2 && ovl_dp_lane_h2_ok(match, mismatch, indel);
+            if (k.h2) k.slots = (int64_t)c->cu_count * 10;  // LDS: 16 KiB per wavefront, 10 per CU
             k.sfx_words = as<uint32_t>(c->sfx);
             k.pfx_words = as<uint32_t>(c->pfx);
             k.srow = c->srow;
@@ -747,6 +752,7 @@ Knobs read_knobs() {
         const int v = atoi(e);
         k.lane_prof = v & 1;
         k.lane_sfx = (v >> 1) & 1;
+        k.lane_h2 = (v >> 2) & 1;
     }
     if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));

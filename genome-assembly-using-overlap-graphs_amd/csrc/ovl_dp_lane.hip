@@ -358,6 +358,251 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
     }
 }
 
+// ----------------------------------------------------------------------------- full DP, two pairs per lane
+//
+// dp_lane_kernel's recurrence (PROF, SFX, HO 2) with a lane holding two pairs -- p and p + 64 of a 128-pair
+// tile -- as the low and high halves of packed f16 cells, so one v_pk_add_f16 and one v_pk_maximum3_f16
+// advance two cells, and one v_perm_b32 makes both cells' scores: byte 1 of the selector picks the row
+// symbol's score for t_p (from the pair's 4-byte row table), byte 3 the other pair's, bytes 0 and 2 select
+// zero -- the diagonal scores' f16 encodings have a zero low byte (the host checks).  1.5 VALU per cell
+// against 2.25.
+//
+// Exactness: f16 holds integers to 2048.  A strip's values are kept relative to a per-pair offset: it starts
+// at row 0's value in column j0, and every 32 rows the previous row's left-column value (the row's minimum:
+// G rises along rows and columns) moves into the offset.  Between two moves a cell lies within 32 row steps
+// of the left column and 32 column steps of the moved value, each step in [0, smax], smax = max(match,
+// mismatch) - 2*indel <= 15 (HO 2's bound), so every value and diagonal sum stays below 65*smax + 128
+// (the host checks < 2048).  Virtual rows keep column 0 at 0 (any value <= row 0's works there).
+//
+// The hand-off column: 4-bit steps of both pairs, a dword per four rows (pair p in bits 0-15, p + 64 in bits
+// 16-31), in LDS ([row / 4][wavefront][lane], 16 KiB per wavefront at 256 rows: two wavefronts per block).
+// A step's f16 value plus 1024 has the step in its low mantissa bits, which is how steps move between f16
+// cells and nibbles in both directions.
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+namespace {
+__device__ __forceinline__ half2_t as_h2(uint32_t v) { return __builtin_bit_cast(half2_t, v); }
+__device__ __forceinline__ uint32_t h2_bits(half2_t v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ half2_t h2_splat(int32_t v) {
+    const _Float16 h = (_Float16)(float)v;
+    return half2_t{h, h};
+}
+__device__ __forceinline__ half2_t hmax3(half2_t a, half2_t b, half2_t c) {
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+}  // namespace
+
+constexpr uint32_t kH2Bias4 = 0x64006400u + (0x64006400u << 4) + (0x64006400u << 8) + (0x64006400u << 12);
+
+template <int OCC>
+__global__ __launch_bounds__(128, OCC) void dp_lane_h2_kernel(const int32_t* __restrict__ len, int32_t n_reads,
+                                                              const uint32_t* __restrict__ sfx,
+                                                              const uint32_t* __restrict__ pfx, int32_t srow,
+                                                              int32_t wsfx, const int32_t* __restrict__ a_idx,
+                                                              const int32_t* __restrict__ b_idx, int64_t n_pairs,
+                                                              int32_t lcap, int32_t match, int32_t mismatch,
+                                                              int32_t indel, int32_t* __restrict__ out_score,
+                                                              int32_t* __restrict__ out_end,
+                                                              uint32_t* __restrict__ err_flag) {
+    constexpr int CW = 32;
+    constexpr int HS = 128;  // hand-off dwords per row quad: [wavefront in block][lane]
+    const int lane = threadIdx.x & 63;
+    extern __shared__ uint32_t lds_hand[];
+    uint32_t* __restrict__ hcol = lds_hand + (threadIdx.x >> 6) * 64 + lane;
+    const int64_t wslot = (int64_t)blockIdx.x * 2 + (threadIdx.x >> 6);
+    const int64_t nslots = (int64_t)gridDim.x * 2;
+    const int64_t ntiles = (n_pairs + 127) >> 7;
+    const int32_t g = indel;
+    // the row tables' bytes: the high byte of the diagonal score's f16 (match / mismatch, in G units)
+    const uint32_t hi_ma = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)(match - 2 * g)) >> 8;
+    const uint32_t hi_mm = (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)(float)(mismatch - 2 * g)) >> 8;
+    const uint32_t tbl_base = hi_mm * 0x01010101u;  // every t mismatches
+    const uint32_t tbl_diff = hi_ma ^ hi_mm;         // byte x -> match
+    const half2_t h1024 = h2_splat(1024);
+    for (int64_t tile = wslot; tile < ntiles; tile += nslots) {
+        int64_t p[2];
+        bool live[2], bad[2];
+        int32_t n[2], m[2], sk[2], best[2], bend[2];
+        const uint32_t* __restrict__ srow_p[2];
+        const uint32_t* __restrict__ tcol_p[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            p[h] = tile * 128 + h * 64 + lane;
+            live[h] = p[h] < n_pairs;
+            int32_t a = live[h] ? a_idx[p[h]] : 0;
+            int32_t b = live[h] ? b_idx[p[h]] : 0;
+            bad[h] = live[h] && (a < 0 || a >= n_reads || b < 0 || b >= n_reads);
+            if (!live[h] || bad[h]) { a = 0; b = 0; }
+            n[h] = (live[h] && !bad[h]) ? len[a] : 0;
+            m[h] = (live[h] && !bad[h]) ? len[b] : 0;
+            if (n[h] > lcap || m[h] > lcap) { bad[h] = true; n[h] = 0; m[h] = 0; }
+            srow_p[h] = sfx + (int64_t)a * srow;
+            tcol_p[h] = pfx + (int64_t)b * srow;  // (left-aligned: word pair q holds columns 32q + 1 .. 32q + 32)
+            best[h] = 0;  // dp[n][0] = 0 is the j = 0 candidate
+            bend[h] = 0;
+        }
+        const int32_t nmax = wave_max(max(n[0], n[1]));
+        const int32_t nmin = wave_min(min(n[0], n[1]));
+        const int32_t mmax = wave_max(max(m[0], m[1]));
+        const int32_t R = (nmax + 31) / 32 * 32;  // row iterations (end-aligned rows)
+        const int32_t mcut = R - nmin;            // iterations in which some pair is virtual
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            sk[h] = R - n[h];
+            srow_p[h] += 2 * (wsfx - R / 32);
+        }
+
+        auto strip = [&](int32_t j0, auto first_tag) {
+            constexpr bool FIRST = decltype(first_tag)::value;
+            // selectors: byte 1 = t code of pair p (row table in src1), byte 3 = 4 + t code of pair p + 64
+            // (columns past m compute unread values: any code will do)
+            uint32_t SEL[CW];
+            {
+                const uint2 w0 = *reinterpret_cast<const uint2*>(tcol_p[0] + 2 * (j0 >> 5));
+                const uint2 w1 = *reinterpret_cast<const uint2*>(tcol_p[1] + 2 * (j0 >> 5));
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    const uint32_t t0 = ((w0.x >> c) & 1u) | (((w0.y >> c) & 1u) << 1);
+                    const uint32_t t1 = ((w1.x >> c) & 1u) | (((w1.y >> c) & 1u) << 1);
+                    SEL[c] = 0x040C000Cu | (t0 << 8) | (t1 << 24);
+                }
+            }
+            half2_t A[CW];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) A[c] = h2_splat(-g * (1 + c));  // row 0, relative to G[0][j0]
+            int32_t offs[2] = {-g * j0, -g * j0};                          // G = cell + offs (per pair)
+            half2_t prevL = h2_splat(0);                                   // G[i-1][j0], relative
+            half2_t lprev = prevL;                                         // the left column's running value
+            half2_t vprev = h2_splat(-g * CW);                             // this strip's last column, row before
+            uint32_t hr = 0, hn = 0;
+            uint32_t S[2][2], Sn[2][2];  // bit planes of the current / next 32 rows, per pair
+            auto fetch_planes = [&](int32_t kb) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(srow_p[h] + 2 * kb);
+                    Sn[h][0] = v.x;
+                    Sn[h][1] = v.y;
+                }
+            };
+            // rows it .. it+3, skewed: step s advances row k at column s - k, so the four rows' cells of a
+            // step are independent (row k reads row k-1's column c one step after it was written, in place)
+            auto body = [&](int32_t it, auto masked_tag) {
+                constexpr bool MASKED = decltype(masked_tag)::value;
+                if ((it & 31) == 0) {
+                    // next 32 rows: rotate the plane words, prefetch the block after; move the previous
+                    // row's left value (its minimum) into the offsets
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        S[h][0] = Sn[h][0];
+                        S[h][1] = Sn[h][1];
+                    }
+                    if (it + 32 < R) fetch_planes((it + 32) >> 5);
+                    const half2_t C = prevL;
+                    offs[0] += (int32_t)(float)C.x;
+                    offs[1] += (int32_t)(float)C.y;
+#pragma unroll
+                    for (int c = 0; c < CW; ++c) A[c] -= C;
+                    prevL -= C;
+                    lprev -= C;
+                    vprev -= C;
+                }
+                if constexpr (!FIRST) {
+                    hr = hn;
+                    if (it + 4 < R) hn = hcol[(int64_t)(it / 4 + 1) * HS];
+                }
+                half2_t d[4], l[4];
+                uint32_t t0[4], t1[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    half2_t step;
+                    if constexpr (FIRST) {
+                        // column 0: -indel per real row, 0 on virtual rows
+                        if constexpr (MASKED) {
+                            const _Float16 s0 = (_Float16)(float)(it + k >= sk[0] ? -g : 0);
+                            const _Float16 s1 = (_Float16)(float)(it + k >= sk[1] ? -g : 0);
+                            step = half2_t{s0, s1};
+                        } else {
+                            step = h2_splat(-g);
+                        }
+                    } else {
+                        step = as_h2(((hr >> (4 * k)) & 0x000F000Fu) | 0x64006400u) - h1024;
+                    }
+                    d[k] = k ? lprev : prevL;  // G[i-1][j0]
+                    lprev += step;
+                    l[k] = lprev;              // G[i][j0]
+                    // the row's tables (byte t = the f16 high byte of s(x, t) - 2*indel; virtual rows: zero)
+                    const uint32_t r = (uint32_t)(it + k) & 31u;
+                    uint32_t tbl[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)S[h][0], r, 1);
+                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)S[h][1], r, 1);
+                        const uint32_t x8 = (m0 & 8u) | (m1 & 16u);  // 8 * the row symbol
+                        tbl[h] = tbl_base ^ (tbl_diff << x8);
+                        if constexpr (MASKED) tbl[h] &= (uint32_t)~((it + k - sk[h]) >> 31);
+                    }
+                    t0[k] = tbl[0];
+                    t1[k] = tbl[1];
+                }
+                prevL = lprev;
+#pragma unroll
+                for (int st = 0; st < CW + 3; ++st) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int c = st - k;
+                        if (c < 0 || c >= CW) continue;
+                        const half2_t s2 = as_h2(__builtin_amdgcn_perm(t1[k], t0[k], SEL[c]));
+                        const half2_t u = A[c];
+                        A[c] = hmax3(d[k] + s2, u, l[k]);
+                        d[k] = u;
+                        l[k] = A[c];
+                    }
+                }
+                // this strip's last column as steps (also after the last strip: never read, no branch)
+                uint32_t hw = h2_bits((l[0] - vprev) + h1024);
+                hw += h2_bits((l[1] - l[0]) + h1024) << 4;
+                hw += h2_bits((l[2] - l[1]) + h1024) << 8;
+                hw += h2_bits((l[3] - l[2]) + h1024) << 12;
+                vprev = l[3];
+                hcol[(int64_t)(it / 4) * HS] = hw - kH2Bias4;
+            };
+            fetch_planes(0);
+            if constexpr (!FIRST) hn = hcol[0];
+            int32_t it = 0;
+            for (; it < mcut; it += 4) body(it, std::true_type{});
+            for (; it < R; it += 4) body(it, std::false_type{});
+            // A holds row n of both pairs: the strip's part of the last-row scan (strict '>', j ascending)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int32_t base = offs[h] + g * (n[h] + j0 + 1);  // dp = G + indel * (n + j)
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    const int32_t v = (int32_t)(float)(h ? A[c].y : A[c].x) + base + g * c;
+                    const bool better = (j0 + 1 + c <= m[h]) && v > best[h];
+                    best[h] = better ? v : best[h];
+                    bend[h] = better ? j0 + 1 + c : bend[h];
+                }
+            }
+        };
+        if (mmax > 0) strip(0, std::true_type{});
+        // the next strip reads this strip's hand-off column (same lane, program order)
+        for (int32_t j0 = CW; j0 < mmax; j0 += CW) strip(j0, std::false_type{});
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (live[h]) {
+                if (bad[h]) {
+                    ovl_flag_error(err_flag);
+                    out_score[p[h]] = -1;
+                    out_end[p[h]] = -1;
+                } else {
+                    out_score[p[h]] = best[h];
+                    out_end[p[h]] = bend[h];
+                }
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------------------- band knob, lane per pair
 //
 // The build's seed-and-extend band (oracle_overlap_banded; not a reference mode): cells with
@@ -789,6 +1034,10 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
 
 using ovl::dp_lane_kernel;
 
+#ifndef OVL_H2_OCC
+#define OVL_H2_OCC 3
+#endif
+
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap) { return ((lcap + 31) & ~31) + 4; }
 
 // waves per SIMD the strip width is compiled for: 32 columns at 4 (64 columns spill even at 3 waves per SIMD:
@@ -798,8 +1047,43 @@ extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw) { return cw == 32 ? 4 
 // the LDS hand-off (HO 2): rows rounded to 32, 4 bits per row, a dword per 8 rows, per wavefront of the block
 extern "C" int32_t ovl_dp_lane_lds_bytes(int32_t lcap) { return ((lcap + 31) & ~31) / 8 * 4 * 64 * 4; }
 
+// dp_lane_h2_kernel: a diagonal score's f16 encoding ends in a zero byte when its odd part is <= 7 (at most three
+// significant bits); the relative values stay below 65 * 15 + 128 < 2048 under HO 2's step bound
+static bool h2_byte_score(int64_t v) {
+    if (v == 0) return true;
+    uint64_t u = (uint64_t)(v < 0 ? -v : v);
+    while (!(u & 1)) u >>= 1;
+    return u <= 7 && (v < 0 ? -v : v) <= 2048;
+}
+
+extern "C" int32_t ovl_dp_lane_h2_ok(int64_t match, int64_t mismatch, int64_t indel) {
+    return indel <= 0 && h2_byte_score(match - 2 * indel) && h2_byte_score(mismatch - 2 * indel) &&
+                   std::max(match, mismatch) - 2 * indel <= 15 ? 1 : 0;
+}
+
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* k, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
+    if (k->h2) {
+        const int32_t lcap = g->mcap;
+        if (!k->sfx || !k->prof || k->ho != 2 || !k->sfx_words || !k->pfx_words || k->wsfx * 32 < lcap ||
+            lcap > ovl::kLaneLdsMaxLen ||
+            !ovl_dp_lane_h2_ok(g->match, g->mismatch, g->indel))
+            return hipErrorInvalidValue;
+        // a 128-pair tile per wavefront, two per block: the dispatcher places blocks as LDS and registers free up
+        const int64_t tiles = (g->n_pairs + 127) / 128;
+#ifdef OVL_H2_PERSIST  // A/B: k->slots resident wavefronts looping over the tiles
+        int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 1) / 2;
+#else
+        int64_t blocks = (tiles + 1) / 2;
+#endif
+        if (blocks < 1) blocks = 1;
+        const size_t shmem = (size_t)((lcap + 31) & ~31) / 4 * 128 * 4;
+        ovl::dp_lane_h2_kernel<OVL_H2_OCC><<<(unsigned)blocks, 128, shmem, stream>>>(
+            g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx, g->n_pairs,
+            lcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,
+            g->err_flag);
+        return hipGetLastError();
+    }
     const int64_t tiles = (g->n_pairs + 63) / 64;
     int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 3) / 4;
     if (blocks < 1) blocks = 1;

@@ -120,10 +120,13 @@ struct OvlLaneArgs {
     uint32_t* colbuf;
     int64_t slots;              // resident wavefront slots (one hand-off column each)
     int32_t split;              // band knob: two lanes per pair (band_lane2_kernel) instead of one
+    int32_t h2;                 // full DP (prof, sfx, ho 2): two pairs per lane as packed f16 cells
+                                // (dp_lane_h2_kernel; the diagonal scores' f16 encodings end in a zero byte)
 };
 extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);
 extern "C" int32_t ovl_dp_lane_lds_bytes(int32_t lcap);
+extern "C" int32_t ovl_dp_lane_h2_ok(int64_t match, int64_t mismatch, int64_t indel);
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
 // band knob, a lane per pair (ovl_dp_lane.hip): ovl_band_lane_ok(band), <= 4 symbols, scores in int8;
 // uses lane->slots, and lane->sfx (row symbols and t codes from the bit planes) with sfx/pfx_words

@@ -54,12 +54,16 @@ def mixed_set(request):
 # so the 13 scorings below reach every form
 VARIANTS = {f"prof{pr}-sfx{sx}": {"OVL_LANE_FORM": str(int(pr) + 2 * int(sx))}
             for pr in ("0", "1") for sx in ("0", "1") if pr == "1" or sx == "0"}
+# the default form: with the LDS hand-off, two pairs per lane as packed f16 cells (dp_lane_h2_kernel) when both
+# diagonal scores' f16 encodings end in a zero byte -- (10, -1, -2), (1, -1, -1), (3, 2, -1), (-1, -2, -1),
+# (2, -1, 0), (2, -3, -5), (8, -8, -3) and (12, -4, -1) below
+VARIANTS["prof1-sfx1-h2"] = {"OVL_LANE_FORM": "7"}
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("params", [(10, -1, -2), (1, -1, -1), (2, -3, -5), (10, -1, -30), (5, -4, -8), (3, 2, -1),
                                     (-1, -2, -1), (0, 0, -1), (100, -90, -60), (1000, -1, -3), (2, -1, 0),
-                                    (2, -1, 1), (-3, -5, 2)])
+                                    (2, -1, 1), (-3, -5, 2), (8, -8, -3), (12, -4, -1)])
 def test_lane_vs_oracle_mixed_lengths(oracle_mod, mixed_set, params, variant):
     """(100, -90, -60) and (1000, -1, -3) leave the int8 profile and the int16 column, and a positive
     indel leaves the zero-profile virtual rows: those fall back to compare/select, masked virtual rows
@@ -90,6 +94,30 @@ def test_lane_uniform_reads_with_truncated_tail(oracle_mod, variant):
         sc, en = eng.score(a, b, 10, -1, -2)
     np.testing.assert_array_equal(sc, rs)
     np.testing.assert_array_equal(en, re_)
+
+
+@pytest.mark.parametrize("params", [(10, -1, -2), (12, -4, -1), (8, -8, -3)])
+def test_lane_h2_vs_int32_at_scale(oracle_mod, params):
+    """BASELINE configs[4]'s shape (l = 250, p = 0.05), >= 65,536 pairs: the packed-f16 two-pairs-per-lane
+    kernel (default) equals the int32 lane kernel (OVL_LANE_FORM=3) on every pair, and the oracle on a
+    strided sample -- long strips through the 32-row offset moves at the largest steps the form takes."""
+    from ovlgraph.candidates import dedup_reads, enumerate_candidates
+    from ovlgraph.reads import read_genome_from_fasta, simulate_reads
+    reads, _ = dedup_reads(simulate_reads(read_genome_from_fasta(), 250, 8000, 0.05, seed=11))
+    a, b = enumerate_candidates(reads, 5)
+    assert a.shape[0] >= 65536
+    with _engine_env({}) as eng:
+        eng.set_reads(reads)
+        sc, en = eng.score(a, b, *params)
+    with _engine_env({"OVL_LANE_FORM": "3"}) as eng:
+        eng.set_reads(reads)
+        s3, e3 = eng.score(a, b, *params)
+    np.testing.assert_array_equal(sc, s3)
+    np.testing.assert_array_equal(en, e3)
+    idx = np.arange(0, a.shape[0], 97)
+    rs, re_ = oracle_mod.batch_dp(reads, a[idx], b[idx], *params)
+    np.testing.assert_array_equal(sc[idx], rs)
+    np.testing.assert_array_equal(en[idx], re_)
 
 
 def test_lane_wide_alphabet_vs_oracle(oracle_mod):

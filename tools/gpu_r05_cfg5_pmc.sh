@@ -10,7 +10,7 @@ OUT="$GRAFT_REPO_ROOT/gpurun_out/${1:-r05cfg5}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B="$GRAFT_REPO_ROOT/bench.py"
-KRE="dp_lane_kernel|band_lane"
+KRE="dp_lane|band_lane"
 for BAND in ${BANDS:--1 64 32 16 8 4}; do
   ARGS="--config cfg5 --band-sweep=$BAND --sweep-steps 3 --steps 3 --warmup 1 --no-cpu-baseline --no-extra"
   D="$OUT/b$BAND"
