@@ -1085,7 +1085,11 @@ extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* 
         return hipGetLastError();
     }
     const int64_t tiles = (g->n_pairs + 63) / 64;
+#ifdef OVL_LANE_GRID_ALL  // (the LDS hand-off only: the HBM hand-off columns are per resident slot)
+    int64_t blocks = k->ho == 2 ? (tiles + 3) / 4 : (std::min<int64_t>(k->slots, tiles) + 3) / 4;
+#else
     int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 3) / 4;
+#endif
     if (blocks < 1) blocks = 1;
     const int32_t lcap = g->mcap;
     const int32_t rcap = ovl_dp_lane_rcap(lcap);
@@ -1125,6 +1129,9 @@ hipError_t launch_band_lane_w(const OvlDpArgs* g, const OvlLaneArgs* k, int64_t 
         const int64_t tiles = (g->n_pairs + 63) / 64;
         blocks = std::max<int64_t>(1, (std::min<int64_t>(k->slots / 6 * 8, tiles) + 3) / 4);
     }
+#ifdef OVL_LANE_GRID_ALL
+    blocks = std::max<int64_t>(1, ((g->n_pairs + 63) / 64 + 3) / 4);
+#endif
     ovl::band_lane_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
         g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx,
         g->n_pairs, g->mcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,
@@ -1139,7 +1146,11 @@ hipError_t launch_band_lane2_w(const OvlDpArgs* g, const OvlLaneArgs* k, hipStre
     constexpr int H = W + 1;
     constexpr int OCC = H <= 17 ? 6 : (H <= 33 ? 4 : 3);
     const int64_t tiles = (g->n_pairs + 31) / 32;
+#ifdef OVL_LANE_GRID_ALL  // A/B: a tile per wavefront, the dispatcher places blocks as they free up
+    int64_t blocks = (tiles + 3) / 4;
+#else
     int64_t blocks = (std::min<int64_t>(k->slots / 6 * OCC, tiles) + 3) / 4;
+#endif
     if (blocks < 1) blocks = 1;
     ovl::band_lane2_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
         g->codes, g->off, g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx,

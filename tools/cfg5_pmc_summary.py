@@ -1,7 +1,7 @@
 """Summarise tools/gpu_r05_cfg5_pmc.sh into profiles/r05_cfg5_pmc.json (BASELINE configs[4], the kernel of every
 point of the cfg5 band sweep).
 
-    python tools/cfg5_pmc_summary.py gpurun_out/r05cfg5
+    python tools/cfg5_pmc_summary.py gpurun_out/r05cfg5 [gpurun_out/<later run> ...]   (a later run's bands win)
 
 Per kernel (averaged per launch, each counter from its own pass):
   waves_per_simd = 4 * SQ_WAVE_CYCLES / (duration * shader clock * 1024 SIMDs)  (SQ_WAVE_CYCLES counts quad-cycles);
@@ -78,16 +78,18 @@ def kernel_entry(cs, ds):
 
 
 def main():
-    run = sys.argv[1]
+    runs = sys.argv[1:]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = {"workload": "cfg5 (BASELINE configs[4]) band sweep at indel -2, the bench's points (-1 = full DP)",
-           "command": "bash tools/gpu_r05_cfg5_pmc.sh r05cfg5; python tools/cfg5_pmc_summary.py gpurun_out/r05cfg5",
+           "command": "bash tools/gpu_r05_cfg5_pmc.sh <tag> (BANDS=...); python tools/cfg5_pmc_summary.py " + " ".join(runs),
            "definitions": __doc__.strip().split("\n\n")[2], "bands": {}}
-    dirs = {int(os.path.basename(d)[1:]): d for d in glob.glob(os.path.join(run, "b*"))}
+    dirs = {}
+    for run in runs:
+        dirs.update({int(os.path.basename(d)[1:]): d for d in glob.glob(os.path.join(run, "b*"))})
     for b in sorted(dirs, key=lambda x: (x < 0, x)):  # (widths ascending, then the full DP)
         d, band = dirs[b], str(b)
         vals, durs = passes(d)
-        want = "dp_lane_kernel" if band == "-1" else "band_lane"
+        want = "dp_lane" if band == "-1" else "band_lane"
         ks = {k: kernel_entry(vals[k], durs[k]) for k in vals if want in k}
         stats = glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True)
         trace = {}
@@ -102,7 +104,7 @@ def main():
         pt = None
         if line and line.get("band_sweep"):
             pt = line["band_sweep"]["points"][0]
-        out["bands"][band] = {"kernels": ks, "bench_point_same_run": pt}
+        out["bands"][band] = {"kernels": ks, "bench_point_same_run": pt, "run": os.path.basename(os.path.dirname(d))}
     path = os.path.join(root, "profiles", "r05_cfg5_pmc.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1)[:6000])
