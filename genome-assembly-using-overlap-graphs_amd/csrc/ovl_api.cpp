@@ -641,8 +641,6 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
             OvlLaneArgs k{};
             k.cw = 32;
             k.slots = (int64_t)c->cu_count * 4 * ovl_dp_lane_waves_per_simd(k.cw);
-            const size_t col_bytes = (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t);
-            HIPCHK(c, scratch_acquire(c, s, {{&c->lane_col, col_bytes}}));
             const int64_t L = std::max<int32_t>(c->lmax, 1);
             const int64_t M = std::max(std::max(iabs64(match), iabs64(mismatch)), iabs64(indel));
             const int64_t sma = (int64_t)match - 2 * indel, smm = (int64_t)mismatch - 2 * indel;
@@ -656,7 +654,11 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                 step_max <= 15 && g.mcap <= 256)
                 k.ho = 2;
             k.h2 = k.ho == 2 && c->lane_h2 && ovl_dp_lane_h2_ok(match, mismatch, indel);
-            if (k.h2) k.slots = (int64_t)c->cu_count * 10;  // LDS: 16 KiB per wavefront, 10 per CU
+            // hand-off columns in HBM: one per resident slot (HO 0 / 1), per tile for the h2 form's HBM variant
+            const size_t col_bytes =
+                k.h2 ? (size_t)ovl_dp_lane_h2_col_bytes(n_pairs, g.mcap)
+                     : (k.ho == 2 ? 0 : (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t));
+            HIPCHK(c, scratch_acquire(c, s, {{&c->lane_col, col_bytes}}));
             k.sfx_words = as<uint32_t>(c->sfx);
             k.pfx_words = as<uint32_t>(c->pfx);
             k.srow = c->srow;

@@ -375,9 +375,10 @@ __global__ __launch_bounds__(256, OCC) void dp_lane_kernel(const uint8_t* __rest
 // (the host checks < 2048).  Virtual rows keep column 0 at 0 (any value <= row 0's works there).
 //
 // The hand-off column: 4-bit steps of both pairs, a dword per four rows (pair p in bits 0-15, p + 64 in bits
-// 16-31), in LDS ([row / 4][wavefront][lane], 16 KiB per wavefront at 256 rows: two wavefronts per block).
-// A step's f16 value plus 1024 has the step in its low mantissa bits, which is how steps move between f16
-// cells and nibbles in both directions.
+// 16-31), in HBM per tile ([tile][row / 4][lane], read two quads ahead; the next strip reads it soon after, from
+// the caches).  In LDS (the OVL_H2_LDS build) its 16 KiB per wavefront capped residency at 2.5 wavefronts per
+// SIMD: 13.0 ms against 11.1 for cfg5's full DP.  A step's f16 value plus 1024 has the step in its low mantissa
+// bits, which is how steps move between f16 cells and nibbles in both directions.
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 namespace {
@@ -403,12 +404,19 @@ __global__ __launch_bounds__(128, OCC) void dp_lane_h2_kernel(const int32_t* __r
                                                               int32_t lcap, int32_t match, int32_t mismatch,
                                                               int32_t indel, int32_t* __restrict__ out_score,
                                                               int32_t* __restrict__ out_end,
-                                                              uint32_t* __restrict__ err_flag) {
+                                                              uint32_t* __restrict__ err_flag,
+                                                              uint32_t* __restrict__ colbuf, int32_t hq) {
     constexpr int CW = 32;
-    constexpr int HS = 128;  // hand-off dwords per row quad: [wavefront in block][lane]
     const int lane = threadIdx.x & 63;
+#ifndef OVL_H2_LDS  // the hand-off column per tile in HBM ([tile][row quad][lane], hq quads); A/B: LDS
+    constexpr int HS = 64;
+#else
+    constexpr int HS = 128;  // hand-off dwords per row quad: [wavefront in block][lane]
     extern __shared__ uint32_t lds_hand[];
     uint32_t* __restrict__ hcol = lds_hand + (threadIdx.x >> 6) * 64 + lane;
+    (void)colbuf;
+    (void)hq;
+#endif
     const int64_t wslot = (int64_t)blockIdx.x * 2 + (threadIdx.x >> 6);
     const int64_t nslots = (int64_t)gridDim.x * 2;
     const int64_t ntiles = (n_pairs + 127) >> 7;
@@ -420,6 +428,9 @@ __global__ __launch_bounds__(128, OCC) void dp_lane_h2_kernel(const int32_t* __r
     const uint32_t tbl_diff = hi_ma ^ hi_mm;         // byte x -> match
     const half2_t h1024 = h2_splat(1024);
     for (int64_t tile = wslot; tile < ntiles; tile += nslots) {
+#ifndef OVL_H2_LDS
+        uint32_t* __restrict__ hcol = colbuf + tile * (int64_t)hq * 64 + lane;
+#endif
         int64_t p[2];
         bool live[2], bad[2];
         int32_t n[2], m[2], sk[2], best[2], bend[2];
@@ -474,7 +485,7 @@ __global__ __launch_bounds__(128, OCC) void dp_lane_h2_kernel(const int32_t* __r
             half2_t prevL = h2_splat(0);                                   // G[i-1][j0], relative
             half2_t lprev = prevL;                                         // the left column's running value
             half2_t vprev = h2_splat(-g * CW);                             // this strip's last column, row before
-            uint32_t hr = 0, hn = 0;
+            uint32_t hr = 0, hn = 0, hn2 = 0;
             uint32_t S[2][2], Sn[2][2];  // bit planes of the current / next 32 rows, per pair
             auto fetch_planes = [&](int32_t kb) {
 #pragma unroll
@@ -507,8 +518,14 @@ __global__ __launch_bounds__(128, OCC) void dp_lane_h2_kernel(const int32_t* __r
                     vprev -= C;
                 }
                 if constexpr (!FIRST) {
+#ifndef OVL_H2_LDS  // two quads ahead
+                    hr = hn;
+                    hn = hn2;
+                    if (it + 8 < R) hn2 = hcol[(int64_t)(it / 4 + 2) * HS];
+#else
                     hr = hn;
                     if (it + 4 < R) hn = hcol[(int64_t)(it / 4 + 1) * HS];
+#endif
                 }
                 half2_t d[4], l[4];
                 uint32_t t0[4], t1[4];
@@ -567,7 +584,10 @@ __global__ __launch_bounds__(128, OCC) void dp_lane_h2_kernel(const int32_t* __r
                 hcol[(int64_t)(it / 4) * HS] = hw - kH2Bias4;
             };
             fetch_planes(0);
-            if constexpr (!FIRST) hn = hcol[0];
+            if constexpr (!FIRST) {
+                hn = hcol[0];
+                hn2 = hcol[HS];  // (R >= 32: quad 1 exists)
+            }
             int32_t it = 0;
             for (; it < mcut; it += 4) body(it, std::true_type{});
             for (; it < R; it += 4) body(it, std::false_type{});
@@ -1061,6 +1081,17 @@ extern "C" int32_t ovl_dp_lane_h2_ok(int64_t match, int64_t mismatch, int64_t in
                    std::max(match, mismatch) - 2 * indel <= 15 ? 1 : 0;
 }
 
+// hand-off bytes dp_lane_h2_kernel needs in HBM (0: it hands off through LDS)
+extern "C" int64_t ovl_dp_lane_h2_col_bytes(int64_t n_pairs, int32_t lcap) {
+#ifndef OVL_H2_LDS
+    return (n_pairs + 127) / 128 * (int64_t)(((lcap + 31) & ~31) / 4) * 64 * 4;
+#else
+    (void)n_pairs;
+    (void)lcap;
+    return 0;
+#endif
+}
+
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* k, hipStream_t stream) {
     if (g->n_pairs <= 0) return hipSuccess;
     if (k->h2) {
@@ -1069,23 +1100,29 @@ extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* g, const OvlLaneArgs* 
             lcap > ovl::kLaneLdsMaxLen ||
             !ovl_dp_lane_h2_ok(g->match, g->mismatch, g->indel))
             return hipErrorInvalidValue;
-        // a 128-pair tile per wavefront, two per block: the dispatcher places blocks as LDS and registers free up
+        // a 128-pair tile per wavefront, two per block, all launched: the dispatcher places blocks as they free up
+        // (resident slots looping over the tiles: 18.5 ms against 13.0, cfg5's full DP with the LDS hand-off)
         const int64_t tiles = (g->n_pairs + 127) / 128;
-#ifdef OVL_H2_PERSIST  // A/B: k->slots resident wavefronts looping over the tiles
+#ifdef OVL_LANE_GRID_SLOTS  // A/B: k->slots resident wavefronts looping over the tiles
         int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 1) / 2;
 #else
         int64_t blocks = (tiles + 1) / 2;
 #endif
         if (blocks < 1) blocks = 1;
+#ifndef OVL_H2_LDS
+        const size_t shmem = 0;
+        if (!k->colbuf) return hipErrorInvalidValue;
+#else
         const size_t shmem = (size_t)((lcap + 31) & ~31) / 4 * 128 * 4;
+#endif
         ovl::dp_lane_h2_kernel<OVL_H2_OCC><<<(unsigned)blocks, 128, shmem, stream>>>(
             g->len, g->n_reads, k->sfx_words, k->pfx_words, k->srow, k->wsfx, g->a_idx, g->b_idx, g->n_pairs,
             lcap, (int32_t)g->match, (int32_t)g->mismatch, (int32_t)g->indel, g->out_score, g->out_end,
-            g->err_flag);
+            g->err_flag, k->colbuf, ((lcap + 31) & ~31) / 4);
         return hipGetLastError();
     }
     const int64_t tiles = (g->n_pairs + 63) / 64;
-#ifdef OVL_LANE_GRID_ALL  // (the LDS hand-off only: the HBM hand-off columns are per resident slot)
+#ifndef OVL_LANE_GRID_SLOTS  // (the LDS hand-off only: the HBM hand-off columns are per resident slot)
     int64_t blocks = k->ho == 2 ? (tiles + 3) / 4 : (std::min<int64_t>(k->slots, tiles) + 3) / 4;
 #else
     int64_t blocks = (std::min<int64_t>(k->slots, tiles) + 3) / 4;
@@ -1129,7 +1166,7 @@ hipError_t launch_band_lane_w(const OvlDpArgs* g, const OvlLaneArgs* k, int64_t 
         const int64_t tiles = (g->n_pairs + 63) / 64;
         blocks = std::max<int64_t>(1, (std::min<int64_t>(k->slots / 6 * 8, tiles) + 3) / 4);
     }
-#ifdef OVL_LANE_GRID_ALL
+#ifndef OVL_LANE_GRID_SLOTS
     blocks = std::max<int64_t>(1, ((g->n_pairs + 63) / 64 + 3) / 4);
 #endif
     ovl::band_lane_kernel<NB, OCC, PL><<<(unsigned)blocks, 256, 0, stream>>>(
@@ -1146,7 +1183,7 @@ hipError_t launch_band_lane2_w(const OvlDpArgs* g, const OvlLaneArgs* k, hipStre
     constexpr int H = W + 1;
     constexpr int OCC = H <= 17 ? 6 : (H <= 33 ? 4 : 3);
     const int64_t tiles = (g->n_pairs + 31) / 32;
-#ifdef OVL_LANE_GRID_ALL  // A/B: a tile per wavefront, the dispatcher places blocks as they free up
+#ifndef OVL_LANE_GRID_SLOTS  // a tile per wavefront, the dispatcher places blocks as they free up
     int64_t blocks = (tiles + 3) / 4;
 #else
     int64_t blocks = (std::min<int64_t>(k->slots / 6 * OCC, tiles) + 3) / 4;

@@ -127,6 +127,7 @@ extern "C" int32_t ovl_dp_lane_rcap(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_waves_per_simd(int32_t cw);
 extern "C" int32_t ovl_dp_lane_lds_bytes(int32_t lcap);
 extern "C" int32_t ovl_dp_lane_h2_ok(int64_t match, int64_t mismatch, int64_t indel);
+extern "C" int64_t ovl_dp_lane_h2_col_bytes(int64_t n_pairs, int32_t lcap);
 extern "C" hipError_t ovl_launch_dp_lane(const OvlDpArgs* args, const OvlLaneArgs* lane, hipStream_t stream);
 // band knob, a lane per pair (ovl_dp_lane.hip): ovl_band_lane_ok(band), <= 4 symbols, scores in int8;
 // uses lane->slots, and lane->sfx (row symbols and t codes from the bit planes) with sfx/pfx_words

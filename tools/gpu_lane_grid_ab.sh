@@ -17,3 +17,20 @@ for l in open('$O/$f.log'):
     if l.startswith('{\"metric\"'):
         d=json.loads(l); print('$f', [(p['band'], p.get('kernel'), round(p['kernel_ms'],3)) for p in d['band_sweep']['points']])"; done
 echo ok
+# the h2 kernel's hand-off in HBM (build/ablate_h2hbm, -DOVL_H2_HBM): its lane tests, then cfg5's full DP against the default
+V2=genome-assembly-using-overlap-graphs_amd/build/ablate_h2hbm/libovl.so
+if [ -f $V2 ]; then
+  OVL_LIB_PATH=$V2 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dp_lane.py -x -q -k "h2" --timeout 200 --timeout-method thread -p no:cacheprovider > $O/hbm_tests.log 2>&1 || { tail -20 $O/hbm_tests.log; exit 1; }
+  tail -1 $O/hbm_tests.log
+  A2="--config cfg5 --band-sweep=-1 --sweep-steps 5 --steps 3 --warmup 1 --no-cpu-baseline --no-extra"
+  for pass in 1 2; do
+    timeout -k 10 300 python3 bench.py $A2 > $O/h2lds$pass.log 2>&1 || { tail -20 $O/h2lds$pass.log; exit 1; }
+    OVL_LIB_PATH=$V2 timeout -k 10 300 python3 bench.py $A2 > $O/h2hbm$pass.log 2>&1 || { tail -20 $O/h2hbm$pass.log; exit 1; }
+  done
+  for f in h2lds1 h2hbm1 h2lds2 h2hbm2; do python3 -c "
+import json
+for l in open('$O/$f.log'):
+    if l.startswith('{\"metric\"'):
+        d=json.loads(l); print('$f', [(p['band'], p.get('kernel'), round(p['kernel_ms'],3)) for p in d['band_sweep']['points']])"; done
+fi
+echo done2
