@@ -799,7 +799,18 @@ __global__ __launch_bounds__(256, OCC) void band_lane_kernel(const uint8_t* __re
         else fetch4(0);
         int32_t it = 0;
         for (; it < mcut; it += 4) body(it, std::true_type{});
+#ifndef OVL_BAND_UNROLL1  // eight rows per trip, as in band_lane2_kernel
+        if (it < R && ((R - it) & 7)) {
+            body(it, std::false_type{});
+            it += 4;
+        }
+        for (; it < R; it += 8) {
+            body(it, std::false_type{});
+            body(it + 4, std::false_type{});
+        }
+#else
         for (; it < R; it += 4) body(it, std::false_type{});
+#endif
         // row n: in-band cells with 0 <= j <= m, largest value, first j (the oracle's scan)
         int32_t best = INT32_MIN, bend = -1;
 #pragma unroll
@@ -1030,7 +1041,20 @@ __global__ __launch_bounds__(256, OCC) void band_lane2_kernel(const uint8_t* __r
         else fetch4(0);
         int32_t t = 0;
         for (; t < mcut + 1 && t < R; t += 4) body(t, std::true_type{});
+#ifndef OVL_BAND_UNROLL1
+        // eight rows per trip: the window's one-word shift per four rows lands in place in the first body and
+        // costs a register move per window word only at the trip's end (half the moves)
+        if (t < R && ((R - t) & 7)) {
+            body(t, std::false_type{});
+            t += 4;
+        }
+        for (; t < R; t += 8) {
+            body(t, std::false_type{});
+            body(t + 4, std::false_type{});
+        }
+#else
         for (; t < R; t += 4) body(t, std::false_type{});
+#endif
         if (!h) scan();  // lane 0 has finished iteration R - 1
         // step R: lane 1's last iteration (R - 1, byte 3 of the last group); lane 0's cells are no longer read
         step(R, xs8_prev >> 24, ts_prev >> 24, std::true_type{});
