@@ -1,6 +1,7 @@
 #!/bin/bash
-# A/B of the band kernels' body loop: eight rows per trip (default) against four (build/ablate_unroll1,
-# -DOVL_BAND_UNROLL1), cfg5 bands 64 / 32 / 8 / 4, two passes each; the banded GPU tests first.
+# A/B of the band kernels' body loop: eight rows per trip (default) against four (make -C
+# genome-assembly-using-overlap-graphs_amd/csrc variant_lane V=unroll1 DEFS=-DOVL_BAND_UNROLL1), cfg5 bands
+# 64 / 32 / 8 / 4, two passes each; the banded GPU tests first.
 # usage: bash tools/gpu_band_unroll_ab.sh [tag]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1

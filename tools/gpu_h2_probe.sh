@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 probe of dp_lane_h2_kernel (two pairs per lane, packed f16): the lane tests, then cfg5's full DP point
-# under rocprofv3 (default build), then the int32 lane kernel (OVL_LANE_FORM=3) and the default again.
+# under rocprofv3 (default build), then the int32 lane kernel (OVL_LANE_FORM=3) and the default again; with
+# build/ablate_persist (make variant_lane V=persist DEFS=-DOVL_LANE_GRID_SLOTS) the resident-slots grid too.
 # usage: bash tools/gpu_h2_probe.sh [tag]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1

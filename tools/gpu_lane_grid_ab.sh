@@ -1,6 +1,8 @@
 #!/bin/bash
-# A/B of the lane kernels' grid: resident slots looping over the tiles (default build) against a tile per wavefront
-# (build/ablate_gridall, -DOVL_LANE_GRID_ALL), cfg5 points: full DP int32 (OVL_LANE_FORM=3), bands 64 / 32 / 8.
+# A/B of the lane kernels' grid, cfg5 points: full DP int32 (OVL_LANE_FORM=3), bands 64 / 32 / 8.  Round 5 ran it
+# when resident slots looping over the tiles was the default and "all" a variant; now every tile launched is the
+# default and the slots grid the variant: make -C genome-assembly-using-overlap-graphs_amd/csrc variant_lane
+# V=gridall DEFS=-DOVL_LANE_GRID_SLOTS (the labels def/all then swap).
 # usage: bash tools/gpu_lane_grid_ab.sh [tag]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -17,7 +19,8 @@ for l in open('$O/$f.log'):
     if l.startswith('{\"metric\"'):
         d=json.loads(l); print('$f', [(p['band'], p.get('kernel'), round(p['kernel_ms'],3)) for p in d['band_sweep']['points']])"; done
 echo ok
-# the h2 kernel's hand-off in HBM (build/ablate_h2hbm, -DOVL_H2_HBM): its lane tests, then cfg5's full DP against the default
+# the h2 kernel's hand-off, HBM against LDS (round 5: LDS the default, HBM the variant; now HBM is the default and
+# the variant is make variant_lane V=h2hbm DEFS=-DOVL_H2_LDS, labels swapped): its lane tests, then cfg5's full DP
 V2=genome-assembly-using-overlap-graphs_amd/build/ablate_h2hbm/libovl.so
 if [ -f $V2 ]; then
   OVL_LIB_PATH=$V2 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dp_lane.py -x -q -k "h2" --timeout 200 --timeout-method thread -p no:cacheprovider > $O/hbm_tests.log 2>&1 || { tail -20 $O/hbm_tests.log; exit 1; }
