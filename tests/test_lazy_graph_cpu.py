@@ -219,3 +219,34 @@ def test_streamed_build_rejects_a_mismatched_csr():
         mod.build_overlap_stream(*args, cut, np.ascontiguousarray(heads[:n]), np.ascontiguousarray(w[:n]))
     node, succ, pred, _rem, n_removed = mod.build_overlap_stream(*args, off, heads, w)
     assert len(node) == len(succ) == len(pred) == E.n_nodes() and n_removed >= 0
+
+
+@pytest.mark.parametrize("on", ["1", "0"])
+def test_arena_pool_installs_and_reuses(on):
+    """csrc/ovl_digraph.c arena_pool: with OVL_ARENA_POOL=1 (the default) the builder module's first load installs the
+    pooled arena allocator; arenas freed by one batch of dicts serve the next (reused, not mapped again); with
+    OVL_ARENA_POOL=0 CPython's allocator stays.  In a child process: the allocator is process-wide."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from ovlgraph import overlapGraphs as og\n"
+        "m = og._digraph()\n"
+        "x = [{'weight': i, 'end_position': i} for i in range(300000)]; del x\n"
+        "a = m.arena_pool(False)\n"
+        "y = [{'weight': i, 'end_position': i} for i in range(300000)]\n"
+        "assert sum(d['weight'] for d in y) == 299999 * 300000 // 2\n"
+        "b = m.arena_pool(False)\n"
+        "print(a['on'], a['mapped_bytes'], b['mapped_bytes'], b['reused_arenas'])\n"
+    ) % os.path.join(root, "genome-assembly-using-overlap-graphs_amd")
+    env = dict(os.environ, OVL_ARENA_POOL=on)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    installed, mapped_a, mapped_b, reused = (int(v) for v in out.stdout.split())
+    if on == "1":
+        assert installed == 1 and mapped_a > 0 and reused > 0
+        assert mapped_b == mapped_a  # the second batch fit in the arenas the first one freed
+    else:
+        assert installed == 0 and mapped_a == 0 and reused == 0
