@@ -49,6 +49,7 @@
 #include "ovl_expand.h"
 #include "ovl_pool.h"
 #include "ovl_kernels.h"
+#include "ovl_resident.h"
 
 #define OVL_API extern "C" __attribute__((visibility("default")))
 
@@ -108,6 +109,12 @@ struct Knobs {
     // by the widen / runs kernels), plain (the caller's int32 arrays)
     int32_t compact = 1;
     int32_t pairs_ix = 1;
+    // OVL_RESIDENT: scoring calls over the resident candidate list into host arrays go to the device's resident grid
+    // (ovl_resident.h) -- 0 never, 1 (default) from resident_min pairs up to resident_max, 2 at every size
+    int32_t resident = 1;
+    int64_t resident_min = 1;
+    int64_t resident_max = int64_t(1) << 40;
+    int32_t resident_blocks = 2;  // the grid's blocks of 256 threads per CU
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -248,6 +255,7 @@ struct Dev {
     const uint16_t* ix_b16 = nullptr;
     const uint8_t* ix_d8 = nullptr;
     const int32_t* ix_base = nullptr;
+    ResidentGrid res;  // the resident scoring grid (ovl_resident.h), launched by the first call that uses it
 };
 
 // The host side of a read-set upload in one pinned block (grown on demand, kept by the context): offsets,
@@ -654,17 +662,37 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
                 step_max <= 15 && g.mcap <= 256)
                 k.ho = 2;
             k.h2 = k.ho == 2 && c->lane_h2 && ovl_dp_lane_h2_ok(match, mismatch, indel);
-            // hand-off columns in HBM: one per resident slot (HO 0 / 1), per tile for the h2 form's HBM variant
-            const size_t col_bytes =
-                k.h2 ? (size_t)ovl_dp_lane_h2_col_bytes(n_pairs, g.mcap)
+            // hand-off columns in HBM: one per resident slot (HO 0 / 1), per tile for the h2 form's HBM variant --
+            // which launches at most kH2Slice pairs at a time over one reused column buffer (lcap / 2 bytes per
+            // pair: 1 GiB at 256-base reads), and falls back to the int32 form (HO 2: no HBM column) when even that
+            // cannot be allocated
+            constexpr int64_t kH2Slice = int64_t(1) << 23;
+            const int64_t slice = k.h2 ? std::min(n_pairs, kH2Slice) : n_pairs;
+            size_t col_bytes =
+                k.h2 ? (size_t)ovl_dp_lane_h2_col_bytes(slice, g.mcap)
                      : (k.ho == 2 ? 0 : (size_t)k.slots * ovl_dp_lane_rcap(g.mcap) * 64 * sizeof(uint32_t));
-            HIPCHK(c, scratch_acquire(c, s, {{&c->lane_col, col_bytes}}));
+            hipError_t se = scratch_acquire(c, s, {{&c->lane_col, col_bytes}});
+            if (se == hipErrorOutOfMemory && k.h2) {
+                (void)hipGetLastError();
+                k.h2 = 0;
+                col_bytes = 0;
+                se = scratch_acquire(c, s, {{&c->lane_col, col_bytes}});
+            }
+            HIPCHK(c, se);
             k.sfx_words = as<uint32_t>(c->sfx);
             k.pfx_words = as<uint32_t>(c->pfx);
             k.srow = c->srow;
             k.wsfx = c->wmax;
             k.colbuf = as<uint32_t>(c->lane_col);
-            HIPCHK(c, ovl_launch_dp_lane(&g, &k, s));
+            for (int64_t lo = 0; lo < n_pairs; lo += slice) {
+                OvlDpArgs gs = g;
+                gs.a_idx = d_a + lo;
+                gs.b_idx = d_b + lo;
+                gs.out_score = d_score + lo;
+                gs.out_end = d_end + lo;
+                gs.n_pairs = std::min(slice, n_pairs - lo);
+                HIPCHK(c, ovl_launch_dp_lane(&gs, &k, s));
+            }
             HIPCHK(c, scratch_release(c, s));
             return OVL_OK;
         }
@@ -757,6 +785,10 @@ Knobs read_knobs() {
         k.lane_h2 = (v >> 2) & 1;
     }
     if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("OVL_RESIDENT")) {  // mode[,blocks per CU] (also "1x4")
+        k.resident = std::max(0, std::min(2, atoi(e)));
+        if (const char* c = strpbrk(e, ",x")) k.resident_blocks = std::max(1, std::min(8, atoi(c + 1)));
+    }
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
         k.pack_direct_pct = std::max(0, std::min(100, atoi(e)));
@@ -802,6 +834,7 @@ void free_staging(int32_t*& p) {
 
 void destroy_dev(Dev* d) {
     if (!d) return;
+    d->res.release();
     (void)hipSetDevice(d->device);
     for (hipStream_t s : {d->stream, d->s_in})
         if (s) (void)hipStreamSynchronize(s);
@@ -837,6 +870,9 @@ hipError_t init_dev(Dev* d) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
         d->cu_count = prop.multiProcessorCount;
+    d->res.device = d->device;
+    d->res.cu_count = d->cu_count;
+    d->res.blocks_per_cu = d->k.resident_blocks;
     for (hipStream_t* s : {&d->stream, &d->s_in}) {
         e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
         if (e != hipSuccess) return e;
@@ -1827,6 +1863,13 @@ int check_scoring_args(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t inde
     return make_plan(c->devs[0], match, mismatch, indel, band, p);
 }
 
+// Stops the context's resident grids (ovl_resident.h) before other work on its devices: a grid's stream would hold
+// a device synchronisation or a free until its idle deadline, and its blocks hold CU slots during other launches.
+void quiet(ovl_ctx* c) {
+    if (c)
+        for (Dev* d : c->devs) (void)d->res.stop();
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------- context
@@ -2157,6 +2200,7 @@ bool same_reads(const ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, i
 // (the pinned stage must outlive the copy)
 int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads, bool sync) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(c);
     if (n_reads < 0) return fail(c, OVL_E_ARG, "n_reads < 0");
     if (n_reads > 0 && !offsets) return fail(c, OVL_E_ARG, "offsets is NULL");
     if (n_reads > 0 && offsets[0] < 0) return fail(c, OVL_E_ARG, "offsets[0] < 0");
@@ -2266,6 +2310,7 @@ OVL_API int ovl_score_device(ovl_ctx* c, const int32_t* d_a, const int32_t* d_b,
                              int32_t mismatch, int64_t indel, int32_t band, int32_t* d_score, int32_t* d_end,
                              void* stream) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(c);
     if (n_pairs < 0) return fail(c, OVL_E_ARG, "n_pairs < 0");
     if (n_pairs > 0 && (!d_a || !d_b || !d_score || !d_end)) return fail(c, OVL_E_ARG, "NULL device pointer");
     Dev* d = c->devs[0];
@@ -2281,6 +2326,7 @@ OVL_API int ovl_score_device(ovl_ctx* c, const int32_t* d_a, const int32_t* d_b,
 
 OVL_API int ovl_check_device_errors(ovl_ctx* c) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(c);
     DeviceGuard guard;
     int rc = OVL_OK;
     for (Dev* d : c->devs) {
@@ -2299,6 +2345,7 @@ OVL_API int ovl_check_device_errors(ovl_ctx* c) {
 OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_idx, int64_t n_pairs, int32_t match,
                            int32_t mismatch, int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end) {
     if (!c) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(c);
     if (n_pairs < 0) return fail(c, OVL_E_ARG, "n_pairs < 0");
     if (n_pairs > 0 && (!a_idx || !b_idx || !out_score || !out_end))
         return fail(c, OVL_E_ARG, "NULL host pointer");
@@ -2355,6 +2402,7 @@ OVL_API int ovl_score_pairs(ovl_ctx* c, const uint8_t* seqs, const int64_t* offs
 OVL_API int ovl_align_one(ovl_ctx* ctx, int32_t a, int32_t b, int32_t match, int32_t mismatch, int64_t indel,
                           int32_t* out_score, int32_t* out_end, int8_t* traceback) {
     if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(ctx);
     Dev* c = ctx->devs[0];
     if (!out_score || !out_end) return fail(c, OVL_E_ARG, "NULL output pointer");
     if (c->n_reads < 0) return fail(c, OVL_E_STATE, "no resident reads: call ovl_set_reads first");
@@ -2469,6 +2517,7 @@ int cand_emit(Dev* c, int32_t k) {
 
 OVL_API int ovl_candidates(ovl_ctx* ctx, int32_t k, int64_t* out_n_pairs) {
     if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(ctx);
     if (!out_n_pairs) return fail(ctx, OVL_E_ARG, "out_n_pairs is NULL");
     if (k < 0) return fail(ctx, OVL_E_ARG, "k-mer length must be non-negative (k=%d)", k);
     Dev* d0 = ctx->devs[0];
@@ -2535,6 +2584,7 @@ OVL_API int ovl_candidates_device(const ovl_ctx* ctx, const int32_t** d_a_idx, c
 
 OVL_API int ovl_candidates_shards(ovl_ctx* ctx, int32_t n_shards, int64_t* bounds) {
     if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(ctx);
     if (n_shards <= 0 || !bounds) return fail(ctx, OVL_E_ARG, "n_shards <= 0 or bounds is NULL");
     Dev* d = ctx->devs[0];
     if (d->cand_n < 0) return fail(ctx, OVL_E_STATE, "no candidate list: call ovl_candidates first");
@@ -2543,6 +2593,108 @@ OVL_API int ovl_candidates_shards(ovl_ctx* ctx, int32_t n_shards, int64_t* bound
     int rc = device_cuts(d, 0, d->cand_n, n_shards, cuts);
     if (rc != OVL_OK) return rc;
     std::copy(cuts.begin(), cuts.end(), bounds);
+    return OVL_OK;
+}
+
+namespace {
+
+constexpr int kResidentFellBack = 1000;  // (resident_call: the call goes through the launch pipeline instead)
+
+// A call over the resident candidate list that the resident grid scores: one device, the uniform kernel's form with
+// int32 keys and 2-byte record codes (ends <= 254), timing off (its launch events time the launch pipeline), and a
+// host pool of at least 6 threads to expand the records (fewer: several processes share the CPUs, pack_ok)
+bool resident_ok(const ovl_ctx* c, const Plan& p, int64_t n) {
+    if (c->devs.size() != 1 || c->timing || CopyPool::threads() < 6) return false;
+    const Dev* d = c->devs[0];
+    if (d->k.resident == 0 || d->res.broken) return false;
+    if (d->k.resident == 1 && (n < d->k.resident_min || n > d->k.resident_max)) return false;
+    return p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 && d->planes == 2 && d->wmax >= 1 && d->wmax <= 8 &&
+           d->lmax >= 1 && d->lmax <= 254 && d->cand_n >= 0;
+}
+
+int resident_call(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t match, int32_t mismatch, int32_t* out_s,
+                  int32_t* out_e) {
+    Dev* d = ctx->devs[0];
+    HIPCHK(d, hipSetDevice(d->device));
+    // heavy tiles first when the range starts on a list tile (uniform_kernel's order); built once per list, with the
+    // grid stopped (ensure_heavy may reallocate)
+    ResidentCall rc_;
+    if (lo % 64 == 0) {
+        if (d->heavy_for != d->cand_n) {
+            (void)d->res.stop();
+            const int r = ensure_heavy(d);
+            if (r != OVL_OK) return r;
+        }
+        const int64_t t0 = lo / 64, t1 = t0 + (hi - lo + 63) / 64;
+        const auto k0 = std::lower_bound(d->h_heavy.begin(), d->h_heavy.end(), t0);
+        const auto k1 = std::lower_bound(d->h_heavy.begin(), d->h_heavy.end(), t1);
+        if (k1 > k0) {
+            rc_.heavy_ids = as<int32_t>(d->heavy_ids) + (k0 - d->h_heavy.begin());
+            rc_.heavy_n = (int64_t)(k1 - k0);
+            rc_.tile_base = t0;
+        }
+    }
+    ResidentReads rd;
+    rd.sfx = as<uint32_t>(d->sfx);
+    rd.pfx = as<uint32_t>(d->pfx);
+    rd.len = as<int32_t>(d->len);
+    rd.n_reads = d->n_reads;
+    rd.lw = d->lmax;
+    rd.wmax = d->wmax;
+    rd.full = as<uint32_t>(d->full);
+    rd.tile_flags = rc_.heavy_n > 0 ? as<uint8_t>(d->tile_flags) : nullptr;
+    rc_.d_a = as<int32_t>(d->cand_a) + lo;
+    rc_.d_b = as<int32_t>(d->cand_b) + lo;
+    rc_.n = hi - lo;
+    rc_.match = match;
+    rc_.mismatch = mismatch;
+    rc_.out_s = out_s;
+    rc_.out_e = out_e;
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t n_bad = 0;
+    hipError_t e = hipSuccess;
+    const int r = d->res.score(rd, rc_, &n_bad, &e);
+    if (r == ResidentGrid::kFallback) return kResidentFellBack;
+    if (r != ResidentGrid::kOk)
+        return fail(ctx, OVL_E_HIP, "resident grid: %s", hipGetErrorString(e));
+    ctx->t_launches.clear();
+    ctx->t_kernel_ms = 0.0;
+    ctx->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const int64_t n = hi - lo, nt = (n + 63) / 64;
+    ctx->x_res_bytes = 128 * nt + 8 * d->res.last_specials;
+    ctx->x_link_bytes = ctx->x_res_bytes;
+    ctx->x_packed_pairs = n;
+    ctx->x_rec_pairs = n;
+    ctx->x_esc = d->res.last_specials;
+    ctx->x_ix_pairs = ctx->x_dec_pairs = 0;
+    if (n_bad > 0) return fail(ctx, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
+    return OVL_OK;
+}
+
+}  // namespace
+
+OVL_API int ovl_quiesce(ovl_ctx* ctx) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    DeviceGuard guard;
+    for (Dev* d : ctx->devs) HIPCHK(ctx, d->res.stop());
+    return OVL_OK;
+}
+
+OVL_API int ovl_resident_stats(const ovl_ctx* ctx, int32_t* alive, int64_t* launches, int64_t* relaunches,
+                               int32_t* broken) {
+    if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    int32_t al = 0, br = 0;
+    int64_t l = 0, rl = 0;
+    for (const Dev* d : ctx->devs) {
+        al += d->res.alive() ? 1 : 0;
+        br += d->res.broken ? 1 : 0;
+        l += d->res.n_launches;
+        rl += d->res.n_relaunches;
+    }
+    if (alive) *alive = al;
+    if (launches) *launches = l;
+    if (relaunches) *relaunches = rl;
+    if (broken) *broken = br;
     return OVL_OK;
 }
 
@@ -2560,6 +2712,11 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     if (hi == lo) return OVL_OK;
     if (!out_score || !out_end) return fail(ctx, OVL_E_ARG, "NULL host pointer");
     DeviceGuard guard;
+    if (resident_ok(ctx, p, hi - lo)) {
+        rc = resident_call(ctx, lo, hi, match, mismatch, out_score, out_end);
+        if (rc != kResidentFellBack) return rc;
+    }
+    quiet(ctx);
     const size_t bytes = sizeof(int32_t) * (size_t)(hi - lo);
     Call C;
     C.plan = &p;
@@ -2603,6 +2760,7 @@ OVL_API int ovl_local_align(ovl_ctx* ctx, const uint8_t* query, int32_t n, const
                             int32_t* out_end_j, int32_t* out_start_i, int32_t* out_start_j, int8_t* ops,
                             int64_t ops_cap, int64_t* out_n_ops) {
     if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
+    quiet(ctx);
     Dev* c = ctx->devs[0];
     DeviceGuard guard;
     if (n < 0 || m < 0) return fail(c, OVL_E_ARG, "negative length");

@@ -227,18 +227,18 @@ inline bool rec_tile_ready_scalar(const uint32_t* r, uint32_t phase) {
 }
 
 // One record's pairs [0, cnt) (cnt <= 64) into s / e (scalar) once the record and all its special words have
-// landed: the specials' count (their words in taken[0 ..), the bad pairs among them added to *bad), or -2 (nothing
-// written) while something has not.
-inline int rec_tile_scalar(int32_t* s, int32_t* e, const uint32_t* r, uint32_t* sp, const RecK& k, size_t cnt,
-                           uint32_t phase, int* bad, uint32_t** taken) {
+// landed: the specials' count (the bad pairs among them added to *bad), or -2 (nothing written) while something has
+// not.  get(l) is pair l's special word once it has landed, else 0 (a special word is never 0).
+template <class Get>
+inline int rec_tile_scalar_t(int32_t* s, int32_t* e, const uint32_t* r, const RecK& k, size_t cnt, uint32_t phase,
+                             int* bad, Get&& get) {
     if (!rec_tile_ready_scalar(r, phase)) return -2;
     const volatile uint32_t* v = r;
     uint32_t wv[64];
     int m = 0;
     for (size_t l = 0; l < cnt; ++l) {  // (every special word first: a tile is taken whole or not at all)
         if (((v[l & 31] >> (l < 32 ? 0 : 15)) & 0x7FFFu) != kRecSpecial) continue;
-        taken[m] = sp + l;
-        if ((wv[m] = *(volatile uint32_t*)taken[m]) == 0u) return -2;
+        if ((wv[m] = get(l)) == 0u) return -2;
         ++m;
     }
     int q = 0;
@@ -254,14 +254,37 @@ inline int rec_tile_scalar(int32_t* s, int32_t* e, const uint32_t* r, uint32_t* 
     return m;
 }
 
+// the launch form (sink 3): special words in a side array, zero until they land; the words read go to taken[0 ..)
+inline int rec_tile_scalar(int32_t* s, int32_t* e, const uint32_t* r, uint32_t* sp, const RecK& k, size_t cnt,
+                           uint32_t phase, int* bad, uint32_t** taken) {
+    int m = 0;
+    return rec_tile_scalar_t(s, e, r, k, cnt, phase, bad, [&](size_t l) -> uint32_t {
+        taken[m] = sp + l;
+        const uint32_t w = *(volatile uint32_t*)taken[m];
+        m += w != 0u;
+        return w;
+    });
+}
+
+// the resident grid's ring form (ovl_kernels.h OvlResidentBody): 8-byte words {payload, seq}, current when the high
+// half is the request's seq
+struct RingSp {
+    const uint64_t* sp;
+    uint32_t seq;
+    uint32_t operator()(size_t l) const {
+        const uint64_t w = *(const volatile uint64_t*)(sp + l);
+        return (uint32_t)(w >> 32) == seq ? (uint32_t)w : 0u;
+    }
+};
+
 // AVX-512: readiness check and decode of one full record (64 pairs) from the same two loads; *ready = false (nothing
-// written) while the record or one of its special words has not landed.  Stores non-temporally when `al` (s and e
-// 64-byte aligned).  Returns the specials' count (their words in taken[0 ..)).
-__attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(int32_t* s, int32_t* e,
-                                                                                  const uint32_t* r, uint32_t* sp,
-                                                                                  const RecK& k, uint32_t phase,
-                                                                                  bool al, bool* ready, int* bad,
-                                                                                  uint32_t** taken) {
+// written) while the record or one of its special words has not landed (get: as rec_tile_scalar_t).  Stores
+// non-temporally when `al` (s and e 64-byte aligned).  Returns the specials' count.
+template <class Get>
+__attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512_t(int32_t* s, int32_t* e,
+                                                                                    const uint32_t* r, const RecK& k,
+                                                                                    uint32_t phase, bool al,
+                                                                                    bool* ready, int* bad, Get&& get) {
     const __m512i w0 = _mm512_load_si512(r), w1 = _mm512_load_si512(r + 16);
     const __m512i sign = _mm512_set1_epi32((int)0x80000000u);
     const __mmask16 want = phase ? (__mmask16)0xFFFF : (__mmask16)0;
@@ -290,10 +313,8 @@ __attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(
     int m = 0, nb = 0;
     for (int q = 0; q < 4; ++q)
         for (uint32_t b = spm[q]; b; b &= b - 1, ++m) {
-            uint32_t* w = sp + 16 * q + __builtin_ctz(b);
-            const uint32_t v = *(volatile uint32_t*)w;
+            const uint32_t v = get((size_t)(16 * q + __builtin_ctz(b)));
             if (v == 0u) return 0;
-            taken[m] = w;
             int32_t sv, ev;
             rec_decode_special(v, k, sv, ev);
             nb += v == 0xFFFFFFFFu;
@@ -308,6 +329,20 @@ __attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(
     *bad += nb;
     *ready = true;
     return m;
+}
+
+__attribute__((target("avx512f,avx512bw,avx512dq"))) inline int rec_tile_avx512(int32_t* s, int32_t* e,
+                                                                                  const uint32_t* r, uint32_t* sp,
+                                                                                  const RecK& k, uint32_t phase,
+                                                                                  bool al, bool* ready, int* bad,
+                                                                                  uint32_t** taken) {
+    int m = 0;
+    return rec_tile_avx512_t(s, e, r, k, phase, al, ready, bad, [&](size_t l) -> uint32_t {
+        taken[m] = sp + l;
+        const uint32_t w = *(volatile uint32_t*)taken[m];
+        m += w != 0u;
+        return w;
+    });
 }
 
 // this CPU runs rec_tile_avx512

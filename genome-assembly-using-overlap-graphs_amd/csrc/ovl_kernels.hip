@@ -32,6 +32,7 @@
 #include <hip/hip_ext.h>
 
 #include "ovl_kernels.h"
+#include "ovl_grid.h"
 
 // uniform sweep: two shifts from one shifted row (sweep_uniform, keys_s2 / keys_t2); 0: one shifted row per shift
 #ifndef OVL_SHIFT_PAIR
@@ -1153,6 +1154,264 @@ __global__ __launch_bounds__(256) void general_kernel(
         general_unit<P, W, KM>(mine, p, a, b, sfx, pfx, len, n_reads, r0, rs_log2, 0, match, mismatch, out_score,
                                out_end, err_flag);
     }
+}
+
+// ----------------------------------------------------------------------------- resident grid
+
+// One tile's results as a ring record (ovl_grid.h OvlResidentBody): put_tile_rec's codes, the phase bit of the ring
+// lap, and a special pair's word as one 8-byte store {payload, seq} (payload: put_tile_rec's special word).  Every
+// store is a system-scope (sc0 sc1) write-through store: a resident grid never ends, so a store the XCD's L2 kept
+// (plain or non-temporal) would reach host memory only when evicted (measured: records arrived only when the grid
+// left).  The record goes out as 16 lanes x 8 bytes.
+__device__ __forceinline__ void put_ring_rec(uint32_t* rec, uint64_t* sp, int64_t ri, uint32_t phase, uint32_t seq,
+                                             bool mine, int32_t sc, int32_t en, int32_t n, int32_t match, float inv,
+                                             int lane) {
+    uint32_t c = 0;
+    if (mine) {
+        uint32_t special = 0;
+        if (en < 0) {
+            special = 0xFFFFFFFFu;
+        } else if (en > n) {
+            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * n - sc) * inv);
+            special = 0x80000000u | (uint32_t)en << 16 | x << 8 | (uint32_t)n;
+        } else {
+            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * en - sc) * inv);
+            c = ((uint32_t)en * (uint32_t)(en + 1) >> 1) + x;
+        }
+        if (special) {
+            c = 0x7FFFu;
+            __hip_atomic_store(sp + 64 * ri + lane, (uint64_t)seq << 32 | special, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    const uint32_t hi = (uint32_t)__shfl_xor((int)c, 32, 64);
+    const uint32_t d = phase << 31 | hi << 15 | c;  // (dword `lane` of the record, lanes < 32)
+    const uint32_t d0 = (uint32_t)__shfl((int)d, 2 * (lane & 15), 64);
+    const uint32_t d1 = (uint32_t)__shfl((int)d, 2 * (lane & 15) + 1, 64);
+    if (lane < 16)
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(rec + 32 * ri) + lane, (uint64_t)d1 << 32 | d0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One 64-pair tile of a resident request: uniform_kernel's throughput-mode sweep with every pair in it (TT: reads
+// b cut at the genome end snapshot their block maxima, shorter reads a add their window keys), into the ring.
+template <int W>
+__device__ __forceinline__ void resident_tile(int64_t tile, const OvlResidentBody& q, const uint32_t* __restrict__ sfx,
+                                              const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
+                                              int32_t n_reads, int32_t lw, const uint32_t* __restrict__ full,
+                                              int32_t match, int32_t mismatch, int lane) {
+    constexpr int P = 2;
+    constexpr int SROW = (W * P + 3) & ~3;
+    constexpr int TROW = (W * P + 3) & ~3;
+    const int64_t p = tile * 64 + lane;
+    const bool mine = p < q.n_pairs;
+    int32_t a = mine ? q.a_idx[p] : 0;
+    int32_t b = mine ? q.b_idx[p] : 0;
+    const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
+    if (!ok) { a = 0; b = 0; }
+    uint32_t Sw[SROW], Tw[TROW];
+    load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
+    load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
+    const bool fa = ok && ((full[a >> 5] >> (a & 31)) & 1u);
+    const int32_t mb = len[b];
+    int32_t na = lw;
+    if (ok && !fa) na = len[a];
+    const bool uni = fa && mb == lw;
+    const bool tt = ok && !uni;
+    const int32_t tm = tt ? (na < mb ? na : mb) : -1;
+    uint32_t tmask = 0;
+    for (uint64_t bm = __ballot(tt); bm; bm &= bm - 1)
+        tmask |= 1u << (__builtin_amdgcn_readlane(tm, (int)__builtin_ctzll(bm)) & 31);
+    int32_t best = sweep_uniform<W, 0>(Sw, Tw, lw, match, mismatch - match, 0u, 32u, tmask, tm);
+    const bool win = tt && na < mb;
+    uint64_t wm = __ballot(win);
+    if (wm) {
+        int32_t jlo = 1 << 30, jhi = 0;
+        for (; wm; wm &= wm - 1) {
+            const int l = (int)__builtin_ctzll(wm);
+            jlo = min(jlo, __builtin_amdgcn_readlane(na, l) + 1);
+            jhi = max(jhi, __builtin_amdgcn_readlane(mb, l));
+        }
+        const int32_t wk = window_keys<W>(Sw, Tw, na, mb, jlo, jhi, match, mismatch - match);
+        if (win && wk > best) best = wk;
+    }
+    int32_t sc, en;
+    Key<0>::decode(best, sc, en);
+    const int64_t g = q.pos + tile;
+    const int64_t ri = g & ((int64_t(1) << q.ring_log2) - 1);
+    const uint32_t phase = (uint32_t)((g >> q.ring_log2) + 1) & 1u;
+    put_ring_rec(q.rec, q.sp, ri, phase, (uint32_t)q.seq, mine, ok ? sc : -1, ok ? en : -1, na, match,
+                 pack_inv(match, mismatch), lane);
+}
+
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// The resident scoring grid: launched once, it serves requests posted by the host in pinned memory until the host
+// asks it to leave or none comes for idle_ticks (the host relaunches it on its next request), so a call pays
+// neither a launch nor a completion signal -- the results' ring records tell the host when it is done.
+//   Block 0's thread 0 polls the host mailbox (a relaxed system-scope load per poll, s_sleep between), reads the
+// request body, writes a device copy of it under a seqlock (8-byte agent-scope atomics, each group drained) and
+// forwards the sequence number through one device word; the other blocks' thread 0 polls that word and reads the
+// copy (the hand-off of MI355X_MICROARCH.md's first valid row: sc1 stores drained, one flag, sc1 loads).  Each
+// block then scores tiles: wavefront w of the grid takes items w, w + waves, ... (heavy tiles first, as
+// uniform_kernel orders them).  No fan-in, no fence: nothing is waited for on the device.
+//   Every wait is bounded: block 0 leaves (and tells the others) after idle_ticks without a request; the other
+// blocks leave after twice that without a new forward, so a grid whose block 0 never ran still ends.
+template <int W>
+__global__ __launch_bounds__(256, (W >= 7 ? 2 : 4)) void resident_kernel(
+    const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
+    int32_t n_reads, int32_t lw, const uint32_t* __restrict__ full, const uint8_t* __restrict__ tile_flags,
+    const OvlResidentCtl* mailbox, uint32_t* fwd, OvlResidentBody* dslot, uint32_t seq_base, uint64_t idle_ticks,
+    uint64_t* status) {
+    __shared__ uint64_t s_body[kResidentBodyWords];
+    __shared__ int s_go;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t n_waves = (int64_t)gridDim.x * 4;
+    uint32_t last = seq_base;  // (thread 0)
+    for (;;) {
+        if (threadIdx.x == 0) {
+            int go = 0;
+            uint64_t v[kResidentBodyWords];
+            if (blockIdx.x == 0) {
+                const uint64_t t_end = wall_clock64() + idle_ticks;
+                uint32_t seq = 0;
+                for (;;) {
+                    const uint64_t c = __hip_atomic_load(&mailbox->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (c >> 32) break;  // asked to leave
+                    if ((uint32_t)c != last) {
+                        seq = (uint32_t)c;
+                        go = 1;
+                        break;
+                    }
+                    if (wall_clock64() > t_end) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                int why = go ? 0 : 2;  // (status: 1 asked to leave, 2 idle, 3 a body that is not the request's)
+                if (!go && wall_clock64() <= t_end) why = 1;
+                if (go) {
+                    vm_drain();
+                    const uint64_t* src = reinterpret_cast<const uint64_t*>(&mailbox->body[seq & 1]);
+#pragma unroll
+                    for (int k = 0; k < kResidentBodyWords; ++k)
+                        v[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    go = (uint32_t)v[0] == seq;  // (the host writes the body before ctl: always)
+                    if (!go) why = 3;
+                }
+                if (!go && status) {  // why block 0 left, for the host's trace (pinned, written only here)
+                    __hip_atomic_store(status + 1, (uint64_t)last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(status + 2, (uint64_t)seq | (v[0] << 32), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(status + 3, idle_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    vm_drain();
+                    __hip_atomic_store(status, (uint64_t)why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                if (go) {
+                    uint64_t* ds = reinterpret_cast<uint64_t*>(&dslot[seq & 3]);
+                    __hip_atomic_store(ds, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    vm_drain();
+#pragma unroll
+                    for (int k = 1; k < kResidentBodyWords; ++k)
+                        __hip_atomic_store(ds + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    vm_drain();
+                    __hip_atomic_store(ds, (uint64_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    vm_drain();
+                    __hip_atomic_store(fwd, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    last = seq;
+                } else {
+                    __hip_atomic_store(fwd, kResidentLeave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                const uint64_t t_end = wall_clock64() + 2 * idle_ticks;
+                for (;;) {
+                    const uint32_t f = __hip_atomic_load(fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (f == kResidentLeave) break;
+                    if (f != 0u && f != last) {
+                        vm_drain();
+                        const uint64_t* ds = reinterpret_cast<const uint64_t*>(&dslot[f & 3]);
+                        const uint64_t s1 = __hip_atomic_load(ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        vm_drain();
+#pragma unroll
+                        for (int k = 1; k < kResidentBodyWords; ++k)
+                            v[k] = __hip_atomic_load(ds + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        vm_drain();
+                        const uint64_t s2 = __hip_atomic_load(ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (s1 == (uint64_t)f && s2 == (uint64_t)f) {  // (else rewritten meanwhile: poll again)
+                            v[0] = s1;
+                            last = f;
+                            go = 1;
+                            break;
+                        }
+                    }
+                    if (wall_clock64() > t_end) break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (!go && status)  // (a block that left on its own deadline, not told to)
+                    if (__hip_atomic_load(fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kResidentLeave)
+                        __hip_atomic_store(status + 4, (uint64_t)blockIdx.x + 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (go) {
+#pragma unroll
+                for (int k = 0; k < kResidentBodyWords; ++k) s_body[k] = v[k];
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) return;
+        OvlResidentBody q;  // (wave-uniform: scalar registers, as kernel arguments would be)
+        {
+            uint64_t* d = reinterpret_cast<uint64_t*>(&q);
+#pragma unroll
+            for (int k = 0; k < kResidentBodyWords; ++k) {
+                const uint64_t x = s_body[k];
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+                d[k] = (uint64_t)hi << 32 | lo;
+            }
+        }
+        const int32_t match = (int32_t)(uint32_t)q.scoring, mismatch = (int32_t)(uint32_t)(q.scoring >> 32);
+        const int64_t n_tiles = (q.n_pairs + 63) >> 6;
+        const bool hf = q.heavy_ids != nullptr && q.heavy_n > 0;
+        const int64_t n_items = hf ? n_tiles + q.heavy_n : n_tiles;
+        for (int64_t item = wave; item < n_items; item += n_waves) {  // (wave-uniform)
+            int64_t tile = item;
+            if (hf) {
+                if (item < q.heavy_n) {
+                    tile = (int64_t)q.heavy_ids[item] - q.tile_base;
+                } else {
+                    tile = item - q.heavy_n;
+                    if (tile_flags[q.tile_base + tile]) continue;  // done among the heavy ones
+                }
+            }
+            resident_tile<W>(tile, q, sfx, pfx, len, n_reads, lw, full, match, mismatch, lane);
+        }
+        __syncthreads();  // (thread 0 rewrites s_body for the next request)
+    }
+}
+
+extern "C" hipError_t ovl_launch_resident(const OvlResidentArgs* g, hipStream_t stream) {
+    if (g->lw <= 0 || g->lw > 254 || g->blocks <= 0 || !g->mailbox || !g->fwd || !g->dslot) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)g->blocks), block(256);
+#define OVL_RESIDENT_CASE(Wc)                                                                                       \
+    case Wc:                                                                                                        \
+        resident_kernel<Wc><<<grid, block, 0, stream>>>(g->sfx, g->pfx, g->len, g->n_reads, g->lw, g->full,         \
+                                                        g->tile_flags, g->mailbox, g->fwd, g->dslot, g->seq_base,   \
+                                                        g->idle_ticks, g->status);                                  \
+        break;
+    switch (g->wmax) {
+        OVL_RESIDENT_CASE(1)
+        OVL_RESIDENT_CASE(2)
+        OVL_RESIDENT_CASE(3)
+        OVL_RESIDENT_CASE(4)
+        OVL_RESIDENT_CASE(5)
+        OVL_RESIDENT_CASE(6)
+        OVL_RESIDENT_CASE(7)
+        OVL_RESIDENT_CASE(8)
+        default: return hipErrorInvalidValue;
+    }
+#undef OVL_RESIDENT_CASE
+    return hipGetLastError();
 }
 
 // ----------------------------------------------------------------------------- generic DP

@@ -277,6 +277,20 @@ class OverlapEngine:
                 check(rc, ctx)
         return score
 
+    def quiesce(self) -> None:
+        """Make this context's resident scoring grids leave the device now (ovl_quiesce): before a whole-device
+        synchronisation (torch.cuda.synchronize), which would otherwise wait for their idle deadline.  The next
+        eligible scoring call relaunches them."""
+        check(self._L.ovl_quiesce(self._ctx), self._ctx)
+
+    def resident_stats(self) -> Dict[str, int]:
+        """{alive, launches, relaunches, broken} of this context's resident grids (ovl_resident_stats)."""
+        al, br = ctypes.c_int32(), ctypes.c_int32()
+        ln, rl = ctypes.c_int64(), ctypes.c_int64()
+        check(self._L.ovl_resident_stats(self._ctx, ctypes.byref(al), ctypes.byref(ln), ctypes.byref(rl),
+                                         ctypes.byref(br)), self._ctx)
+        return {"alive": al.value, "launches": ln.value, "relaunches": rl.value, "broken": br.value}
+
     def candidate_shards(self, n_shards: int) -> List[int]:
         """Shard bounds of the resident candidate list balanced by sum len(a)*len(b) + 1 (on the device)."""
         bounds = np.zeros(int(n_shards) + 1, dtype=np.int64)

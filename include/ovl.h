@@ -214,6 +214,18 @@ int ovl_score_candidates(ovl_ctx* ctx, int32_t match, int32_t mismatch, int64_t 
 int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t match, int32_t mismatch,
                                int64_t indel, int32_t band, int32_t* out_score, int32_t* out_end);
 
+/* The resident grid (one per device of a single-device context): ovl_score_candidates(_range) calls of the
+ * uniform kernel's form (ungapped plan, int32 keys, <= 4 symbols, reads <= 254 bases) are served by a kernel that
+ * stays on the device between calls, fed requests through pinned memory -- a call pays no launch and no completion
+ * signal.  It leaves by itself after ~20 ms without a request, when another entry point of the context needs the
+ * device, and at ovl_destroy; OVL_RESIDENT=0 routes every call through the launch pipeline.  ovl_quiesce makes the
+ * context's grids leave now (before a whole-device synchronisation such as torch.cuda.synchronize(), which would
+ * otherwise wait for the idle deadline); the next call relaunches them.  ovl_resident_stats reports how many grids
+ * are resident, their launches (relaunches: calls that found their grid gone) and whether a failed call disabled
+ * the path (its calls then go through the launch pipeline). */
+int ovl_quiesce(ovl_ctx* ctx);
+int ovl_resident_stats(const ovl_ctx* ctx, int32_t* alive, int64_t* launches, int64_t* relaunches, int32_t* broken);
+
 /* Contiguous shard bounds of the candidate list, balanced by sum len(a)*len(b) + 1:
  * bounds[0] = 0 <= bounds[1] <= ... <= bounds[n_shards] = n_pairs (the rule of
  * ovlgraph/sharded.py:shard_bounds, computed on the device). */

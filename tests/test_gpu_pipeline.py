@@ -263,7 +263,7 @@ def test_tile_records_across_read_sets(oracle_mod):
         a, b = enumerate_candidates(reads, 5)
         rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
         sets[cfg] = (reads, a, b, rs, re_, np.random.default_rng(1).permutation(a.shape[0]))
-    with _engine_env({"OVL_PACK": "2"}) as eng:
+    with _engine_env({"OVL_PACK": "2", "OVL_RESIDENT": "0"}) as eng:
         for rnd in range(2):
             for cfg in ("cfg2", "cfg3"):
                 reads, a, b, rs, re_, perm = sets[cfg]
@@ -292,7 +292,7 @@ def test_packed_adaptive_share(oracle_mod, cfg2, cfg2_ref):
     test_step_transport_vs_oracle.)"""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
-    eng = _engine_env({"OVL_PACK_MIN": "0", "OVL_PACK": "1"})
+    eng = _engine_env({"OVL_PACK_MIN": "0", "OVL_PACK": "1", "OVL_RESIDENT": "0"})
     try:
         eng.set_reads(reads)
         eng.candidates(5)
@@ -698,7 +698,10 @@ def test_step_transport_vs_oracle(oracle_mod, cfg, pct):
     from ovlgraph.hostmem import pinned_empty
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
-    eng = _engine_env({"OVL_PACK": "2", "OVL_PACK_DIRECT_PCT": pct} if pct else {"OVL_PACK": "2"})
+    env = {"OVL_PACK": "2", "OVL_RESIDENT": "0"}  # (the launch transport; the resident grid: test_gpu_resident.py)
+    if pct:
+        env["OVL_PACK_DIRECT_PCT"] = pct
+    eng = _engine_env(env)
     try:
         eng.set_reads(reads)
         a, b = eng.candidates(5)

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genome-assembly-using-overlap-graphs_amd"))
 import numpy as np  # noqa: E402
 
-KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN")
+KNOBS = ("OVL_PACK", "OVL_PACK_DIRECT_PCT", "OVL_PIPE_CHUNK", "OVL_PACK_MIN", "OVL_RESIDENT")
 SETTINGS = (("default", {}),)
 if os.environ.get("SHARD_AB_SETTINGS"):
     SETTINGS = tuple((nm, dict(kv.split(":") for kv in spec.split(",") if kv))
