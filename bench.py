@@ -1076,6 +1076,55 @@ def extra_plan(args, world: int):
 SHARDED_SWEEP_BANDS = [4, 8, 16, 32, 64, -1]
 
 
+class Heartbeat:
+    """Rank 0's progress on stderr while the N > 1 stages run: a line when a stage ends and, from a daemon thread,
+    one every `every` seconds naming the stage still running, so a long stage never reads as a hung run (a
+    harness ends a command that writes nothing for 3 minutes)."""
+
+    def __init__(self, rank: int, every: float = 30.0):
+        import threading
+        self.rank, self.every, self.t0 = rank, every, time.perf_counter()
+        self.stage = "setup"
+        self._stop = threading.Event()
+        self._thread = None
+        if rank == 0 and every > 0:
+            self._thread = threading.Thread(target=self._beat, daemon=True)
+            self._thread.start()
+
+    def _beat(self):
+        while not self._stop.wait(self.every):
+            print(f"bench.py: {self.stage} still running at {time.perf_counter() - self.t0:.1f} s", file=sys.stderr,
+                  flush=True)
+
+    def start(self, stage: str):
+        self.stage = stage
+
+    def done(self, what: str):
+        if self.rank == 0:
+            print(f"bench.py: {what} done at {time.perf_counter() - self.t0:.1f} s", file=sys.stderr, flush=True)
+
+    def close(self):
+        self._stop.set()
+
+
+def run_extras(plan, run_stage, budget_s: float, elapsed_max, hb: Heartbeat) -> dict:
+    """The secondary N > 1 stages in order, each under the run's time budget: a stage starts only while the
+    slowest rank's elapsed time (elapsed_max(): the same value on every rank, so every rank takes the same
+    decision and no collective is left waiting) is below budget_s; the others are recorded as skipped."""
+    extras = {}
+    for item in plan:
+        spent = elapsed_max()
+        if spent >= budget_s:
+            extras[item] = {"skipped": f"the N > 1 stages' time budget ({budget_s:.0f} s) was spent "
+                                       f"({spent:.1f} s) before this stage"}
+            hb.done(f"{item} skipped,")
+            continue
+        hb.start(item)
+        extras[item] = run_stage(item)
+        hb.done(item)
+    return extras
+
+
 def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
     """N > 1: the workload's one list sharded over the ranks (the line's value), then the secondary shapes."""
     import torch
@@ -1087,28 +1136,27 @@ def multi_gpu(args, world: int, rank: int, dev, backend: str, shared: bool):
     if shared:
         ident["note"] = ("more ranks than visible GPUs: ranks share devices (flow rehearsal, gloo barriers) -- "
                          "not a scaling number")
-    t_run = time.perf_counter()
-
-    def progress(what):  # (rank 0, stderr: the line on stdout stays the only output there)
-        if rank == 0:
-            print(f"bench.py: {what} done at {time.perf_counter() - t_run:.1f} s", file=sys.stderr, flush=True)
-
+    hb = Heartbeat(rank)
+    hb.start("sharded list")
     top = sharded_list(name, world, rank, dev, backend, args)
-    progress("sharded list")
+    hb.done("sharded list")
     w = top["w"]
-    extras = {}
-    for item in extra_plan(args, world):
+
+    def run_stage(item):
         if item == "weak_scaling":
-            extras[item] = weak_scaling(name, world, rank, dev, backend, args)
+            r = weak_scaling(name, world, rank, dev, backend, args)
         elif item == "cfg4_strong":
-            extras[item] = strong_scaling("cfg4", world, rank, dev, backend, max(5, args.steps // 2), 2)
+            r = strong_scaling("cfg4", world, rank, dev, backend, max(5, args.steps // 2), 2)
         elif item == "cfg5_sharded_band_sweep":
-            extras[item] = sharded_band_sweep(world, rank, dev, w.eng, SHARDED_SWEEP_BANDS, args.sweep_indel, 3,
-                                              backend)
-        elif item == "single_process_all_gpus":
-            extras[item] = single_process_all_gpus(rank, world, shared, w.reads, w.cfg["k"], args.steps, w.eng)
+            r = sharded_band_sweep(world, rank, dev, w.eng, SHARDED_SWEEP_BANDS, args.sweep_indel, 3, backend)
+        else:
+            r = single_process_all_gpus(rank, world, shared, w.reads, w.cfg["k"], args.steps, w.eng)
         dist.barrier()
-        progress(item)
+        return r
+
+    extras = run_extras(extra_plan(args, world), run_stage, args.extra_budget,
+                        lambda: max_over_ranks(time.perf_counter() - hb.t0, world, dev, backend), hb)
+    hb.close()
     line = multi_line(args, world, ident, top, extras) if rank == 0 else None
     w.close()
     return line
@@ -1190,6 +1238,10 @@ def parse_args(argv=None):
     # multi-process line's collectives, gathers and sharded step for real (tests/test_gpu_bench_dist.py)
     ap.add_argument("--dist-path", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run-stage-s", type=float, default=0.0, help=argparse.SUPPRESS)  # each stage sleeps this
+    ap.add_argument("--extra-budget", type=float, default=240.0,
+                    help="seconds after which the N > 1 run starts no further secondary stage")
+    ap.add_argument("--heartbeat", type=float, default=30.0, help=argparse.SUPPRESS)
     # profiling aid at N = 1: time only shard R of N of the list (what rank R scores at N ranks), so rocprofv3 and
     # PMC passes on a one-GPU box see a rank's launches (tools/gpu_r04_shard_profile.sh)
     ap.add_argument("--shard", default=None, help=argparse.SUPPRESS)
@@ -1227,10 +1279,29 @@ def dry_run(args) -> int:
         return 3
     if world > 1:
         dist.barrier()
+    # the stages' budget and heartbeat as a real run takes them (each stage sleeps --dry-run-stage-s instead)
+    hb = Heartbeat(rank, args.heartbeat)
+
+    def elapsed_max():
+        if world == 1:
+            return time.perf_counter() - hb.t0
+        import torch
+        t = torch.tensor([time.perf_counter() - hb.t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def run_stage(item):
+        time.sleep(args.dry_run_stage_s)
+        if world > 1:
+            dist.barrier()
+        return None
+
+    extras = run_extras(extra_plan(args, world), run_stage, args.extra_budget, elapsed_max, hb)
+    hb.close()
     if rank == 0:
         ident = {"world_size": dist.get_world_size() if world > 1 else 1,
                  "backend": dist.get_backend() if world > 1 else None}
-        line = multi_line(args, world, ident, {}, {k: None for k in extra_plan(args, world)})
+        line = multi_line(args, world, ident, {}, extras)
         line["dry_run"] = True
         print(json.dumps(line), flush=True)
     if world > 1:

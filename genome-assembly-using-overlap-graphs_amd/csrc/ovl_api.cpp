@@ -1574,6 +1574,7 @@ int stream_chunk(const Call& C, Job& J, int64_t k) {
         }
         specials.fetch_add(m, std::memory_order_relaxed);
         bad.fetch_add(nbad, std::memory_order_relaxed);
+        _mm_sfence();  // (this part's non-temporal stores drained before the part is reported done)
         taken_by[i] = std::move(taken);
         if (i == 0 && need_end) {  // the kernel's end (its event): direct tiles, timing
             if (g_trace) g_trace->mark('p', k);

@@ -89,7 +89,7 @@ static PyObject* new_attr(PyObject* tmpl, PyObject* kw, PyObject* ke, Py_ssize_t
     return d;
 }
 
-static PyObject* build(PyObject* self, PyObject* args) {
+static PyObject* build_impl(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *names, *ou, *ov, *ow, *oe, *shared = NULL;
     if (!PyArg_ParseTuple(args, "O!OOOO|O!", &PyList_Type, &names, &ou, &ov, &ow, &oe, &PyDict_Type, &shared))
@@ -484,7 +484,7 @@ static PyObject* int_of(PyObject** cache, long v) {
     return PyLong_FromLong(v);
 }
 
-static PyObject* build_overlap(PyObject* self, PyObject* args) {
+static PyObject* build_overlap_impl(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *names, *oc, *oa, *ob, *os, *oe, *ok = NULL, *oalive = NULL, *shared = NULL;
     if (!PyArg_ParseTuple(args, "O!OOOOO|OOO!", &PyList_Type, &names, &oc, &oa, &ob, &os, &oe, &ok, &oalive,
@@ -1040,7 +1040,7 @@ static void* replay_main(void* arg) {
     return NULL;
 }
 
-static PyObject* build_overlap_stream(PyObject* self, PyObject* args) {
+static PyObject* build_overlap_stream_impl(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *names, *oc, *oa, *ob, *os, *oe, *ok, *shared, *ooff, *oh, *ow;
     unsigned long long fn_addr;
@@ -1436,31 +1436,40 @@ done:
 // ----------------------------------------------------------------------------- pooled object arenas
 //
 // The graph's dicts (an attribute dict per edge, a row and a predecessor dict per node: ~2.3 M objects at the
-// target point, ~0.4 GB) come from CPython's object arenas (256 KiB each, one mmap per arena, unmapped when
-// empty).  Every call's dicts then land on pages the kernel must fault in and zero, 4 KiB at a time: ~2·10^5
-// minor faults in a process's first removal, ~1.2·10^5 in later ones (the previous graph's arenas were returned).
-// arena_pool() installs an arena allocator that carves arenas from 64 MiB regions aligned to 2 MiB and advised
-// for transparent huge pages, and keeps freed arenas on a free list for the next graph (never unmapped).  Installed
-// once per process, for the rest of it; an arena the previous allocator made goes back to it.
+// target point, ~0.4 GB) come from CPython's object arenas (256 KiB each, one mmap per arena).  Fresh arenas land on
+// pages the kernel must fault in and zero, 4 KiB at a time: ~2·10^5 minor faults in a process's first removal.
+// While a builder call runs (build, build_overlap, build_overlap_stream: pool_scope), an arena allocator carves
+// arenas from 64 MiB regions aligned to 2 MiB and advised for transparent huge pages (far fewer faults), and arenas
+// freed meanwhile go on a free list for the call's own later dicts.  The previous allocator is restored when the
+// call returns, so the pool touches nothing else in the process: the graph's arenas go back to the kernel by
+// CPython's own munmap when the graph is freed, and of the free list at most kPoolKeep arenas stay mapped for the
+// next call (the rest are unmapped).  OVL_ARENA_POOL=0: builder calls keep CPython's allocator.
 #include <sys/mman.h>
 
 #define OVL_POOL_REGION (64u << 20)
 #define OVL_POOL_MAX_REGIONS 1024
+#define OVL_POOL_KEEP 256  // freed arenas kept mapped across builder calls (64 MiB of 256 KiB arenas)
 
 static PyObjectArenaAllocator g_prev_arena;
-static int g_pool_on = 0;
+static int g_pool_enabled = -1;   // OVL_ARENA_POOL (read once): 0 off, else on
+static int g_pool_depth = 0;      // builder calls in progress (the allocator is installed while > 0)
 static void* g_pool_free = NULL;  // freed pool arenas, linked through their first word
+static size_t g_pool_nfree = 0;
 static char* g_pool_cur = NULL;
 static size_t g_pool_left = 0;
 static size_t g_pool_arena = 0;  // the arena size CPython asks for (the first request's)
-static char* g_region_base[OVL_POOL_MAX_REGIONS];
+static char* g_region_base[OVL_POOL_MAX_REGIONS];  // ascending
 static int g_regions = 0;
-static size_t g_pool_mapped = 0, g_pool_reused = 0;
+static size_t g_pool_mapped = 0, g_pool_reused = 0, g_pool_released = 0;
 
-static int pool_owns(const void* p) {
-    for (int i = 0; i < g_regions; ++i)
-        if ((const char*)p >= g_region_base[i] && (const char*)p < g_region_base[i] + OVL_POOL_REGION) return 1;
-    return 0;
+static int pool_owns(const void* p) {  // (binary search over the ascending region bases)
+    int lo = 0, hi = g_regions;
+    while (lo < hi) {
+        const int mid = (lo + hi) / 2;
+        if ((const char*)p < g_region_base[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo > 0 && (const char*)p < g_region_base[lo - 1] + OVL_POOL_REGION;
 }
 
 static void* pool_arena_alloc(void* ctx, size_t size) {
@@ -1470,6 +1479,7 @@ static void* pool_arena_alloc(void* ctx, size_t size) {
     if (g_pool_free) {
         void* p = g_pool_free;
         g_pool_free = *(void**)p;
+        --g_pool_nfree;
         ++g_pool_reused;
         return p;
     }
@@ -1485,7 +1495,9 @@ static void* pool_arena_alloc(void* ctx, size_t size) {
 #ifdef MADV_HUGEPAGE
         madvise(a, OVL_POOL_REGION, MADV_HUGEPAGE);
 #endif
-        g_region_base[g_regions++] = a;
+        int i = g_regions++;
+        for (; i > 0 && g_region_base[i - 1] > a; --i) g_region_base[i] = g_region_base[i - 1];
+        g_region_base[i] = a;
         g_pool_cur = a;
         g_pool_left = OVL_POOL_REGION;
         g_pool_mapped += OVL_POOL_REGION;
@@ -1501,28 +1513,75 @@ static void pool_arena_free(void* ctx, void* p, size_t size) {
     if (p && size == g_pool_arena && pool_owns(p)) {
         *(void**)p = g_pool_free;
         g_pool_free = p;
+        ++g_pool_nfree;
         return;
     }
     g_prev_arena.free(g_prev_arena.ctx, p, size);
 }
 
+// a builder call's start / end (with the GIL held): install the pool / trim its free list and restore CPython's
+static void pool_begin(void) {
+    if (g_pool_enabled < 0) {
+        const char* e = getenv("OVL_ARENA_POOL");
+        g_pool_enabled = !(e && !strcmp(e, "0"));
+    }
+    if (!g_pool_enabled || g_pool_depth++ > 0) return;
+    PyObjectArenaAllocator mine = {NULL, pool_arena_alloc, pool_arena_free};
+    PyObject_GetArenaAllocator(&g_prev_arena);
+    PyObject_SetArenaAllocator(&mine);
+}
+
+static void pool_end(void) {
+    if (!g_pool_enabled || g_pool_depth == 0 || --g_pool_depth > 0) return;
+    void* keep = NULL;
+    void** tail = &keep;
+    size_t kept = 0;
+    for (void* p = g_pool_free; p;) {
+        void* next = *(void**)p;
+        if (kept < OVL_POOL_KEEP) {
+            *tail = p;
+            tail = (void**)p;
+            ++kept;
+        } else {
+            munmap(p, g_pool_arena);  // (its addresses are never handed out again: off the list, below g_pool_cur)
+            ++g_pool_released;
+        }
+        p = next;
+    }
+    *tail = NULL;
+    g_pool_free = keep;
+    g_pool_nfree = kept;
+    PyObject_SetArenaAllocator(&g_prev_arena);
+}
+
+// stats (tests): {on: installed now, enabled, arena_bytes, mapped_bytes, reused_arenas, kept_arenas, released_arenas}
 static PyObject* arena_pool(PyObject* self, PyObject* args) {
     (void)self;
-    int on = 1;
-    if (!PyArg_ParseTuple(args, "|p", &on)) return NULL;
-    if (on && !g_pool_on) {
-        PyObjectArenaAllocator mine = {NULL, pool_arena_alloc, pool_arena_free};
-        PyObject_GetArenaAllocator(&g_prev_arena);
-        PyObject_SetArenaAllocator(&mine);
-        g_pool_on = 1;
-    }
-    return Py_BuildValue("{s:i,s:n,s:n,s:n}", "on", g_pool_on, "arena_bytes", (Py_ssize_t)g_pool_arena,
-                         "mapped_bytes", (Py_ssize_t)g_pool_mapped, "reused_arenas", (Py_ssize_t)g_pool_reused);
+    (void)args;
+    return Py_BuildValue("{s:i,s:i,s:n,s:n,s:n,s:n,s:n}", "on", g_pool_depth > 0 ? 1 : 0, "enabled", g_pool_enabled,
+                         "arena_bytes", (Py_ssize_t)g_pool_arena, "mapped_bytes", (Py_ssize_t)g_pool_mapped,
+                         "reused_arenas", (Py_ssize_t)g_pool_reused, "kept_arenas", (Py_ssize_t)g_pool_nfree,
+                         "released_arenas", (Py_ssize_t)g_pool_released);
 }
+
+// the builder entry points, each inside a pool scope
+static PyObject* build_impl(PyObject* self, PyObject* args);
+static PyObject* build_overlap_impl(PyObject* self, PyObject* args);
+static PyObject* build_overlap_stream_impl(PyObject* self, PyObject* args);
+#define OVL_POOL_SCOPED(name)                                  \
+    static PyObject* name(PyObject* self, PyObject* args) {    \
+        pool_begin();                                          \
+        PyObject* r = name##_impl(self, args);                 \
+        pool_end();                                            \
+        return r;                                              \
+    }
+OVL_POOL_SCOPED(build)
+OVL_POOL_SCOPED(build_overlap)
+OVL_POOL_SCOPED(build_overlap_stream)
 
 static PyMethodDef methods[] = {
     {"arena_pool", arena_pool, METH_VARARGS,
-     "arena_pool([on]) -> stats: install the pooled, huge-page-advised object arena allocator (once per process)"},
+     "arena_pool() -> stats of the pooled, huge-page-advised object arenas builder calls allocate from"},
     {"overlap_csr", overlap_csr, METH_VARARGS,
      "overlap_csr(counts, a, b, score[, keep]) -> (off int64, heads int32, weights int64) bytearrays"},
     {"build_overlap_stream", build_overlap_stream, METH_VARARGS,

@@ -63,11 +63,11 @@ struct ResidentCall {
     int32_t* out_e = nullptr;
 };
 
-// Host memory the grid writes and the host reads (ring, status): fine-grained (coherent), so the grid's stores --
-// system-scope (sc0 sc1) write-through stores, none kept in the XCD's L2 -- invalidate the lines host threads poll.
-// (Non-temporal stores stayed in the L2 until the grid left; the uncached kind, MTYPE_UC, is not snooped: host
-// threads polled stale copies in their caches.)
-constexpr unsigned kRingMem = hipHostMallocPortable | hipHostMallocCoherent;
+// Host memory the grid writes and the host reads (ring, status): uncached (MTYPE_UC), so the XCD's L2 keeps none of
+// the grid's stores (into the coherent kind, non-temporal record stores stayed in the L2 until the grid left, and
+// write-through 8-byte stores cost 0.23 against 0.14 ms at N = 1); the host's polls see them land (the stores
+// still invalidate the host's cached copies).
+constexpr unsigned kRingMem = hipHostMallocPortable | hipHostMallocUncached;
 // The mailbox, which the host writes and the grid's block 0 polls: uncached (MTYPE_UC), so no XCD's L2 serves the
 // poll an old copy of the request word (with the coherent kind a polled copy stayed in the L2 for 20 ms and more),
 // and, since the grid's reads of it do not snoop the host's caches, the host writes its lines back to memory

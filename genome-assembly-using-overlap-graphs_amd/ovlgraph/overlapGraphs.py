@@ -193,11 +193,9 @@ def _digraph():
             spec = importlib.util.spec_from_file_location("ovlgraph._digraph", path)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
+            # (its builder calls take the graph's dicts from pooled, huge-page-advised object arenas while they run:
+            # csrc/ovl_digraph.c arena_pool; OVL_ARENA_POOL=0 leaves CPython's allocator)
             _digraph_mod = mod
-            # the graph's dicts from pooled, huge-page-advised object arenas kept across graphs
-            # (csrc/ovl_digraph.c arena_pool; OVL_ARENA_POOL=0 leaves CPython's allocator)
-            if os.environ.get("OVL_ARENA_POOL", "1") != "0":
-                mod.arena_pool(True)
     return _digraph_mod or None
 
 

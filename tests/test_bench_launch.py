@@ -40,13 +40,32 @@ def test_args_defaults():
         bench.parse_args(["--gpus", "0"])
 
 
-def _dry(n, *extra):
+def _dry(n, *extra, stderr=None):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--steps", "7", "--dry-run", *extra],
                        capture_output=True, text=True, timeout=240, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # one JSON line, from rank 0 only
+    if stderr is not None:
+        stderr.append(r.stderr)
     return json.loads(lines[0])
+
+
+def test_n2_stages_are_bounded_and_heard():
+    """the secondary N > 1 stages run under a time budget that every rank applies alike (the slowest
+    rank's elapsed time, all-reduced), later stages are recorded as skipped, and a heartbeat on rank 0's stderr
+    names the running stage while a long stage runs (two ranks over gloo; each stage sleeps 1.5 s, budget 2.5 s,
+    a heartbeat every 0.5 s)."""
+    err = []
+    got = _dry(2, "--dry-run-stage-s", "1.5", "--extra-budget", "2.5", "--heartbeat", "0.5", stderr=err)
+    plan = ["weak_scaling", "cfg4_strong", "cfg5_sharded_band_sweep", "single_process_all_gpus"]
+    ran = [k for k in plan if got[k] is None]
+    skipped = [k for k in plan if isinstance(got[k], dict) and "skipped" in got[k]]
+    assert ran == plan[:2] and skipped == plan[2:], got
+    assert "weak_scaling still running" in err[0] and "cfg4_strong done" in err[0], err[0][-2000:]
+    # no budget pressure: every stage runs
+    got = _dry(2, "--dry-run-stage-s", "0.2")
+    assert all(got[k] is None for k in plan)
 
 
 @pytest.mark.parametrize("n", [2, 3])

@@ -70,8 +70,18 @@ def test_resident_whole_list_call_after_call(oracle_mod, cfg):
             eng.score_candidates(out=out)
             np.testing.assert_array_equal(out[0], ref_s, err_msg=f"call {it}")
             np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
+        # (a gap between calls longer than the grid's idle deadline -- the checks above take ~20 ms at cfg3 -- lets
+        # it leave: the next call relaunches it; never a second launch otherwise)
         st = eng.resident_stats()
-        assert st["alive"] == 1 and st["launches"] == 1 and st["broken"] == 0, st
+        assert st["alive"] == 1 and st["launches"] == 1 + st["relaunches"] and st["broken"] == 0, st
+        # back to back, no gap: one grid serves every call (after the first, which may find it gone)
+        eng.score_candidates(out=out)
+        before = eng.resident_stats()["launches"]
+        for _ in range(20):
+            eng.score_candidates(out=out)
+        assert eng.resident_stats()["launches"] == before
+        np.testing.assert_array_equal(out[0], ref_s)
+        np.testing.assert_array_equal(out[1], ref_e)
         x = eng.last_transfer()
         assert x["record_pairs"] == n and x["result_bytes"] == 128 * ((n + 63) // 64) + 8 * x["escapes"], x
         if cfg == "target":
