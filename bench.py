@@ -454,8 +454,10 @@ def end_to_end(w: Workload, seed: int = 0):
     t3 = time.perf_counter()
     n_kept = L.number_of_edges()
     del L
-    # the same twice more on fresh lazy graphs: remove_cycles_s is the median of the three (one call's time moves
-    # with the box's host by +-10 %); every run is on the line
+    # the same twice more on fresh lazy graphs: remove_cycles_s is the process's first call (what a user's single
+    # graph build pays), remove_cycles_median_s the median of the three (one call's time moves with the box's host
+    # by +-10 %); every run is on the line.  (The builder's pooled arenas live only inside its calls, so no call
+    # reuses the memory of the one before: csrc/ovl_digraph.c arena_pool.)
     import gc
     runs = [(t3 - t2, rc_l)]
     for _ in range(2):
@@ -468,7 +470,8 @@ def end_to_end(w: Workload, seed: int = 0):
         assert L.number_of_edges() == n_kept
         del L
     gc.collect()
-    t_med, rc_l = sorted(runs, key=lambda x: x[0])[1]
+    t_first, rc_l = runs[0]
+    t_med = sorted(runs, key=lambda x: x[0])[1][0]
     # the same with the replay, then the dicts (OVL_CYCLES_STREAM=0), for comparison
     saved = og._STREAM_OFF
     og._STREAM_OFF = True
@@ -501,17 +504,19 @@ def end_to_end(w: Workload, seed: int = 0):
             "dedup_enumerate_score_stages_s": {k: round(v, 5) for k, v in stages.items()},
             "dedup_enumerate_score_first_stages_s": {k: round(v, 5) for k, v in cold.items()},
             "construct_s": round(t2 - t0, 4),
-            "remove_cycles_s": round(t_med, 4),
+            "remove_cycles_s": round(t_first, 4),
+            "remove_cycles_median_s": round(t_med, 4),
             "remove_cycles_runs_s": [round(x[0], 4) for x in runs],
             "remove_cycles_stages_s": {k: round(rc_l[k], 4) for k in ("csr", "replay", "remove")},
             "remove_cycles_overlapped": bool(rc_l.get("overlapped")),
-            "construct_plus_remove_cycles_s": round(t2 - t0 + t_med, 4),
+            "construct_plus_remove_cycles_s": round(t2 - t0 + t_first, 4),
             "remove_cycles_serial_s": round(ts1 - ts0, 4),
             "remove_cycles_serial_stages_s": {k: round(rc_s[k], 4) for k in ("csr", "replay", "remove")},
             "what": "construct_s: overlap_edges_k + the lazy DiGraph (dicts built on first use); remove_cycles_s: "
                     "on that graph, CSR from the columns, then the replay with the surviving edges' dicts built "
                     "while it runs (stage 'replay' holds both; remove_cycles_serial_s: replay, then the dicts) -- "
-                    "the median of three calls on fresh lazy graphs, remove_cycles_runs_s in call order",
+                    "the process's first call; remove_cycles_median_s: the median of three calls on fresh lazy "
+                    "graphs, remove_cycles_runs_s in call order; construct_plus_remove_cycles_s: both first calls",
             "eager": {"digraph_direct_s": round(t5 - t4, 4), "digraph_networkx_s": round(t6 - t5, 4),
                       "remove_cycles_s": round(t8 - t7, 4),
                       "remove_cycles_stages_s": {k: round(rc_e[k], 4) for k in ("csr", "replay", "remove")}}}

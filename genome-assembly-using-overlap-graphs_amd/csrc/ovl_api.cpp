@@ -115,6 +115,8 @@ struct Knobs {
     int64_t resident_min = 1;
     int64_t resident_max = int64_t(1) << 40;
     int32_t resident_blocks = 2;  // the grid's blocks of 256 threads per CU
+    int32_t resident_pf = 1;      // its tiles software-pipelined (fewer, fatter wavefronts) or one at a time
+    int32_t resident_sleep = 4;   // its non-lead blocks' pause between polls (~0.1 us units)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -785,9 +787,15 @@ Knobs read_knobs() {
         k.lane_h2 = (v >> 2) & 1;
     }
     if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
-    if (const char* e = getenv("OVL_RESIDENT")) {  // mode[,blocks per CU] (also "1x4")
+    if (const char* e = getenv("OVL_RESIDENT")) {  // mode[,blocks per CU[,pipelined[,poll sleep]]] ("1x2x1x4")
         k.resident = std::max(0, std::min(2, atoi(e)));
-        if (const char* c = strpbrk(e, ",x")) k.resident_blocks = std::max(1, std::min(8, atoi(c + 1)));
+        if (const char* c = strpbrk(e, ",x")) {
+            k.resident_blocks = std::max(1, std::min(8, atoi(c + 1)));
+            if (const char* c2 = strpbrk(c + 1, ",x")) {
+                k.resident_pf = atoi(c2 + 1) != 0;
+                if (const char* c3 = strpbrk(c2 + 1, ",x")) k.resident_sleep = std::max(0, std::min(1000, atoi(c3 + 1)));
+            }
+        }
     }
     if (const char* e = getenv("OVL_PACK_MIN")) k.pack_min = std::max(0LL, atoll(e));
     if (const char* e = getenv("OVL_PACK_DIRECT_PCT")) {
@@ -873,6 +881,8 @@ hipError_t init_dev(Dev* d) {
     d->res.device = d->device;
     d->res.cu_count = d->cu_count;
     d->res.blocks_per_cu = d->k.resident_blocks;
+    d->res.pipelined = d->k.resident_pf;
+    d->res.poll_sleep = d->k.resident_sleep;
     for (hipStream_t* s : {&d->stream, &d->s_in}) {
         e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
         if (e != hipSuccess) return e;

@@ -48,6 +48,10 @@ struct OvlResidentArgs {
     uint32_t seq_base;          // the last request already served (the grid serves the next one on)
     uint64_t idle_ticks;        // block 0 leaves after this many wall-clock ticks without a request
     uint64_t* status;           // pinned words the grid writes when it leaves (why, its last request; trace)
+    uint32_t poll_sleep;        // the other blocks' pause between polls of the forward word, in ~0.1 us units
+    int32_t pipelined;          // tiles software-pipelined in fewer, fatter wavefronts (else one at a time)
+    uint64_t* tbuf;             // trace (or null): 4 words per wavefront (knew the request, last tile done, records
+                                // written back, request seq), then block 0's clock when it saw the request
     int32_t blocks;
 };
 constexpr uint32_t kResidentLeave = 0xFFFFFFFFu;

@@ -109,7 +109,8 @@ __device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
 }
 
 // OM 3: streamed tile records.  A 64-pair tile's results as one 128-byte record at out_score + 32 * tile
-// (dwords), which host threads read while the kernel still runs (ovl_expand.h rec_tile_ready / expand_rec):
+// (dwords), which host threads read while the kernel still runs (ovl_expand.h rec_tile_ready_scalar /
+// rec_tile_scalar / rec_tile_avx512):
 //   dword w (w < 32) = phase << 31 | c[w + 32] << 15 | c[w]   (c[l]: lane l's 15-bit code)
 // The phase bit (the host flips it each time it reuses the staging slot) tells the host which dwords this
 // launch has written: every dword is one aligned 32-bit store, so a dword whose phase bit is the launch's
@@ -1159,10 +1160,12 @@ __global__ __launch_bounds__(256) void general_kernel(
 // ----------------------------------------------------------------------------- resident grid
 
 // One tile's results as a ring record (ovl_grid.h OvlResidentBody): put_tile_rec's codes, the phase bit of the ring
-// lap, and a special pair's word as one 8-byte store {payload, seq} (payload: put_tile_rec's special word).  The ring
-// is uncached host memory (MTYPE_UC, ovl_resident.h): the XCD's L2 keeps none of these stores -- into the coherent
-// kind a resident grid's non-temporal stores stayed in the L2 until the grid left -- and the record goes out as one
-// 128-byte line (32 lanes x 4 bytes; as 16 system-scope 8-byte stores it took 0.23 ms at N = 1 against 0.14).
+// lap, and a special pair's word as one 8-byte store {payload, seq} (payload: put_tile_rec's special word).  The
+// stores are non-temporal 128-byte lines into fine-grained host memory, which the XCD's L2 keeps (write-back) until
+// the wavefront's release fence after its last tile of the request (resident_kernel): a resident grid never reaches
+// the end-of-kernel write-back.  (Measured against the alternatives, target point, N = 8 / N = 1 shards: write-through
+// 16-byte sc1 stores 0.056 / 0.326 ms, 8-byte system-scope stores 0.071 / 0.344, non-temporal stores into uncached
+// (MTYPE_UC) memory 0.062 / 0.340, this form 0.049 / 0.223; profiles/r06_resident_store_ab.json.)
 __device__ __forceinline__ void put_ring_rec(uint32_t* rec, uint64_t* sp, int64_t ri, uint32_t phase, uint32_t seq,
                                              bool mine, int32_t sc, int32_t en, int32_t n, int32_t match, float inv,
                                              int lane) {
@@ -1189,34 +1192,61 @@ __device__ __forceinline__ void put_ring_rec(uint32_t* rec, uint64_t* sp, int64_
 
 // One 64-pair tile of a resident request: uniform_kernel's throughput-mode sweep with every pair in it (TT: reads
 // b cut at the genome end snapshot their block maxima, shorter reads a add their window keys), into the ring.
+// Split in stages so a wavefront can have the next tiles' loads in flight during a sweep (resident_kernel):
+// the indices (ResIdx), then the rows and lengths they select (ResRows), then the sweep (resident_sweep).
+struct ResIdx {
+    int32_t a, b;
+    bool mine, ok;
+};
 template <int W>
-__device__ __forceinline__ void resident_tile(int64_t tile, const OvlResidentBody& q, const uint32_t* __restrict__ sfx,
-                                              const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
-                                              int32_t n_reads, int32_t lw, const uint32_t* __restrict__ full,
-                                              int32_t match, int32_t mismatch, int lane) {
-    constexpr int P = 2;
-    constexpr int SROW = (W * P + 3) & ~3;
-    constexpr int TROW = (W * P + 3) & ~3;
+struct ResRows {
+    uint32_t Sw[(W * 2 + 3) & ~3], Tw[(W * 2 + 3) & ~3];
+    uint32_t fw;  // read a's word of the length bitmap
+    int32_t la, lb;
+};
+
+__device__ __forceinline__ ResIdx resident_idx(int64_t tile, const OvlResidentBody& q, int32_t n_reads, int lane) {
+    ResIdx x;
     const int64_t p = tile * 64 + lane;
-    const bool mine = p < q.n_pairs;
-    int32_t a = mine ? q.a_idx[p] : 0;
-    int32_t b = mine ? q.b_idx[p] : 0;
-    const bool ok = mine && a >= 0 && a < n_reads && b >= 0 && b < n_reads;
-    if (!ok) { a = 0; b = 0; }
-    uint32_t Sw[SROW], Tw[TROW];
-    load_words<SROW>(sfx + (int64_t)a * SROW, Sw);
-    load_words<TROW>(pfx + (int64_t)b * TROW, Tw);
-    const bool fa = ok && ((full[a >> 5] >> (a & 31)) & 1u);
-    const int32_t mb = len[b];
+    x.mine = tile >= 0 && p < q.n_pairs;
+    x.a = x.mine ? q.a_idx[p] : 0;
+    x.b = x.mine ? q.b_idx[p] : 0;
+    x.ok = x.mine && x.a >= 0 && x.a < n_reads && x.b >= 0 && x.b < n_reads;
+    if (!x.ok) {
+        x.a = 0;
+        x.b = 0;
+    }
+    return x;
+}
+
+template <int W>
+__device__ __forceinline__ void resident_rows(const ResIdx& x, ResRows<W>& r, const uint32_t* __restrict__ sfx,
+                                              const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
+                                              const uint32_t* __restrict__ full) {
+    constexpr int SROW = (W * 2 + 3) & ~3;
+    load_words<SROW>(sfx + (int64_t)x.a * SROW, r.Sw);
+    load_words<SROW>(pfx + (int64_t)x.b * SROW, r.Tw);
+    r.fw = full[x.a >> 5];
+    r.la = len[x.a];
+    r.lb = len[x.b];
+}
+
+template <int W>
+__device__ __forceinline__ void resident_sweep(int64_t tile, const ResIdx& x, const ResRows<W>& r,
+                                               const OvlResidentBody& q, int32_t lw, int32_t match, int32_t mismatch,
+                                               int lane) {
+    const bool ok = x.ok;
+    const bool fa = ok && ((r.fw >> (x.a & 31)) & 1u);
+    const int32_t mb = r.lb;
     int32_t na = lw;
-    if (ok && !fa) na = len[a];
+    if (ok && !fa) na = r.la;
     const bool uni = fa && mb == lw;
     const bool tt = ok && !uni;
     const int32_t tm = tt ? (na < mb ? na : mb) : -1;
     uint32_t tmask = 0;
     for (uint64_t bm = __ballot(tt); bm; bm &= bm - 1)
         tmask |= 1u << (__builtin_amdgcn_readlane(tm, (int)__builtin_ctzll(bm)) & 31);
-    int32_t best = sweep_uniform<W, 0>(Sw, Tw, lw, match, mismatch - match, 0u, 32u, tmask, tm);
+    int32_t best = sweep_uniform<W, 0>(r.Sw, r.Tw, lw, match, mismatch - match, 0u, 32u, tmask, tm);
     const bool win = tt && na < mb;
     uint64_t wm = __ballot(win);
     if (wm) {
@@ -1226,7 +1256,7 @@ __device__ __forceinline__ void resident_tile(int64_t tile, const OvlResidentBod
             jlo = min(jlo, __builtin_amdgcn_readlane(na, l) + 1);
             jhi = max(jhi, __builtin_amdgcn_readlane(mb, l));
         }
-        const int32_t wk = window_keys<W>(Sw, Tw, na, mb, jlo, jhi, match, mismatch - match);
+        const int32_t wk = window_keys<W>(r.Sw, r.Tw, na, mb, jlo, jhi, match, mismatch - match);
         if (win && wk > best) best = wk;
     }
     int32_t sc, en;
@@ -1234,7 +1264,7 @@ __device__ __forceinline__ void resident_tile(int64_t tile, const OvlResidentBod
     const int64_t g = q.pos + tile;
     const int64_t ri = g & ((int64_t(1) << q.ring_log2) - 1);
     const uint32_t phase = (uint32_t)((g >> q.ring_log2) + 1) & 1u;
-    put_ring_rec(q.rec, q.sp, ri, phase, (uint32_t)q.seq, mine, ok ? sc : -1, ok ? en : -1, na, match,
+    put_ring_rec(q.rec, q.sp, ri, phase, (uint32_t)q.seq, x.mine, ok ? sc : -1, ok ? en : -1, na, match,
                  pack_inv(match, mismatch), lane);
 }
 
@@ -1251,12 +1281,15 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // uniform_kernel orders them).  No fan-in, no fence: nothing is waited for on the device.
 //   Every wait is bounded: block 0 leaves (and tells the others) after idle_ticks without a request; the other
 // blocks leave after twice that without a new forward, so a grid whose block 0 never ran still ends.
-template <int W>
-__global__ __launch_bounds__(256, (W >= 7 ? 2 : 4)) void resident_kernel(
+// PF: tiles software-pipelined (fewer, fatter wavefronts: 2-4 per SIMD) or one tile at a time (UNI_OCC(W, 0)
+// wavefronts per SIMD, uniform_kernel's register budget)
+#define RES_OCC(W, PF) ((PF) ? ((W) >= 3 ? 2 : 4) : UNI_OCC(W, 0))
+template <int W, bool PF>
+__global__ __launch_bounds__(256, RES_OCC(W, PF)) void resident_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
     int32_t n_reads, int32_t lw, const uint32_t* __restrict__ full, const uint8_t* __restrict__ tile_flags,
     const OvlResidentCtl* mailbox, uint32_t* fwd, OvlResidentBody* dslot, uint32_t seq_base, uint64_t idle_ticks,
-    uint64_t* status) {
+    uint64_t* status, uint32_t poll_sleep, uint64_t* tbuf) {
     __shared__ uint64_t s_body[kResidentBodyWords];
     __shared__ int s_go;
     const int lane = threadIdx.x & 63;
@@ -1312,6 +1345,7 @@ __global__ __launch_bounds__(256, (W >= 7 ? 2 : 4)) void resident_kernel(
                     vm_drain();
                     __hip_atomic_store(fwd, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     last = seq;
+                    if (tbuf) __builtin_nontemporal_store(wall_clock64(), tbuf + 4 * (int64_t)gridDim.x * 4);
                 } else {
                     __hip_atomic_store(fwd, kResidentLeave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
@@ -1338,7 +1372,7 @@ __global__ __launch_bounds__(256, (W >= 7 ? 2 : 4)) void resident_kernel(
                         }
                     }
                     if (wall_clock64() > t_end) break;
-                    __builtin_amdgcn_s_sleep(2);
+                    for (uint32_t z = 0; z < poll_sleep; ++z) __builtin_amdgcn_s_sleep(4);  // (~0.1 us each)
                 }
                 if (!go && status)  // (a block that left on its own deadline, not told to)
                     if (__hip_atomic_load(fwd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kResidentLeave)
@@ -1353,6 +1387,9 @@ __global__ __launch_bounds__(256, (W >= 7 ? 2 : 4)) void resident_kernel(
         }
         __syncthreads();
         if (!s_go) return;
+        // (trace, OVL_TRACE_PIPE: per wavefront the wall clock when it knew the request, finished its last tile
+        // and had its records written back; block 0 stored when it saw the request)
+        if (tbuf && lane == 0) __builtin_nontemporal_store(wall_clock64(), tbuf + 4 * wave);
         OvlResidentBody q;  // (wave-uniform: scalar registers, as kernel arguments would be)
         {
             uint64_t* d = reinterpret_cast<uint64_t*>(&q);
@@ -1368,17 +1405,64 @@ __global__ __launch_bounds__(256, (W >= 7 ? 2 : 4)) void resident_kernel(
         const int64_t n_tiles = (q.n_pairs + 63) >> 6;
         const bool hf = q.heavy_ids != nullptr && q.heavy_n > 0;
         const int64_t n_items = hf ? n_tiles + q.heavy_n : n_tiles;
-        for (int64_t item = wave; item < n_items; item += n_waves) {  // (wave-uniform)
-            int64_t tile = item;
-            if (hf) {
-                if (item < q.heavy_n) {
-                    tile = (int64_t)q.heavy_ids[item] - q.tile_base;
-                } else {
-                    tile = item - q.heavy_n;
-                    if (tile_flags[q.tile_base + tile]) continue;  // done among the heavy ones
+        // The wave's items w, w + waves, ... (heavy tiles first, as uniform_kernel orders them; an item whose tile
+        // was done among the heavy ones is skipped): item -> tile, or -1 past the last.  Software-pipelined: while
+        // tile i sweeps, the rows of tile i + 1 and the indices of tile i + 2 are in flight (a resident grid runs
+        // a few wavefronts per SIMD, too few to hide a tile's two dependent loads by switching waves).
+        if constexpr (!PF) {
+            for (int64_t item = wave; item < n_items; item += n_waves) {  // (wave-uniform)
+                int64_t tile = item;
+                if (hf) {
+                    if (item < q.heavy_n) {
+                        tile = (int64_t)q.heavy_ids[item] - q.tile_base;
+                    } else {
+                        tile = item - q.heavy_n;
+                        if (tile_flags[q.tile_base + tile]) continue;  // done among the heavy ones
+                    }
                 }
+                const ResIdx x = resident_idx(tile, q, n_reads, lane);
+                ResRows<W> r;
+                resident_rows<W>(x, r, sfx, pfx, len, full);
+                resident_sweep<W>(tile, x, r, q, lw, match, mismatch, lane);
             }
-            resident_tile<W>(tile, q, sfx, pfx, len, n_reads, lw, full, match, mismatch, lane);
+        }
+        int64_t item = PF ? wave : n_items;
+        const auto next_tile = [&]() -> int64_t {  // (wave-uniform; leaves `item` on the tile's item)
+            for (; item < n_items; item += n_waves) {
+                if (!hf) return item;
+                if (item < q.heavy_n) return (int64_t)q.heavy_ids[item] - q.tile_base;
+                const int64_t t = item - q.heavy_n;
+                if (!tile_flags[q.tile_base + t]) return t;
+            }
+            return -1;
+        };
+        int64_t t0 = next_tile();
+        ResIdx x0 = resident_idx(t0, q, n_reads, lane);
+        ResRows<W> r0;
+        if (t0 >= 0) resident_rows<W>(x0, r0, sfx, pfx, len, full);
+        item += n_waves;
+        int64_t t1 = t0 >= 0 ? next_tile() : -1;
+        ResIdx x1 = resident_idx(t1, q, n_reads, lane);
+        while (t0 >= 0) {
+            ResRows<W> r1;
+            if (t1 >= 0) resident_rows<W>(x1, r1, sfx, pfx, len, full);
+            item += n_waves;
+            const int64_t t2 = t1 >= 0 ? next_tile() : -1;
+            const ResIdx x2 = resident_idx(t2, q, n_reads, lane);
+            resident_sweep<W>(t0, x0, r0, q, lw, match, mismatch, lane);
+            t0 = t1;
+            x0 = x1;
+            r0 = r1;
+            t1 = t2;
+            x1 = x2;
+        }
+        // this wavefront's records out of the XCD's L2 (system-scope release: an L2 write-back)
+        if (tbuf && lane == 0) __builtin_nontemporal_store(wall_clock64(), tbuf + 4 * wave + 1);
+        if (wave < n_items) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (tbuf && lane == 0) {
+            __hip_atomic_store(tbuf + 4 * wave + 2, (uint64_t)wall_clock64(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(tbuf + 4 * wave + 3, q.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();  // (thread 0 rewrites s_body for the next request)
     }
@@ -1389,9 +1473,16 @@ extern "C" hipError_t ovl_launch_resident(const OvlResidentArgs* g, hipStream_t 
     const dim3 grid((unsigned)g->blocks), block(256);
 #define OVL_RESIDENT_CASE(Wc)                                                                                       \
     case Wc:                                                                                                        \
-        resident_kernel<Wc><<<grid, block, 0, stream>>>(g->sfx, g->pfx, g->len, g->n_reads, g->lw, g->full,         \
-                                                        g->tile_flags, g->mailbox, g->fwd, g->dslot, g->seq_base,   \
-                                                        g->idle_ticks, g->status);                                  \
+        if (g->pipelined)                                                                                           \
+            resident_kernel<Wc, true><<<grid, block, 0, stream>>>(g->sfx, g->pfx, g->len, g->n_reads, g->lw,        \
+                                                                  g->full, g->tile_flags, g->mailbox, g->fwd,       \
+                                                                  g->dslot, g->seq_base, g->idle_ticks, g->status,  \
+                                                                  g->poll_sleep, g->tbuf);                          \
+        else                                                                                                        \
+            resident_kernel<Wc, false><<<grid, block, 0, stream>>>(g->sfx, g->pfx, g->len, g->n_reads, g->lw,       \
+                                                                   g->full, g->tile_flags, g->mailbox, g->fwd,      \
+                                                                   g->dslot, g->seq_base, g->idle_ticks, g->status, \
+                                                                   g->poll_sleep, g->tbuf);                         \
         break;
     switch (g->wmax) {
         OVL_RESIDENT_CASE(1)

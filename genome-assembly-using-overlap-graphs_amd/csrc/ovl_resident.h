@@ -63,11 +63,9 @@ struct ResidentCall {
     int32_t* out_e = nullptr;
 };
 
-// Host memory the grid writes and the host reads (ring, status): uncached (MTYPE_UC), so the XCD's L2 keeps none of
-// the grid's stores (into the coherent kind, non-temporal record stores stayed in the L2 until the grid left, and
-// write-through 8-byte stores cost 0.23 against 0.14 ms at N = 1); the host's polls see them land (the stores
-// still invalidate the host's cached copies).
-constexpr unsigned kRingMem = hipHostMallocPortable | hipHostMallocUncached;
+// Host memory the grid writes and the host reads (ring, status): fine-grained (coherent), so the grid's stores, once
+// written back from the L2 (resident_kernel's release fence), invalidate the lines host threads poll.
+constexpr unsigned kRingMem = hipHostMallocPortable | hipHostMallocCoherent;
 // The mailbox, which the host writes and the grid's block 0 polls: uncached (MTYPE_UC), so no XCD's L2 serves the
 // poll an old copy of the request word (with the coherent kind a polled copy stayed in the L2 for 20 ms and more),
 // and, since the grid's reads of it do not snoop the host's caches, the host writes its lines back to memory
@@ -108,6 +106,8 @@ class ResidentGrid {
     int32_t device = 0;
     int32_t cu_count = 256;
     int32_t blocks_per_cu = 2;
+    int32_t poll_sleep = 4;     // the non-lead blocks' pause between polls (~0.1 us units)
+    int32_t pipelined = 1;      // resident_kernel's PF form (tiles software-pipelined) or one tile at a time
     int64_t idle_us = 20000;     // the grid leaves after this long without a request
     int64_t call_limit_us = 2000000;
     bool broken = false;         // a failed call disabled the resident path of this device
@@ -140,6 +140,9 @@ class ResidentGrid {
         if (mb_) (void)hipHostFree(mb_);
         if (st_h_) (void)hipHostFree(st_h_);
         st_h_ = nullptr;
+        if (tb_h_) (void)hipHostFree(tb_h_);
+        tb_h_ = nullptr;
+        tb_cap_ = 0;
         if (dev_) (void)hipFree(dev_);
         if (ev_) (void)hipEventDestroy(ev_);
         if (ps_) (void)hipStreamDestroy(ps_);
@@ -206,6 +209,8 @@ class ResidentGrid {
     uint32_t* rec_d_ = nullptr;
     uint64_t* sp_h_ = nullptr;
     uint64_t* sp_d_ = nullptr;
+    uint64_t* tb_h_ = nullptr;            // the grid's trace (OvlResidentArgs::tbuf), pinned; OVL_TRACE_PIPE only
+    int64_t tb_waves_ = 0, tb_cap_ = 0;
     uint64_t* st_h_ = nullptr;            // the grid's exit status (OvlResidentArgs::status), pinned
     uint64_t* st_d_ = nullptr;
     int32_t ring_log2_ = -1;
@@ -257,13 +262,16 @@ class ResidentGrid {
         flush_lines(&mb_->ctl, sizeof(uint64_t));
     }
 
-    // OVL_TRACE_PIPE=1: why the grid left (its status words), on stderr
-    void trace_exit(const char* what, uint32_t s) const {
+    static bool trace_on() {
         static const bool on = [] {
             const char* v = getenv("OVL_TRACE_PIPE");
             return v && atoi(v) != 0;
         }();
-        if (!on || !st_h_) return;
+        return on;
+    }
+    // OVL_TRACE_PIPE=1: why the grid left (its status words), on stderr
+    void trace_exit(const char* what, uint32_t s) const {
+        if (!trace_on() || !st_h_) return;
         const volatile uint64_t* st = st_h_;
         fprintf(stderr, "ovl_resident: %s at request %u: block 0 left (1 asked, 2 idle, 3 body) %llu, its last %llu, "
                         "ctl seq %llu, body seq %llu, idle ticks %llu, a block on its own deadline %llu\n",
@@ -345,7 +353,26 @@ class ResidentGrid {
         a.idle_ticks = (uint64_t)std::max<int64_t>(1, idle_us) * (uint64_t)clk_khz / 1000u;
         memset(st_h_, 0, 64);  // (no grid runs: the stream's previous one has ended)
         a.status = st_d_;
+        a.poll_sleep = (uint32_t)std::max(0, poll_sleep);
+        a.pipelined = pipelined;
         a.blocks = std::max(1, cu_count * std::max(1, blocks_per_cu));
+        // (trace: 4 words per wavefront of the grid, then block 0's word at 16 * blocks -- sized from the grid
+        // launched here, reallocated when a grid has more wavefronts than the buffer holds)
+        a.tbuf = nullptr;
+        if (trace_on()) {
+            const int64_t need = 16 * (int64_t)a.blocks + 8;
+            if (tb_cap_ < need) {
+                if (tb_h_) (void)hipHostFree(tb_h_);
+                tb_h_ = nullptr;
+                tb_cap_ = 0;
+                if (hipHostMalloc((void**)&tb_h_, (size_t)need * sizeof(uint64_t), kRingMem) == hipSuccess) {
+                    memset(tb_h_, 0, (size_t)need * sizeof(uint64_t));
+                    tb_cap_ = need;
+                }
+            }
+            if (tb_h_ && hipHostGetDevicePointer((void**)&a.tbuf, tb_h_, 0) != hipSuccess) a.tbuf = nullptr;
+            tb_waves_ = 4 * (int64_t)a.blocks;
+        }
         if ((e = ovl_launch_resident(&a, ps_)) != hipSuccess) return e;
         if ((e = hipEventRecord(ev_, ps_)) != hipSuccess) return e;
         launched_ = rd;
@@ -372,6 +399,8 @@ class ResidentGrid {
         std::atomic<int> state{0};  // 0 running, 2 failed
         std::atomic<int64_t> left{nt}, bad{0}, specials{0};
         const auto t0 = std::chrono::steady_clock::now();
+        std::atomic<int64_t> t_first{-1};  // (trace: ns from the post to the first record taken, then to the
+        std::atomic<int64_t> t_half{-1}, t_90{-1}, t_99{-1};  // moments half, 90 % and 99 % of the tiles were taken)
         int relaunches = 0;
         hipError_t herr = hipSuccess;
         // one check of the call's progress: false ends the part (the call failed).  The calling thread (part 0) also
@@ -445,7 +474,21 @@ class ResidentGrid {
                 for (; x < pend.size(); ++x) pend[keep++] = pend[x];
                 pend.resize(keep);
                 if (took) {
-                    left.fetch_sub((int64_t)took, std::memory_order_relaxed);
+                    if (trace_on() && t_first.load(std::memory_order_relaxed) < 0) {
+                        int64_t none = -1;
+                        t_first.compare_exchange_strong(
+                            none, (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                      std::chrono::steady_clock::now() - t0).count());
+                    }
+                    const int64_t was = left.fetch_sub((int64_t)took, std::memory_order_relaxed);
+                    if (trace_on()) {
+                        const int64_t now = (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                std::chrono::steady_clock::now() - t0).count();
+                        const int64_t after = was - (int64_t)took;
+                        if (was > nt / 2 && after <= nt / 2) t_half.store(now);
+                        if (was > nt / 10 && after <= nt / 10) t_90.store(now);
+                        if (was > nt / 100 && after <= nt / 100) t_99.store(now);
+                    }
                     polls = 0;
                     continue;
                 }
@@ -463,6 +506,33 @@ class ResidentGrid {
             _mm_sfence();  // (this part's non-temporal stores drained before the part is reported done)
         });
         _mm_sfence();
+        if (trace_on() && tb_h_) {  // the grid's side of this request (wall clock, 100 MHz), from block 0's sight of it
+            const volatile uint64_t* t = tb_h_;
+            const uint64_t t0g = t[4 * tb_waves_];
+            std::vector<double> seen, done, wb;
+            for (int64_t w = 0; w < tb_waves_; ++w) {
+                if (t[4 * w + 3] != s) continue;
+                seen.push_back((double)(int64_t)(t[4 * w] - t0g) * 0.01);
+                done.push_back((double)(int64_t)(t[4 * w + 1] - t0g) * 0.01);
+                wb.push_back((double)(int64_t)(t[4 * w + 2] - t[4 * w + 1]) * 0.01);
+            }
+            const auto pct = [](std::vector<double>& v, double f) {
+                if (v.empty()) return -1.0;
+                std::sort(v.begin(), v.end());
+                return v[(size_t)(f * (double)(v.size() - 1))];
+            };
+            fprintf(stderr, "ovl_resident: grid side of request %u (%zu wavefronts with tiles; us after block 0 saw it): "
+                            "knew it median %.2f max %.2f; last tile done median %.2f p90 %.2f max %.2f; write-back "
+                            "median %.2f max %.2f\n",
+                    s, seen.size(), pct(seen, 0.5), pct(seen, 1.0), pct(done, 0.5), pct(done, 0.9), pct(done, 1.0),
+                    pct(wb, 0.5), pct(wb, 1.0));
+        }
+        if (trace_on())
+            fprintf(stderr, "ovl_resident: request %u, %lld tiles: first record taken %.1f us after the post, half %.1f, "
+                            "90%% %.1f, 99%% %.1f, all %.1f us\n",
+                    s, (long long)nt, (double)t_first.load() * 1e-3, (double)t_half.load() * 1e-3,
+                    (double)t_90.load() * 1e-3, (double)t_99.load() * 1e-3,
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
         *n_bad = bad.load();
         last_specials = specials.load();
         if (state.load() != 0) {

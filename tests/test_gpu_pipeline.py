@@ -173,9 +173,9 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
 @pytest.mark.parametrize("pack", ["1", "2"])
 @pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
 def test_tile_records(oracle_mod, cfg2, pack, scoring):
-    """Packed chunks cross the link as streamed tile records (OVL_PACK=2, the default: ovl_kernels.hip
-    put_tile_rec, 15-bit codes and a phase bit per dword, expanded by host threads while the kernel runs;
-    OVL_PACK=1 keeps 2 bytes per pair expanded after each chunk): cfg2's list tiled six times (731 K pairs) with
+    """Packed chunks cross the link as streamed tile records (OVL_PACK=2, opt-in: ovl_kernels.hip put_tile_rec,
+    15-bit codes and a phase bit per dword, expanded by host threads while the kernel runs; OVL_PACK=1, the
+    default, keeps 2 bytes per pair expanded after each chunk): cfg2's list tiled six times (731 K pairs) with
     bad pairs, under scorings with match == mismatch and mismatch > match, into pinned, pageable and misaligned
     arrays, all packed and with a direct share; every (score, end) equals the oracle's, and the call's link bytes
     are the records' (128 per tile + 4 per special pair) or 2 per pair."""
@@ -288,7 +288,7 @@ def test_tile_records_across_read_sets(oracle_mod):
 def test_packed_adaptive_share(oracle_mod, cfg2, cfg2_ref):
     """The direct share of 2-byte packed calls into pinned arrays (OVL_PACK=1) adapts call by call (no
     OVL_PACK_DIRECT_PCT): every call's results stay exact and the packed part stays within its bounds (50-98 % of
-    the pairs).  (Streamed records, the default, have no direct share unless OVL_PACK_DIRECT_PCT sets one:
+    the pairs).  (Streamed records, OVL_PACK=2, have no direct share unless OVL_PACK_DIRECT_PCT sets one:
     test_step_transport_vs_oracle.)"""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
@@ -663,9 +663,9 @@ def test_cfg5_full_default_scoring_vs_oracle(engine, oracle_mod, cfg5):
 
 
 def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
-    """Gapped (indel -2) on the whole cfg5 list: dp_lane_kernel (the planner's choice) ==
-    dp_fast_kernel (OVL_DP_FORM=fast) pair for pair; both == the oracle's full DP on a strided
-    50k-pair sample."""
+    """Gapped (indel -2) on the whole cfg5 list: the lane-per-pair full DP (the planner's choice, here
+    dp_lane_h2_kernel: two pairs per lane in packed f16) == dp_fast_kernel (OVL_DP_FORM=fast) pair for pair;
+    both == the oracle's full DP on a strided 50k-pair sample."""
     reads, a, b = cfg5
     lane = _engine_env({"OVL_DP_FORM": "lane"})
     fast = _engine_env({"OVL_DP_FORM": "fast"})
