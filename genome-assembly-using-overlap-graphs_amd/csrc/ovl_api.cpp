@@ -38,6 +38,7 @@
 #include <cstring>
 #include <functional>
 #include <initializer_list>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -117,6 +118,7 @@ struct Knobs {
     int32_t resident_blocks = 2;  // the grid's blocks of 256 threads per CU
     int32_t resident_pf = 1;      // its tiles software-pipelined (fewer, fatter wavefronts) or one at a time
     int32_t resident_sleep = 4;   // its non-lead blocks' pause between polls (~0.1 us units)
+    int32_t resident_ring = 0;    // its ring's memory (ResidentGrid::ring_kind)
     int32_t pack_direct_pct = 18; // OVL_PACK_DIRECT_PCT: packed calls into pinned arrays store this share of the
                                   // pairs (the last chunk) as int32 straight into them, over the link while the
                                   // host expands the packed chunks (tools/pack_ab.py, target point, six
@@ -143,8 +145,6 @@ constexpr int32_t kBandLane2Min = 64;
 // them in place.
 constexpr int64_t kLatTiles = 32;
 constexpr int64_t kLatTilesIx = 8;
-// ovl_set_reads keeps a host copy of the resident read set's bytes (same_reads) up to this size
-constexpr int64_t kResidentCopyMax = int64_t(256) << 20;
 // streamed tile records: tiles per group of the expansion (groups go round-robin to the pool's parts, so every
 // part has records arriving while the kernel runs), and pairs per pipeline chunk at most
 constexpr int64_t kRecGroupTiles = 8;
@@ -162,6 +162,85 @@ constexpr size_t kExpandPart = size_t(1) << 14;
 }  // namespace
 
 struct ovl_ctx;
+
+// A host thread per device of a multi-device context (run_pipeline): it runs the device's job of each call, on the
+// CPUs of the GPU's NUMA node when the process may use them, so N devices' launches, polls and synchronisations run
+// side by side instead of one after another on the calling thread.
+class DevWorker {
+  public:
+    explicit DevWorker(int device) : th_([this, device] { run(device); }) {}
+    ~DevWorker() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void post(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            task_ = std::move(f);
+        }
+        cv_.notify_all();
+    }
+
+  private:
+    // the GPU's NUMA node's CPUs (sysfs), intersected with the process's affinity; unchanged when unknown
+    static void bind(int device) {
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return;
+        for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+        char path[160];
+        snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+        int node = -1;
+        if (FILE* f = fopen(path, "r")) {
+            if (fscanf(f, "%d", &node) != 1) node = -1;
+            fclose(f);
+        }
+        if (node < 0) return;
+        snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+        FILE* f = fopen(path, "r");
+        if (!f) return;
+        cpu_set_t want, have;
+        CPU_ZERO(&want);
+        int lo, hi;
+        char sep;
+        while (fscanf(f, "%d", &lo) == 1) {
+            hi = lo;
+            if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+                if (fscanf(f, "%d", &hi) != 1) break;
+                if (fscanf(f, "%c", &sep) != 1) sep = 0;
+            }
+            for (int cpu = lo; cpu <= hi && cpu < CPU_SETSIZE; ++cpu) CPU_SET(cpu, &want);
+            if (sep != ',') break;
+        }
+        fclose(f);
+        if (sched_getaffinity(0, sizeof(have), &have) != 0) return;
+        CPU_AND(&want, &want, &have);
+        if (CPU_COUNT(&want) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(want), &want);
+    }
+    void run(int device) {
+        bind(device);
+        (void)hipSetDevice(device);
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_ || task_; });
+                if (quit_ && !task_) return;
+                f = std::move(task_);
+                task_ = nullptr;
+            }
+            f();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::function<void()> task_;
+    bool quit_ = false;
+    std::thread th_;
+};
 
 // Per-device state.
 struct Dev {
@@ -258,6 +337,7 @@ struct Dev {
     const uint8_t* ix_d8 = nullptr;
     const int32_t* ix_base = nullptr;
     ResidentGrid res;  // the resident scoring grid (ovl_resident.h), launched by the first call that uses it
+    std::unique_ptr<DevWorker> worker;  // multi-device contexts: this device's host thread (run_pipeline)
 };
 
 // The host side of a read-set upload in one pinned block (grown on demand, kept by the context): offsets,
@@ -283,13 +363,16 @@ struct HostReads {
 
 struct ovl_ctx {
     std::vector<Dev*> devs;
+    bool shared_slots = false;   // OVL_SHARE_DEVICES=1: a device listed more than once (tests); every call uses
+                                 // every slot (no device cap, devices_for)
     ReadStage stage;             // pinned upload stage of ovl_set_reads
     HostReads hreads;            // ovl_set_reads' host arrays (reused)
     // the read set resident on every device after the last complete ovl_set_reads: its offsets relative to
-    // offsets[0] and its bytes, so that a call with the same read set (a graph build per k over one read set,
+    // offsets[0] and a digest of its bytes, so that a call with the same read set (a graph build per k over one read set,
     // the one-shot ovl_score_pairs per build) keeps it instead of uploading and packing it again
     std::vector<int64_t> res_off;
-    std::vector<uint8_t> res_bytes;
+    int64_t res_total = 0;
+    uint64_t res_hash[2] = {0, 0};  // reads_hash of its bytes
     bool res_valid = false;
     std::string err;
     std::vector<int32_t> h_len;  // read lengths (shard balance of host pair lists)
@@ -787,13 +870,16 @@ Knobs read_knobs() {
         k.lane_h2 = (v >> 2) & 1;
     }
     if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
-    if (const char* e = getenv("OVL_RESIDENT")) {  // mode[,blocks per CU[,pipelined[,poll sleep]]] ("1x2x1x4")
+    if (const char* e = getenv("OVL_RESIDENT")) {  // mode[,blocks/CU[,pipelined[,poll sleep[,ring]]]] ("1x2x1x4x1")
         k.resident = std::max(0, std::min(2, atoi(e)));
         if (const char* c = strpbrk(e, ",x")) {
             k.resident_blocks = std::max(1, std::min(8, atoi(c + 1)));
             if (const char* c2 = strpbrk(c + 1, ",x")) {
                 k.resident_pf = atoi(c2 + 1) != 0;
-                if (const char* c3 = strpbrk(c2 + 1, ",x")) k.resident_sleep = std::max(0, std::min(1000, atoi(c3 + 1)));
+                if (const char* c3 = strpbrk(c2 + 1, ",x")) {
+                    k.resident_sleep = std::max(0, std::min(1000, atoi(c3 + 1)));
+                    if (const char* c4 = strpbrk(c3 + 1, ",x")) k.resident_ring = std::min(2, std::max(0, atoi(c4 + 1)));
+                }
             }
         }
     }
@@ -842,6 +928,7 @@ void free_staging(int32_t*& p) {
 
 void destroy_dev(Dev* d) {
     if (!d) return;
+    d->worker.reset();
     d->res.release();
     (void)hipSetDevice(d->device);
     for (hipStream_t s : {d->stream, d->s_in})
@@ -883,6 +970,7 @@ hipError_t init_dev(Dev* d) {
     d->res.blocks_per_cu = d->k.resident_blocks;
     d->res.pipelined = d->k.resident_pf;
     d->res.poll_sleep = d->k.resident_sleep;
+    d->res.ring_kind = d->k.resident_ring;
     for (hipStream_t* s : {&d->stream, &d->s_in}) {
         e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
         if (e != hipSuccess) return e;
@@ -925,6 +1013,7 @@ int create_on(const int32_t* ids, int32_t n, ovl_ctx** out) {
     DeviceGuard guard;
     CpuShare::get().refresh(true);
     ovl_ctx* c = new ovl_ctx();
+    c->shared_slots = allow_dup;
     const Knobs knobs = read_knobs();
     for (int32_t i = 0; i < n; ++i) {
         Dev* d = new Dev();
@@ -1670,6 +1759,40 @@ struct HostFlag {
     }
 };
 
+// One device's share of a host-array call: its chunks issued and drained in order.  A compact pair list (one device)
+// has chunk k issued by this thread while the pool encodes chunk k + 1; staged chunks are drained kSlots - 1
+// behind (a streamed record chunk once the chunk after it is queued: its kernel follows on the device while the
+// host expands).  With `sync`, the job ends with its streams synchronised (device workers).
+int run_job(const Call& C, Job& J, bool sync) {
+    int rc = setup_job(C, J);
+    if (rc != OVL_OK) return rc;
+    if (g_trace) g_trace->mark('s', 0);
+    if (C.compact && J.nchunks > 0 && (rc = encode_chunk(C, J, 0)) != OVL_OK) return rc;
+    for (int64_t k = 0; k < J.nchunks && rc == OVL_OK; ++k) {
+        const auto issue = [&]() -> int {
+            const int r = issue_chunk(C, J, k);
+            if (g_trace) g_trace->mark('i', k);
+            return r;
+        };
+        if (C.compact && k + 1 < J.nchunks) rc = encode_chunk(C, J, k + 1, issue);
+        else rc = issue();
+        if (rc != OVL_OK) break;
+        while (J.drained <= k) {
+            const int64_t j = J.drained;
+            if (chunk_staged(C, J, j) && k - j < (J.om[(size_t)j] == 3 ? 1 : kSlots - 1)) break;
+            if (chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
+            ++J.drained;
+        }
+    }
+    for (; rc == OVL_OK && J.drained < J.nchunks; ++J.drained)
+        if (chunk_staged(C, J, J.drained)) rc = drain_chunk(C, J, J.drained);
+    if (rc == OVL_OK && sync && J.nchunks > 0 && J.ended) {
+        HIPCHK(J.d, hipSetDevice(J.d->device));
+        HIPCHK(J.d, hipStreamSynchronize(J.d->stream));
+    }
+    return rc;
+}
+
 int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     const auto t0 = std::chrono::steady_clock::now();
     PipeTrace trace;
@@ -1679,45 +1802,35 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     } unset;
     int rc = OVL_OK;
     HostFlag host_flag(jobs, 1);  // (each chunk sets its own sink: issue_chunk)
-    for (Job& J : jobs)
-        if ((rc = setup_job(C, J)) != OVL_OK) return rc;
-    trace.mark('s', 0);
-    int64_t maxch = 0;
-    for (const Job& J : jobs) maxch = std::max(maxch, J.nchunks);
-    if (C.compact)
-        for (Job& J : jobs)
-            if (J.nchunks > 0 && (rc = encode_chunk(C, J, 0)) != OVL_OK) {
-                quiesce(jobs);  // (its decode kernels may already be queued, reading the pinned encoding)
-                return rc;
-            }
-    for (int64_t k = 0; k < maxch && rc == OVL_OK; ++k) {
-        for (Job& J : jobs) {
-            if (k >= J.nchunks) continue;
-            const auto issue = [&]() -> int {
-                const int r = issue_chunk(C, J, k);
-                trace.mark('i', k);
-                return r;
-            };
-            // compact lists: this chunk is issued (copy, launch) by the calling thread while the pool encodes
-            // the next one, then the next chunk decodes / copies and scores while the one after is encoded
-            if (C.compact && k + 1 < J.nchunks) rc = encode_chunk(C, J, k + 1, issue);
-            else rc = issue();
-            if (rc != OVL_OK) break;
-            // drain in order: a streamed record chunk once the chunk after it is queued (its kernel follows on
-            // the device while the host expands), other staged chunks kSlots - 1 behind
-            while (J.drained <= k) {
-                const int64_t j = J.drained;
-                if (chunk_staged(C, J, j) && k - j < (J.om[(size_t)j] == 3 ? 1 : kSlots - 1)) break;
-                if (chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
-                ++J.drained;
-            }
-            if (rc != OVL_OK) break;
+    if (jobs.size() == 1) {
+        rc = run_job(C, jobs[0], false);
+    } else {
+        // several devices: each device's job on its own host thread (DevWorker, on the GPU's NUMA node), so the
+        // devices' launches, polls and synchronisations run side by side; this thread waits for all of them
+        std::vector<int> rcs(jobs.size(), OVL_OK);
+        std::atomic<int> left{(int)jobs.size()};
+        std::mutex mu;
+        std::condition_variable cv;
+        for (size_t i = 0; i < jobs.size(); ++i) {
+            Dev* d = jobs[i].d;
+            if (!d->worker) d->worker.reset(new DevWorker(d->device));
+            d->worker->post([&, i] {
+                rcs[i] = run_job(C, jobs[i], true);
+                if (left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    cv.notify_all();
+                }
+            });
         }
-    }
-    for (Job& J : jobs) {
-        if (rc != OVL_OK) break;
-        for (; J.drained < J.nchunks; ++J.drained)
-            if (chunk_staged(C, J, J.drained) && (rc = drain_chunk(C, J, J.drained)) != OVL_OK) break;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return left.load(std::memory_order_acquire) == 0; });
+        }
+        for (size_t i = 0; i < jobs.size(); ++i)
+            if (rcs[i] != OVL_OK) {
+                rc = rcs[i];
+                break;
+            }
     }
     if (rc != OVL_OK) {
         quiesce(jobs);
@@ -1858,12 +1971,12 @@ int device_cuts(Dev* d, int64_t lo, int64_t hi, int32_t shards, std::vector<int6
 // list, int32 / packed ms: 131 K 0.040 / 0.041, 262 K 0.065 / 0.057, 524 K 0.099 / 0.082, 1 M 0.182 / 0.100),
 // from a quarter of that into pageable arrays, which need a host pass anyway (cfg2, 122 K pairs: 0.052-0.065
 // against 0.065-0.079 ms; profiles/r02_pack_ab_cfg2_*.json, profiles/r02_pack_size_*.json).
-bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) {
+bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned, int32_t n_devices) {
     const Dev* d = c->devs[0];
     const int64_t min_pairs = out_pinned ? d->k.pack_min : d->k.pack_min / 4;
     // (the expansion needs the host pool: with fewer than 6 threads -- several processes on one CPU set, e.g.
     // joblib workers or many ranks on one quota (CpuShare) -- the int32 stores over the link are faster)
-    return c->devs.size() == 1 && d->k.pack && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
+    return n_devices == 1 && d->k.pack && n_pairs >= min_pairs && CopyPool::threads() >= 6 &&
            p.kernel == OVL_KERNEL_UNGAPPED && !p.key64 &&
            d->planes == 2 &&
            d->wmax > 0 && d->lmax > 0 && d->lmax <= 254;  // (lmax 0: the general kernel scores the list)
@@ -1872,6 +1985,23 @@ bool pack_ok(const ovl_ctx* c, const Plan& p, int64_t n_pairs, bool out_pinned) 
 int check_scoring_args(ovl_ctx* c, int32_t match, int32_t mismatch, int64_t indel, int32_t band, Plan* p) {
     // every device holds the same read set, so device 0 plans for all
     return make_plan(c->devs[0], match, mismatch, indel, band, p);
+}
+
+// Devices (the context's first S) a host-array call over n pairs uses.  Calls over several devices store int32
+// results over each device's own link (no packing: one host pool would expand every link's results), ~145 us per
+// M pairs per link at 55 GB/s, against ~70 us per M pairs for one device with packed results and its resident grid
+// or packed launches: several devices pay only from 3 of them, each with >= kMinPairsPerDevice
+// pairs (their fixed per-call cost, ~15 us, against 36 us of link time).  Fewer -> one device, the single-device
+// paths.  A context whose slots share a GPU (OVL_SHARE_DEVICES=1, tests) uses every slot.
+constexpr int64_t kMinPairsPerDevice = int64_t(1) << 18;
+int32_t devices_for(const ovl_ctx* c, int64_t n_pairs) {
+    const int32_t k = (int32_t)c->devs.size();
+    if (k <= 1) return 1;
+    const int32_t s = (int32_t)std::min<int64_t>(k, n_pairs / kMinPairsPerDevice);
+    return s >= 3 ? s : 1;
+}
+int32_t devices_used(const ovl_ctx* c, int64_t n_pairs) {
+    return c->shared_slots ? (int32_t)c->devs.size() : devices_for(c, n_pairs);
 }
 
 // Stops the context's resident grids (ovl_resident.h) before other work on its devices: a grid's stream would hold
@@ -2183,27 +2313,64 @@ hipError_t upload_reads(Dev* d, const HostReads& h, const ReadStage& st) {
 
 namespace {
 
-// The caller's read set equals the resident one, byte for byte (offsets relative to offsets[0], then the bytes;
-// compared over the host pool, a part stops at its first difference).
+// A 128-bit digest of a read set's bytes (two independent multiply-rotate streams over 8-byte words, per 256 KiB
+// part on the host pool, parts combined in order): what same_reads compares, instead of a host copy of the bytes.
+void reads_hash(const uint8_t* p, int64_t n, uint64_t out[2]) {
+    constexpr size_t kPart = size_t(1) << 18;
+    const size_t parts = (size_t)((n + (int64_t)kPart - 1) / (int64_t)kPart);
+    std::vector<uint64_t> ph(2 * std::max<size_t>(parts, 1), 0);
+    const auto mix = [](uint64_t h, uint64_t w, uint64_t k) {
+        h ^= w * k;
+        h = (h << 31) | (h >> 33);
+        return h * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+    };
+    CopyPool::get().parallel(parts, 1, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            const uint8_t* q = p + i * kPart;
+            const size_t len = std::min<size_t>(kPart, (size_t)n - i * kPart);
+            uint64_t h0 = 0x243F6A8885A308D3ull ^ len, h1 = 0x13198A2E03707344ull + i;
+            size_t k = 0;
+            for (; k + 8 <= len; k += 8) {
+                uint64_t w;
+                memcpy(&w, q + k, 8);
+                h0 = mix(h0, w, 0xC2B2AE3D27D4EB4Full);
+                h1 = mix(h1, w ^ 0xA0761D6478BD642Full, 0x165667B19E3779F9ull);
+            }
+            uint64_t w = 0;
+            memcpy(&w, q + k, len - k);
+            ph[2 * i] = mix(h0, w, 0xC2B2AE3D27D4EB4Full);
+            ph[2 * i + 1] = mix(h1, w ^ 0xA0761D6478BD642Full, 0x165667B19E3779F9ull);
+        }
+    });
+    uint64_t h0 = 0x452821E638D01377ull ^ (uint64_t)n, h1 = 0xBE5466CF34E90C6Cull;
+    for (size_t i = 0; i < parts; ++i) {
+        h0 = mix(h0, ph[2 * i], 0xC2B2AE3D27D4EB4Full);
+        h1 = mix(h1, ph[2 * i + 1], 0x165667B19E3779F9ull);
+    }
+    out[0] = h0;
+    out[1] = h1;
+}
+
+// The caller's read set equals the resident one: the same offsets relative to offsets[0] (compared over the host
+// pool, a part stops at its first difference) and the same 128-bit digest of the bytes.
 bool same_reads(const ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n_reads) {
     if (!c->res_valid || (int64_t)c->res_off.size() != (int64_t)n_reads + 1) return false;
     for (const Dev* d : c->devs)
         if (d->n_reads != n_reads) return false;
     const int64_t base = n_reads > 0 ? offsets[0] : 0;
-    if (n_reads > 0 && offsets[n_reads] - base != (int64_t)c->res_bytes.size()) return false;
+    if (n_reads > 0 && offsets[n_reads] - base != c->res_total) return false;
     CopyPool& pool = CopyPool::get();
     std::atomic<bool> differ{false};
     pool.parallel((size_t)n_reads + 1, size_t(1) << 14, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi && !differ.load(std::memory_order_relaxed); ++i)
             if (offsets[i] - base != c->res_off[i]) differ.store(true, std::memory_order_relaxed);
     });
-    if (differ.load() || c->res_bytes.empty()) return !differ.load();
+    if (differ.load()) return false;
+    if (c->res_total == 0) return true;
     if (!seqs) return false;
-    pool.parallel(c->res_bytes.size(), size_t(1) << 18, [&](size_t lo, size_t hi) {
-        if (!differ.load(std::memory_order_relaxed) && memcmp(seqs + base + lo, c->res_bytes.data() + lo, hi - lo))
-            differ.store(true, std::memory_order_relaxed);
-    });
-    return !differ.load();
+    uint64_t h[2];
+    reads_hash(seqs + base, c->res_total, h);
+    return h[0] == c->res_hash[0] && h[1] == c->res_hash[1];
 }
 
 // ovl_set_reads; sync = false (ovl_score_pairs) leaves the uploads running on each device's kernel stream --
@@ -2274,16 +2441,11 @@ int set_reads(ovl_ctx* c, const uint8_t* seqs, const int64_t* offsets, int32_t n
     const int64_t base = n_reads > 0 ? offsets[0] : 0;
     c->res_off.resize((size_t)n_reads + 1);
     for (int32_t i = 0; i <= n_reads; ++i) c->res_off[(size_t)i] = n_reads > 0 ? offsets[i] - base : 0;
-    // (a host copy of the bytes, so only for read sets up to kResidentCopyMax: larger ones are uploaded every call
-    // rather than doubling their host memory)
-    c->res_valid = h.total <= kResidentCopyMax;
-    c->res_bytes.clear();
-    if (c->res_valid) {
-        c->res_bytes.resize((size_t)h.total);
-        if (h.total > 0) host_copy(c->res_bytes.data(), seqs + base, (size_t)h.total);
-    } else {
-        c->res_bytes.shrink_to_fit();
-    }
+    // (a digest of the bytes, not a copy: the host memory a resident set costs is its offsets)
+    c->res_total = h.total;
+    c->res_hash[0] = c->res_hash[1] = 0;
+    if (h.total > 0) reads_hash(seqs + base, h.total, c->res_hash);
+    c->res_valid = true;
     return OVL_OK;
 }
 
@@ -2379,9 +2541,9 @@ OVL_API int ovl_score_host(ovl_ctx* c, const int32_t* a_idx, const int32_t* b_id
     C.out_e = out_end;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = c->timing != 0;
-    C.pack = pack_ok(c, p, n_pairs, C.out_pinned);
-    C.compact = c->devs.size() == 1 && c->devs[0]->k.compact && n_pairs >= kCompactMin;
-    const int32_t S = (int32_t)c->devs.size();
+    const int32_t S = devices_used(c, n_pairs);
+    C.pack = pack_ok(c, p, n_pairs, C.out_pinned, S);
+    C.compact = S == 1 && c->devs[0]->k.compact && n_pairs >= kCompactMin;
     const std::vector<int64_t> cuts = host_cuts(c, a_idx, b_idx, n_pairs, S);
     std::vector<Job> jobs((size_t)S);
     for (int32_t r = 0; r < S; ++r) {
@@ -2615,7 +2777,7 @@ constexpr int kResidentFellBack = 1000;  // (resident_call: the call goes throug
 // int32 keys and 2-byte record codes (ends <= 254), timing off (its launch events time the launch pipeline), and a
 // host pool of at least 6 threads to expand the records (fewer: several processes share the CPUs, pack_ok)
 bool resident_ok(const ovl_ctx* c, const Plan& p, int64_t n) {
-    if (c->devs.size() != 1 || c->timing || CopyPool::threads() < 6) return false;
+    if (devices_used(c, n) != 1 || c->timing || CopyPool::threads() < 6) return false;
     const Dev* d = c->devs[0];
     if (d->k.resident == 0 || d->res.broken) return false;
     if (d->k.resident == 1 && (n < d->k.resident_min || n > d->k.resident_max)) return false;
@@ -2684,6 +2846,13 @@ int resident_call(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t match, int32_t m
 
 }  // namespace
 
+OVL_API int ovl_devices_for(const ovl_ctx* ctx, int64_t n_pairs, int32_t* out_devices) {
+    if (!ctx || !out_devices) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx or out_devices is NULL");
+    if (n_pairs < 0) return fail(ctx, OVL_E_ARG, "n_pairs < 0");
+    *out_devices = devices_for(ctx, n_pairs);
+    return OVL_OK;
+}
+
 OVL_API int ovl_quiesce(ovl_ctx* ctx) {
     if (!ctx) return fail((ovl_ctx*)nullptr, OVL_E_ARG, "ctx is NULL");
     DeviceGuard guard;
@@ -2739,8 +2908,8 @@ OVL_API int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int
     C.out_base = lo;
     C.out_pinned = host_pinned(out_score, bytes) && host_pinned(out_end, bytes);
     C.timing = ctx->timing != 0;
-    C.pack = pack_ok(ctx, p, hi - lo, C.out_pinned);
-    const int32_t S = (int32_t)ctx->devs.size();
+    const int32_t S = devices_used(ctx, hi - lo);
+    C.pack = pack_ok(ctx, p, hi - lo, C.out_pinned, S);
     std::vector<int64_t> cuts;
     rc = device_cuts(d0, lo, hi, S, cuts);
     if (rc != OVL_OK) return rc;

@@ -23,6 +23,9 @@ struct OvlResidentBody {
     const int32_t* heavy_ids;   // heavy tiles first (uniform_kernel's order), or null
     int64_t heavy_n;
     int64_t tile_base;          // the request's first pair / 64 within the candidate list (tile_flags index)
+    int64_t fence;              // the ring's memory is cached in the XCD's L2 (fine-grained): records written back
+                                // by a release fence -- 2 one per block, by its last wavefront to finish; 1 one per
+                                // wavefront, after its last tile; 0: uncached ring memory, no fence
 };
 constexpr int kResidentBodyWords = (int)(sizeof(OvlResidentBody) / 8);
 // The host's mailbox (pinned, fine-grained): the host writes body[seq & 1], then ctl = seq with a release store;

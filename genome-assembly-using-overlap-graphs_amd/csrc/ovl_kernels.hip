@@ -1278,7 +1278,11 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // forwards the sequence number through one device word; the other blocks' thread 0 polls that word and reads the
 // copy (the hand-off of MI355X_MICROARCH.md's first valid row: sc1 stores drained, one flag, sc1 loads).  Each
 // block then scores tiles: wavefront w of the grid takes items w, w + waves, ... (heavy tiles first, as
-// uniform_kernel orders them).  No fan-in, no fence: nothing is waited for on the device.
+// uniform_kernel orders them).  No fan-in across blocks: nothing is waited for on the device.  The records are
+// non-temporal stores into fine-grained host memory, which stay in the XCD's L2 until written back: a release
+// fence after a block's last tile (body.fence 2: the block's last wavefront, counted in LDS after each wavefront's
+// stores drained; 1: every wavefront) -- each fence writes back the whole L2, and 2,048 of them per request queue
+// behind each other (MI355X_MICROARCH.md: the write-back costs a few microseconds).
 //   Every wait is bounded: block 0 leaves (and tells the others) after idle_ticks without a request; the other
 // blocks leave after twice that without a new forward, so a grid whose block 0 never ran still ends.
 // PF: tiles software-pipelined (fewer, fatter wavefronts: 2-4 per SIMD) or one tile at a time (UNI_OCC(W, 0)
@@ -1292,6 +1296,7 @@ __global__ __launch_bounds__(256, RES_OCC(W, PF)) void resident_kernel(
     uint64_t* status, uint32_t poll_sleep, uint64_t* tbuf) {
     __shared__ uint64_t s_body[kResidentBodyWords];
     __shared__ int s_go;
+    __shared__ int s_done;  // (fence 2: wavefronts of this block done with the request)
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t n_waves = (int64_t)gridDim.x * 4;
@@ -1384,6 +1389,7 @@ __global__ __launch_bounds__(256, RES_OCC(W, PF)) void resident_kernel(
                 for (int k = 0; k < kResidentBodyWords; ++k) s_body[k] = v[k];
             }
             s_go = go;
+            s_done = 0;
         }
         __syncthreads();
         if (!s_go) return;
@@ -1458,7 +1464,15 @@ __global__ __launch_bounds__(256, RES_OCC(W, PF)) void resident_kernel(
         }
         // this wavefront's records out of the XCD's L2 (system-scope release: an L2 write-back)
         if (tbuf && lane == 0) __builtin_nontemporal_store(wall_clock64(), tbuf + 4 * wave + 1);
-        if (wave < n_items) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (q.fence == 1) {
+            if (wave < n_items) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        } else if (q.fence == 2 && (int64_t)blockIdx.x * 4 < n_items) {
+            vm_drain();  // (this wavefront's records are in the L2: the fence of the block's last one covers them)
+            int k = 0;
+            if (lane == 0) k = atomicAdd(&s_done, 1);
+            k = __builtin_amdgcn_readfirstlane(k);
+            if (k == 3) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        }
         if (tbuf && lane == 0) {
             __hip_atomic_store(tbuf + 4 * wave + 2, (uint64_t)wall_clock64(), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);

@@ -108,6 +108,10 @@ class ResidentGrid {
     int32_t blocks_per_cu = 2;
     int32_t poll_sleep = 4;     // the non-lead blocks' pause between polls (~0.1 us units)
     int32_t pipelined = 1;      // resident_kernel's PF form (tiles software-pipelined) or one tile at a time
+    int32_t ring_kind = 0;      // the ring's memory: 0 fine-grained pinned, the records written back by one release
+                                // fence per block (the block's last wavefront); 2 the same, one fence per
+                                // wavefront; 1 host pages registered uncached for the GPU (MTYPE_UC: nothing kept
+                                // in the L2, no fence; the host's own mapping stays cached)
     int64_t idle_us = 20000;     // the grid leaves after this long without a request
     int64_t call_limit_us = 2000000;
     bool broken = false;         // a failed call disabled the resident path of this device
@@ -135,8 +139,7 @@ class ResidentGrid {
     void release() {
         (void)stop();
         (void)hipSetDevice(device);
-        if (rec_h_) (void)hipHostFree(rec_h_);
-        if (sp_h_) (void)hipHostFree(sp_h_);
+        free_ring();
         if (mb_) (void)hipHostFree(mb_);
         if (st_h_) (void)hipHostFree(st_h_);
         st_h_ = nullptr;
@@ -181,6 +184,7 @@ class ResidentGrid {
         b.heavy_ids = c.heavy_n > 0 ? c.heavy_ids : nullptr;
         b.heavy_n = c.heavy_n;
         b.tile_base = c.tile_base;
+        b.fence = ring_uc_ ? 0 : ring_kind == 2 ? 1 : 2;
         __atomic_store_n(&b.seq, (uint64_t)s, __ATOMIC_RELEASE);
         flush_lines(&b, sizeof(b));
         set_ctl(s);
@@ -262,6 +266,47 @@ class ResidentGrid {
         flush_lines(&mb_->ctl, sizeof(uint64_t));
     }
 
+    bool ring_uc_ = false;  // the ring in use is host pages registered uncached (ring_kind 1)
+    // a zeroed ring array of `bytes`: fine-grained pinned memory, or (ring_kind 1) 2 MiB-aligned host pages
+    // registered for the GPU with MTYPE_UC (hipExtHostRegisterUncached)
+    hipError_t ring_alloc(void** h, void** d, size_t bytes) {
+        hipError_t e;
+        if (ring_kind == 1) {
+            const size_t al = size_t(2) << 20, sz = (bytes + al - 1) & ~(al - 1);
+            void* p = nullptr;
+            if (posix_memalign(&p, al, sz) != 0) return hipErrorOutOfMemory;
+            memset(p, 0, sz);
+            e = hipHostRegister(p, sz, hipHostRegisterPortable | hipHostRegisterMapped | hipExtHostRegisterUncached);
+            if (e != hipSuccess) {
+                free(p);
+                return e;
+            }
+            *h = p;
+            ring_uc_ = true;
+        } else {
+            if ((e = hipHostMalloc(h, bytes, kRingMem)) != hipSuccess) return e;
+            memset(*h, 0, bytes);
+            ring_uc_ = false;
+        }
+        return hipHostGetDevicePointer(d, *h, 0);
+    }
+    void ring_free(void* h) {
+        if (!h) return;
+        if (ring_uc_) {
+            (void)hipHostUnregister(h);
+            free(h);
+        } else {
+            (void)hipHostFree(h);
+        }
+    }
+    void free_ring() {
+        ring_free(rec_h_);
+        ring_free(sp_h_);
+        rec_h_ = nullptr;
+        sp_h_ = nullptr;
+        ring_log2_ = -1;
+    }
+
     static bool trace_on() {
         static const bool on = [] {
             const char* v = getenv("OVL_TRACE_PIPE");
@@ -304,19 +349,10 @@ class ResidentGrid {
             int32_t lg = 10;
             while ((int64_t(1) << lg) < nt) ++lg;
             lg = std::max(lg, ring_log2_);
-            if (rec_h_) (void)hipHostFree(rec_h_);
-            if (sp_h_) (void)hipHostFree(sp_h_);
-            rec_h_ = nullptr;
-            sp_h_ = nullptr;
-            ring_log2_ = -1;
+            free_ring();
             const size_t tiles = size_t(1) << lg;
-            const unsigned fl = kRingMem;
-            if ((e = hipHostMalloc((void**)&rec_h_, tiles * 128, fl)) != hipSuccess) return e;
-            if ((e = hipHostMalloc((void**)&sp_h_, tiles * 64 * sizeof(uint64_t), fl)) != hipSuccess) return e;
-            memset(rec_h_, 0, tiles * 128);
-            memset(sp_h_, 0, tiles * 64 * sizeof(uint64_t));
-            if ((e = hipHostGetDevicePointer((void**)&rec_d_, rec_h_, 0)) != hipSuccess) return e;
-            if ((e = hipHostGetDevicePointer((void**)&sp_d_, sp_h_, 0)) != hipSuccess) return e;
+            if ((e = ring_alloc((void**)&rec_h_, (void**)&rec_d_, tiles * 128)) != hipSuccess) return e;
+            if ((e = ring_alloc((void**)&sp_h_, (void**)&sp_d_, tiles * 64 * sizeof(uint64_t))) != hipSuccess) return e;
             ring_log2_ = lg;
             pos_ = 0;
             seq_ = 0;

@@ -67,6 +67,7 @@ SIGNATURES = {
     "ovl_score_candidates_range": (ctypes.c_int, [_P, _i64, _i64, _i32, _i32, _i64, _i32, _P, _P]),
     "ovl_candidates_shards": (ctypes.c_int, [_P, _i32, _P]),
     "ovl_quiesce": (ctypes.c_int, [_P]),
+    "ovl_devices_for": (ctypes.c_int, [_P, _i64, _pi32]),
     "ovl_resident_stats": (ctypes.c_int, [_P, _pi32, _pi64, _pi64, _pi32]),
     "ovl_local_align": (ctypes.c_int, [_P, _P, _i32, _P, _i32, _i32, _i32, _i64, _pi32, _pi32, _pi32, _pi32,
                                        _pi32, _P, _i64, _pi64]),

@@ -277,6 +277,12 @@ class OverlapEngine:
                 check(rc, ctx)
         return score
 
+    def devices_for(self, n_pairs: int) -> int:
+        """How many of this context's devices a host-array call over n_pairs uses (ovl_devices_for)."""
+        k = ctypes.c_int32()
+        check(self._L.ovl_devices_for(self._ctx, int(n_pairs), ctypes.byref(k)), self._ctx)
+        return k.value
+
     def quiesce(self) -> None:
         """Make this context's resident scoring grids leave the device now (ovl_quiesce): before a whole-device
         synchronisation (torch.cuda.synchronize), which would otherwise wait for their idle deadline.  The next

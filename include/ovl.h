@@ -224,6 +224,11 @@ int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t mat
  * are resident, their launches (relaunches: calls that found their grid gone) and whether a failed call disabled
  * the path (its calls then go through the launch pipeline). */
 int ovl_quiesce(ovl_ctx* ctx);
+/* How many of the context's devices (its first ones) a host-array scoring call over n_pairs uses: several only from
+ * 3 devices with >= 262,144 pairs each (multi-device calls store int32 results over every device's link; below
+ * that one device with packed results is faster), else 1 -- so a context over every GPU is never slower than one
+ * GPU.  (A context whose slots share a GPU, OVL_SHARE_DEVICES=1, uses every slot whatever this reports.) */
+int ovl_devices_for(const ovl_ctx* ctx, int64_t n_pairs, int32_t* out_devices);
 int ovl_resident_stats(const ovl_ctx* ctx, int32_t* alive, int64_t* launches, int64_t* relaunches, int32_t* broken);
 
 /* Contiguous shard bounds of the candidate list, balanced by sum len(a)*len(b) + 1:

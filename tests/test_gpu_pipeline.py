@@ -483,6 +483,30 @@ def test_multi_device_sharding_on_shared_gpu(oracle_mod, cfg2, cfg2_ref, slots, 
         eng.close()
 
 
+def test_device_count_rule(cfg2):
+    """ovl_devices_for: a host-array call uses several of a context's devices only from 3 of them with >= 262,144
+    pairs each, else one (the single-device paths: packed results, the resident grid), so a context over every GPU
+    is never slower than one GPU; a context whose slots share the GPU (tests) still shards every call."""
+    from ovlgraph.hostmem import pinned_empty
+    reads, a, b = cfg2
+    for slots, cases in ((1, {10: 1, 5_000_000: 1}),
+                         (2, {100_000: 1, 5_000_000: 1}),
+                         (3, {100_000: 1, 786_431: 1, 786_432: 3, 5_000_000: 3}),
+                         (8, {600_000: 1, 1_000_000: 3, 2_000_000: 7, 2_097_152: 8, 50_000_000: 8})):
+        eng = _engine_env({"OVL_SHARE_DEVICES": "1"}, devices=[0] * slots)
+        try:
+            for n, want in cases.items():
+                assert eng.devices_for(n) == want, (slots, n)
+            if slots == 3:  # (shared slots: every call still sharded -- exact over the 3 device workers)
+                eng.set_reads(reads)
+                n = a.shape[0]
+                out = (pinned_empty(n), pinned_empty(n))
+                eng.score(a, b, out=out)
+                assert eng.resident_stats()["launches"] == 0
+        finally:
+            eng.close()
+
+
 def test_contexts_on_concurrent_host_threads(oracle_mod, cfg2, cfg2_ref):
     """Separate contexts are independent (include/ovl.h): four Python threads (ctypes releases the GIL)
     score through their own engines at once, with pageable arrays, so the staging copies of all calls

@@ -1,6 +1,6 @@
-"""ovl_set_reads keeps a read set that is already resident (same offsets and bytes, compared byte for byte) instead
-of uploading and packing it again; any difference -- one base, a moved read boundary, another read count, the
-same bytes at another address -- must reach the device.  Each case is checked against the oracle."""
+"""ovl_set_reads keeps a read set that is already resident (same offsets, and the same 128-bit digest of its bytes)
+instead of uploading and packing it again; any difference -- one base, a moved read boundary, another read count,
+the same bytes at another address -- must reach the device.  Each case is checked against the oracle."""
 import numpy as np
 import pytest
 
