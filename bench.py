@@ -333,11 +333,15 @@ class Workload:
 
 
 def timed_steps(fn, steps: int, warmup: int, dev, world: int, group=None) -> float:
-    """Warmup, then `steps` calls of fn between barriers + synchronize; this rank's seconds."""
+    """Warmup, then `steps` calls of fn between barriers + synchronize; this rank's seconds.  The engines'
+    resident scoring grids are asked to leave before each synchronize (quiesce_all: inside the timed region after
+    the last step -- ending the job is part of it), else the synchronize would wait out their idle deadline."""
     import torch
     import torch.distributed as dist
+    from ovlgraph.engine import quiesce_all
     for _ in range(warmup):
         fn()
+    quiesce_all()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier(group=group)
@@ -345,6 +349,7 @@ def timed_steps(fn, steps: int, warmup: int, dev, world: int, group=None) -> flo
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
+    quiesce_all()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:

@@ -111,8 +111,9 @@ struct Knobs {
     int32_t compact = 1;
     int32_t pairs_ix = 1;
     // OVL_RESIDENT: scoring calls over the resident candidate list into host arrays go to the device's resident grid
-    // (ovl_resident.h) -- 0 never, 1 (default) from resident_min pairs up to resident_max, 2 at every size
-    int32_t resident = 1;
+    // (ovl_resident.h) -- 0 never (default: on the boxes measured it did not beat the launch pipeline, N = 1 or a
+    // 1/8 shard -- profiles/r06_shard_steps.json), 1 from resident_min pairs up to resident_max, 2 at every size
+    int32_t resident = 0;
     int64_t resident_min = 1;
     int64_t resident_max = int64_t(1) << 40;
     int32_t resident_blocks = 2;  // the grid's blocks of 256 threads per CU

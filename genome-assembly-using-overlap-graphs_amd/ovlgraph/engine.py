@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -22,6 +23,17 @@ from ._lib import OvlError, check
 from .hostmem import pinned_empty
 
 INDEL_DEFAULT = -(2 ** 31)  # aligners.py:7 default indel (the report's "-inf", REPORT p.3)
+
+_LIVE: "weakref.WeakSet[OverlapEngine]" = weakref.WeakSet()  # open contexts (quiesce_all)
+
+
+def quiesce_all() -> None:
+    """ovl_quiesce on every open context of this process: their resident scoring grids leave the device, so a
+    whole-device synchronisation (torch.cuda.synchronize) that follows does not wait for the grids' idle deadline.
+    Call it from the thread that drives the contexts."""
+    for eng in list(_LIVE):
+        if getattr(eng, "_ctx", None):
+            eng.quiesce()
 
 
 def encode_reads(reads: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
@@ -106,6 +118,7 @@ class OverlapEngine:
         self._ctx = ctx
         self._reads_key = None
         self._dev0 = self.devices[0]  # device pointers given to score_device / score_tensors live here
+        _LIVE.add(self)
 
     def _check_tensors(self, what: str, *ts) -> None:
         """Contiguous int32 tensors on this engine's first device (kernels there read and write them)."""

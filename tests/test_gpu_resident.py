@@ -1,7 +1,7 @@
 """GPU: the resident scoring grid (ovl_kernels.hip resident_kernel, ovl_resident.h) against the oracle.
 
-ovl_score_candidates(_range) calls of the uniform kernel's form go to a kernel that stays on the device between
-calls and takes requests through pinned memory.  Every result is compared bit for bit with the
+With OVL_RESIDENT=1 (opt-in), ovl_score_candidates(_range) calls of the uniform kernel's form go to a kernel that
+stays on the device between calls and takes requests through pinned memory.  Every result is compared bit for bit with the
 oracle's closed form (oracle/ovl_oracle.c, the restatement of aligners.py:27-57 where gaps cannot win), call after
 call: into reused and fresh, pinned and pageable, aligned and misaligned arrays; over shards that start inside a
 tile, enough calls for the record ring to wrap many laps; after the grid left by itself (idle) or was asked to
@@ -19,8 +19,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _engine(env=None):
+    """A context with the resident grid on (OVL_RESIDENT=1: opt-in, the default is the launch pipeline)."""
     from ovlgraph import OverlapEngine
-    env = env or {}
+    env = {"OVL_RESIDENT": "1", **(env or {})}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -243,17 +244,25 @@ def test_resident_contexts_close_reopen_and_threads(cfg2_case):
 
 
 def test_resident_off_and_timing_use_the_pipeline(cfg2_case):
-    """OVL_RESIDENT=0, and calls with timing on (whose launch events time the pipeline), never launch a grid."""
+    """OVL_RESIDENT=0 and the default (unset), and calls with timing on (whose launch events time the pipeline),
+    never launch a grid."""
+    from ovlgraph import OverlapEngine
     reads, a, b, (ref_s, ref_e) = cfg2_case
-    eng = _engine({"OVL_RESIDENT": "0"})
+    old = os.environ.pop("OVL_RESIDENT", None)
     try:
-        eng.set_reads(reads)
-        eng.enumerate_candidates(5)
-        s, e = eng.score_candidates()
-        np.testing.assert_array_equal(s, ref_s)
-        assert eng.resident_stats()["launches"] == 0
+        engines = [_engine({"OVL_RESIDENT": "0"}), OverlapEngine(0)]
     finally:
-        eng.close()
+        if old is not None:
+            os.environ["OVL_RESIDENT"] = old
+    for eng in engines:
+        try:
+            eng.set_reads(reads)
+            eng.enumerate_candidates(5)
+            s, e = eng.score_candidates()
+            np.testing.assert_array_equal(s, ref_s)
+            assert eng.resident_stats()["launches"] == 0
+        finally:
+            eng.close()
     eng = _engine()
     try:
         eng.set_reads(reads)

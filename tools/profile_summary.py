@@ -88,6 +88,15 @@ def main():
                 "SQ_LDS_IDX_ACTIVE_per_launch": m.get("SQ_LDS_IDX_ACTIVE"),
                 "lds_bank_conflict_frac": (m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"])
                 if m.get("SQ_LDS_IDX_ACTIVE") else None}
+            if m.get("SQ_LDS_IDX_ACTIVE") is not None:
+                # LDS-array busy cycles per CU cycle of the launch (the LDS's own peak is one array access per
+                # cycle per CU); LDS instructions per wave, and how much of the waves' time they held issue
+                cu_cycles = dur_ns * 1e-9 * e["shader_clock_hz"] * (SIMDS // 4)
+                e["occupancy"]["lds_array_busy_frac_of_cu_cycles"] = m["SQ_LDS_IDX_ACTIVE"] / cu_cycles
+                if m.get("SQ_WAVES"):
+                    e["occupancy"]["lds_insts_per_wave"] = m.get("SQ_INSTS_LDS", 0) / m["SQ_WAVES"]
+                e["occupancy"]["SQ_ACTIVE_INST_LDS_per_launch"] = m.get("SQ_ACTIVE_INST_LDS")
+                e["occupancy"]["SQ_WAIT_INST_LDS_per_launch"] = m.get("SQ_WAIT_INST_LDS")
             if "SQ_WAIT_ANY" in m:
                 wc = m["SQ_WAVE_CYCLES"]
                 e["occupancy"]["wave_cycles_breakdown"] = {
