@@ -884,14 +884,16 @@ def per_rank_projection(name: str):
     sharded by sum n*m over N ranks, scored alone; the committed profile named in `source`), and the speed-ups over
     one GPU they project for N ranks on N GPUs -- each rank on its own GPU, link and CPU share, so this prices the
     per-rank step, not the host memory all ranks of one node share.  None when no profile is committed."""
-    src = os.path.join("profiles", "r05_cfg4_shard_steps.json" if name == "cfg4" else "r05_shard_steps.json")
+    src = os.path.join("profiles", "r05_cfg4_shard_steps.json" if name == "cfg4" else "r06_shard_steps.json")
     try:
         with open(os.path.join(ROOT, src)) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
+    if "runs" in d:  # (round 6: several boxes, resident-grid forms beside the default "pipeline"; the first box)
+        d = d["runs"][0]
     ms = {int(r["ranks"]): float(r["median_ms"]) for r in d.get("results", [])
-          if r.get("setting", "default") in ("default", "def")}
+          if r.get("setting", "default") in ("default", "def", "pipeline")}
     if 1 not in ms:
         return None
     return {"source": src, "config": d.get("config"), "ms_per_rank_step": ms,

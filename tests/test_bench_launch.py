@@ -115,7 +115,7 @@ def test_world_size_mismatch_is_an_error():
 def test_committed_profiles_on_the_line():
     """The committed profiles bench.py puts on its line (no GPU): every cfg5 band-sweep point's kernel counters
     (profiles/r05_cfg5_pmc.json) and the per-rank projections of the target list and of cfg4
-    (profiles/r05_shard_steps.json, profiles/r05_cfg4_shard_steps.json) load and are in range."""
+    (profiles/r06_shard_steps.json, profiles/r05_cfg4_shard_steps.json) load and are in range."""
     for band in (4, 8, 16, 32, 64, -1):
         p = bench.band_pmc(band)
         assert p is not None, band
@@ -125,6 +125,6 @@ def test_committed_profiles_on_the_line():
     assert bench.band_pmc(12345) is None
     for name in ("target", "cfg4"):
         pr = bench.per_rank_projection(name)
-        assert pr is not None and pr["source"].startswith("profiles/r05_"), name
+        assert pr is not None and pr["source"].startswith("profiles/r0"), name
         sp = pr["projected_speedup"]
         assert sp[1] == 1.0 and 1.0 < sp[2] < sp[4] < sp[8] <= 8.0, sp
