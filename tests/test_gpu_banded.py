@@ -77,7 +77,8 @@ def test_full_width_band_is_the_reference_dp(engine, oracle_mod, reads_pairs):
 
 
 def test_banded_cfg5_sample(engine, oracle_mod):
-    """Config 5 reads (PhiX, l=250, p=0.05): a strided 20k-pair sample at the sweep's bands."""
+    """Config 5 reads (PhiX, l=250, p=0.05): a strided 20k-pair sample at every band of the sweep (4, 8, 16, 32,
+    64: one lane per pair up to 32, two lanes per pair at 64), at indel -2 and at the sweep's default indel."""
     from ovlgraph.candidates import dedup_reads, enumerate_candidates
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads("cfg5"))
@@ -85,11 +86,13 @@ def test_banded_cfg5_sample(engine, oracle_mod):
     idx = np.linspace(0, a.shape[0] - 1, 20000).astype(np.int64)
     a, b = a[idx], b[idx]
     engine.set_reads(reads)
-    for band in (8, 64):
-        sc, en = engine.score(a, b, 10, -1, -2, band)
-        rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, -2, band)
-        np.testing.assert_array_equal(sc, rs)
-        np.testing.assert_array_equal(en, re_)
+    from ovlgraph.engine import INDEL_DEFAULT
+    for indel in (-2, INDEL_DEFAULT):
+        for band in (4, 8, 16, 32, 64):
+            sc, en = engine.score(a, b, 10, -1, indel, band)
+            rs, re_ = oracle_mod.batch_banded(reads, a, b, 10, -1, indel, band)
+            np.testing.assert_array_equal(sc, rs, err_msg=f"band {band} indel {indel}")
+            np.testing.assert_array_equal(en, re_, err_msg=f"band {band} indel {indel}")
 
 
 def test_banded_cfg5_full_list(engine, oracle_mod):
