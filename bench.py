@@ -696,9 +696,7 @@ def pair_bytes(lens: np.ndarray, a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 
 SINKS = {0: "int32 results in HBM (copy-engine transfer after)", 1: "int32 results stored into pinned host memory",
-         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)",
-         3: "streamed tile records (15-bit codes + a phase bit per dword: 128 B per 64 pairs + 4 B per special pair) "
-            "stored into pinned host staging, expanded by host threads while the kernel runs"}
+         2: "packed 2 B/pair results stored into pinned host staging (host threads expand)"}
 
 
 def kernel_name(w, sink: int, pairs: int) -> str:
@@ -708,13 +706,12 @@ def kernel_name(w, sink: int, pairs: int) -> str:
     if w.kernel != "ungapped":
         return f"{w.kernel} kernel"
     lmax = w.eng.info()["lmax"]
-    lat = sink != 3 and (pairs + 63) // 64 <= 256 * 32  # (streamed records: always throughput mode)
+    lat = (pairs + 63) // 64 <= 256 * 32
     # (the fifth parameter, IX, is true only for host pair lists read in their encoding)
     return f"uniform_kernel<{(lmax + 31) // 32}, 0, {'true' if lat else 'false'}, {sink}, false>"
 
 
-# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed; 3
-# streamed tile records: 128 B per 64 pairs plus 4 B per special pair, measured per call -- in_step_rooflines)
+# result bytes a launch stores over the host link per pair, by sink (0: HBM outputs, 1: two int32, 2: packed)
 LINK_BYTES_PER_PAIR = {0: 0, 1: 8, 2: 2}
 # a kernel's stores into pinned host memory, measured on the box (profiles/r02_pcie_write.txt)
 LINK_PEAK_GBS = 55.3
@@ -730,20 +727,11 @@ def in_step_rooflines(w, ms_per_step: float, reps: int = 7):
     np.cumsum(pair_bytes(lens, w.a[w.lo:w.hi], w.b[w.lo:w.hi]), out=cum[1:])
     w.eng.set_timing(True)
     runs = []
-    rec_bpp = []
     for _ in range(reps):
         w.step()
         runs.append(w.eng.last_launches())
-        # tile records' bytes per pair: the call's link bytes less those of its other sinks
-        x = w.eng.last_transfer()
-        rec = [r["pairs"] for r in runs[-1] if r["sink"] == 3]
-        if rec:
-            other = sum(r["pairs"] * LINK_BYTES_PER_PAIR.get(r["sink"], 0) for r in runs[-1] if r["sink"] != 3)
-            rec_bpp.append((x["link_bytes"] - other) / sum(rec))
     w.eng.set_timing(False)
     bpp = dict(LINK_BYTES_PER_PAIR)
-    if rec_bpp:
-        bpp[3] = float(np.median(rec_bpp))
     by_sink = {}
     for recs in runs:
         off = 0

@@ -96,11 +96,11 @@ struct Knobs {
     int64_t pipe_chunk = 0;       // OVL_PIPE_CHUNK env: pairs per pipeline chunk (0 = automatic; tests)
     int32_t pack = 1;             // OVL_PACK: 0 host-array results cross the link as int32 pairs even when a packed
                                   // form holds; 1 (default) packed as 2 bytes per pair, expanded chunk by chunk
-                                  // after each chunk's kernel, a last chunk stored as int32 meanwhile; 2 as
-                                  // streamed tile records (ovl_kernels.hip put_tile_rec), one launch whose records
-                                  // host threads expand while it runs.  Same box, per-rank steps of the target list
-                                  // at N = 1 / 2 / 8, 1 against 2: 0.135 / 0.088 / 0.045 against 0.144 / 0.081 /
-                                  // 0.050 ms; cfg4 and cfg3 within 3 % (profiles/r05_stream_vs_packed_ab.json)
+                                  // after each chunk's kernel, a last chunk stored as int32 meanwhile.  (Round 5's
+                                  // streamed tile records, one launch whose records host threads expand while it
+                                  // runs, were removed in round 6: target N = 1 / 2 / 8 0.144 / 0.081 / 0.050 ms
+                                  // against 0.135 / 0.088 / 0.045, profiles/r05_stream_vs_packed_ab.json; its record
+                                  // format lives on in the resident grid's ring)
     int64_t pack_min = 1 << 16;   // OVL_PACK_MIN: packed transport from this many pairs per call into pinned arrays
                                   // (64 K: a 250 K-pair shard -- N = 8 at the target point -- 0.057 -> 0.054 ms)
     int32_t pack_adapt = 1;       // the direct share follows the measured balance (pack_share); off when
@@ -146,13 +146,6 @@ constexpr int32_t kBandLane2Min = 64;
 // them in place.
 constexpr int64_t kLatTiles = 32;
 constexpr int64_t kLatTilesIx = 8;
-// streamed tile records: tiles per group of the expansion (groups go round-robin to the pool's parts, so every
-// part has records arriving while the kernel runs), and pairs per pipeline chunk at most
-constexpr int64_t kRecGroupTiles = 8;
-// incomplete records a pass of the expansion skips before it polls again (4 / 32 / all of a part's: N = 1 step
-// 0.168 / 0.155 / 0.167 ms, N = 8 0.050 / 0.049 / 0.052, profiles/r05_rec_skip_ab.json)
-constexpr size_t kRecSkip = 32;
-constexpr int64_t kRecChunk = int64_t(1) << 22;
 // compact host pair lists from this many pairs per call
 constexpr int64_t kCompactMin = int64_t(1) << 16;
 // host expansion of packed results: pairs per pool part at least (finer parts than 64 K: the expansion of a
@@ -275,20 +268,6 @@ struct Dev {
     hipEvent_t scratch_evt = nullptr;     // last launch that used lane_col / seed_* ...
     hipEvent_t ev_last = nullptr;         // packed calls into pinned arrays: after the last (direct) chunk
     double pack_pct = -1.0;               // live direct share of packed calls into pinned arrays (pack_share)
-    // streamed tile records, per staging slot: the phase bit of the slot's record dwords (every dword of tiles
-    // [0, rec_hw) carries it; the dwords above are still zero from the allocation) and its high-water mark
-    uint8_t rec_phase[kSlots] = {};
-    int64_t rec_hw[kSlots] = {};
-    // ... whether its special words are known zero (false after a chunk of another sink used its staging), the special
-    // words its last record chunk read (zeroed once that chunk's kernel has ended, stream_chunk), and the rotation
-    // of record chunks over the slots (consecutive record chunks take consecutive slots)
-    bool rec_clean[kSlots] = {true, true, true};
-    std::vector<uint32_t*> rec_dirty[kSlots];
-    uint32_t rec_next = 0;
-    uint32_t rec_phase_next = 0;          // the phase the next record launch stores (launch_score_chunk),
-    int64_t rec_tiles = 0;                // its tiles [0, rec_tiles) as records, the rest as int32 into
-    int32_t* dir_score = nullptr;         // these (device addresses of the caller's pinned arrays; null: none)
-    int32_t* dir_end = nullptr;
     double pack_pct_h = -1.0;             // the same for calls with a compact host pair list (the host also
                                           // encodes the list, so its balance point differs)
     hipStream_t scratch_stream = nullptr; // ... and its stream (launches on other streams wait for it)
@@ -650,7 +629,7 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         if (rc != OVL_OK) return rc;
         seed_end = as<int32_t>(c->seed_e);
     }
-    if (c->ix_b16 && (pl.kernel != OVL_KERNEL_UNGAPPED || pl.key64 || (c->out_mode != 3 && !ix_launch(c, n_pairs))))
+    if (c->ix_b16 && (pl.kernel != OVL_KERNEL_UNGAPPED || pl.key64 || !ix_launch(c, n_pairs)))
         return fail(c, OVL_E_UNSUPPORTED, "host-encoded pair list on a launch that cannot read it");
     if (pl.kernel == OVL_KERNEL_UNGAPPED) {
         OvlUngappedArgs g{};
@@ -687,11 +666,6 @@ int launch_score_chunk(Dev* c, const Plan& pl, const int32_t* d_a, const int32_t
         g.ix_b16 = c->ix_b16;
         g.ix_d8 = c->ix_d8;
         g.ix_base = c->ix_base;
-        g.rec_phase = c->rec_phase_next;
-        g.rec_tiles = c->out_mode == 3 ? c->rec_tiles : 0;
-        g.dir_score = c->out_mode == 3 ? c->dir_score : nullptr;
-        g.dir_end = c->out_mode == 3 ? c->dir_end : nullptr;
-        if (c->out_mode == 3) g.rs_log2 = 0;  // (records: throughput mode, every pair of a tile in one wave)
         // a throughput-mode launch over (a 64-aligned part of) the resident candidate list: heavy tiles first
         const int32_t* ca = as<int32_t>(c->cand_a);
         if (!g.ix_b16 && g.lw > 0 && g.rs_log2 == 0 && c->cand_n > 0 && d_a >= ca &&
@@ -870,7 +844,7 @@ Knobs read_knobs() {
         k.lane_sfx = (v >> 1) & 1;
         k.lane_h2 = (v >> 2) & 1;
     }
-    if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(2, atoi(e)));
+    if (const char* e = getenv("OVL_PACK")) k.pack = std::max(0, std::min(1, atoi(e)));
     if (const char* e = getenv("OVL_RESIDENT")) {  // mode[,blocks/CU[,pipelined[,poll sleep[,ring]]]] ("1x2x1x4x1")
         k.resident = std::max(0, std::min(2, atoi(e)));
         if (const char* c = strpbrk(e, ",x")) {
@@ -1111,15 +1085,9 @@ struct Job {
     int32_t* d_end = nullptr;
     std::vector<uint8_t> ixk;    // C.compact: chunk k's list is read in place by uniform_kernel (encode_chunk)
     std::vector<uint8_t> kexact; // timing: chunk k's kernel recorded its own start / end (k_ev)
-    std::vector<uint8_t> om;     // chunk k's result sink (OvlUngappedArgs::host_out): 1 int32, 2 packed, 3 records
-    std::vector<uint8_t> slot;   // chunk k's staging slot: k % kSlots, or the next in Dev::rec_next's rotation (records)
-    int64_t n_esc = 0;           // special pairs seen by the expansion of the record chunks
+    std::vector<uint8_t> om;     // chunk k's result sink (OvlUngappedArgs::host_out): 1 int32, 2 packed
+    std::vector<uint8_t> slot;   // chunk k's staging slot: k % kSlots
     int64_t drained = 0;         // chunks [0, drained) are drained (run_pipeline)
-    int64_t rec_end = 0;         // packed pairs [0, rec_end); streamed records: the pairs from rec_end on are
-                                 // stored as int32 by the last chunk's launch (its tiles from rec_end / 64)
-    int64_t n_bad = 0;           // bad pairs seen by the expansion of the record chunks (their special words)
-    bool ended = true;           // every launch of the job is known finished (false: a streamed chunk returned
-                                 // on its records alone; run_pipeline then needs no stream synchronisation)
 };
 
 // Chunk k's results go through the staging slots (pageable caller arrays, or a packed chunk).
@@ -1134,49 +1102,34 @@ int setup_job(const Call& C, Job& J) {
     HIPCHK(d, hipSetDevice(d->device));
     const bool need_in = C.h_a && !C.in_pinned && !C.compact, need_out = !C.out_pinned || C.pack;
     J.chunk = pick_chunk(d, n, need_in || need_out, C.pack);
-    const bool stream = C.pack && d->k.pack >= 2;  // streamed records: fewer, larger chunks (the host expands
-                                                   // each while its kernel runs)
-    if (stream && d->k.pipe_chunk <= 0) J.chunk = std::min(n, kRecChunk);
     // packed calls: the packed share in equal chunks of <= J.chunk, then (pinned arrays) the direct share
     int64_t packed = 0;
     if (C.pack) {
         double& share = C.compact ? d->pack_pct_h : d->pack_pct;
         if (share < 0.0) share = C.compact ? 2.0 * d->k.pack_direct_pct : d->k.pack_direct_pct;
-        // (streamed records: no direct share unless OVL_PACK_DIRECT_PCT asks for one -- it lengthens the launch
-        // on the link and makes the call wait for the kernel's end: 0 % was fastest at N = 2 / 4 / 8 and within
-        // 4 % at N = 1, profiles/r05_stream_share_ab.json)
-        const int64_t pct = stream ? (d->k.pack_adapt ? 0 : d->k.pack_direct_pct)
-                                   : (d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct);
+        const int64_t pct = d->k.pack_adapt ? (int64_t)(share + 0.5) : d->k.pack_direct_pct;
         packed = C.out_pinned ? (n - n * pct / 100) & ~int64_t(63) : n;
         if (packed >= n - 64) packed = n;
         // (a ramp of growing chunks -- 196 K, x 1.5 each -- to start the host's expansion sooner measured slower:
         // 0.208 against 0.145 ms at the target point, each extra chunk costing an issue and a later direct
         // chunk; profiles/r04_pool_ab_*.json)
-        // (streamed records: the chunks cover every pair, and the last one's launch stores its pairs from
-        // `packed` on as int32 straight into the caller's pinned arrays -- one launch, no second kernel)
-        const int64_t span = stream ? n : packed;
-        const int64_t pieces = (span + J.chunk - 1) / J.chunk;
-        const int64_t step = pieces ? (((span + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
-        for (int64_t o = step; o < span; o += step) J.cb.push_back(o);
-        if (span > 0) J.cb.push_back(span);
+        const int64_t pieces = (packed + J.chunk - 1) / J.chunk;
+        const int64_t step = pieces ? (((packed + pieces - 1) / pieces + 63) & ~int64_t(63)) : 0;
+        for (int64_t o = step; o < packed; o += step) J.cb.push_back(o);
+        if (packed > 0) J.cb.push_back(packed);
         J.n_packed = (int64_t)J.cb.size() - 1;
     }
-    J.rec_end = stream ? packed : J.cb.back();
-    for (int64_t o = J.cb.back(); o < n;) {  // (the direct chunks; none when streamed: the chunks cover every pair)
+    for (int64_t o = J.cb.back(); o < n;) {  // (the direct chunks)
         o = std::min(n, o + J.chunk);
         J.cb.push_back(o);
     }
     J.nchunks = (int64_t)J.cb.size() - 1;
-    // sinks: packed chunks as streamed tile records (OVL_PACK=1: 2 bytes per pair); the rest int32
+    // sinks: packed chunks 2 bytes per pair; the rest int32
     J.om.assign((size_t)J.nchunks, 1);
-    J.n_esc = 0;
-    J.n_bad = 0;
-    J.ended = true;
     J.drained = 0;
-    for (int64_t k = 0; k < J.n_packed; ++k) J.om[(size_t)k] = stream ? 3 : 2;
+    for (int64_t k = 0; k < J.n_packed; ++k) J.om[(size_t)k] = 2;
     J.slot.resize((size_t)J.nchunks);
-    for (int64_t k = 0; k < J.nchunks; ++k)
-        J.slot[(size_t)k] = (uint8_t)(J.om[(size_t)k] == 3 ? d->rec_next++ % kSlots : k % kSlots);
+    for (int64_t k = 0; k < J.nchunks; ++k) J.slot[(size_t)k] = (uint8_t)(k % kSlots);
     for (int64_t k = 0; k < J.nchunks; ++k) J.chunk = std::max(J.chunk, J.cb[(size_t)k + 1] - J.cb[(size_t)k]);
     const size_t bytes = sizeof(int32_t) * (size_t)n;
     if (C.compact) {
@@ -1230,14 +1183,6 @@ int setup_job(const Call& C, Job& J) {
     if (need_in && !d->st_in) HIPCHK(d, alloc_staging(d->st_in, d->st_in_dev, d->st_cap));
     if (need_out && !d->st_out) {
         HIPCHK(d, alloc_staging(d->st_out, d->st_out_dev, d->st_cap));
-        // (streamed records: every record dword and special word starts at zero, phase 0)
-        memset(d->st_out, 0, (size_t)kSlots * 2 * (size_t)d->st_cap * sizeof(int32_t));
-        for (int i = 0; i < kSlots; ++i) {
-            d->rec_phase[i] = 0;
-            d->rec_hw[i] = 0;
-            d->rec_clean[i] = true;
-            d->rec_dirty[i].clear();
-        }
     }
     if (C.timing && (int64_t)d->t_ev.size() < 2 * J.nchunks) {
         while ((int64_t)d->t_ev.size() < 2 * J.nchunks) {
@@ -1326,7 +1271,7 @@ int encode_chunk(const Call& C, Job& J, int64_t k, const std::function<int()>& p
     // throughput-mode uniform launch; else the decode below.
     // (OVL_TRACE_PIPE: 'x' marks a chunk that cannot be read in place, with the first failed condition)
     const int ix_why = wd != 2 ? 1 : !d->k.pairs_ix ? 2 : C.plan->kernel != OVL_KERNEL_UNGAPPED ? 3
-                       : C.plan->key64 ? 4 : !(J.om[(size_t)k] == 3 || ix_launch(d, n)) ? 5 : 0;
+                       : C.plan->key64 ? 4 : !ix_launch(d, n) ? 5 : 0;
     if (g_trace && ix_why) g_trace->mark('x', ix_why);
     if (ix_why == 0) {
         uint8_t* d8 = reinterpret_cast<uint8_t*>(ha);
@@ -1468,36 +1413,6 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     int32_t* os = staged_out ? d->st_out_dev + so : J.d_score + off;
     int32_t* oe = staged_out ? d->st_out_dev + so + d->st_cap : J.d_end + off;
     d->out_mode = J.om[(size_t)k];
-    if (staged_out && d->out_mode != 3) d->rec_clean[slot] = false;  // (its stores leave values in the slot)
-    if (d->out_mode == 3 && (!d->rec_clean[slot] || !d->rec_dirty[slot].empty())) {
-        // the slot's special words are not known zero -- another sink's chunk used it, or the record chunk before
-        // found no later chunk to clear them (stream_chunk): once its writers have ended, zero them here
-        HIPCHK(d, hipStreamSynchronize(d->stream));
-        if (!d->rec_clean[slot]) {
-            memset(d->st_out + so, 0, 2 * (size_t)d->st_cap * sizeof(int32_t));
-            d->rec_phase[slot] = 0;
-            d->rec_hw[slot] = 0;
-            d->rec_clean[slot] = true;
-        } else {
-            for (uint32_t* w : d->rec_dirty[slot]) *(volatile uint32_t*)w = 0u;
-        }
-        d->rec_dirty[slot].clear();
-    }
-    if (d->out_mode == 3) {
-        // streamed records: this launch stores the other phase; a slot growing past its high-water mark first
-        // gives the new tiles' dwords the old phase (they are zero, i.e. phase 0, until then)
-        const int64_t nt = (std::max<int64_t>(0, std::min(n, J.rec_end - off)) + 63) / 64;
-        uint32_t* rec = reinterpret_cast<uint32_t*>(d->st_out + so);
-        if (nt > d->rec_hw[slot]) {
-            if (d->rec_phase[slot]) std::fill(rec + 32 * d->rec_hw[slot], rec + 32 * nt, 0x80000000u);
-            d->rec_hw[slot] = nt;
-        }
-        d->rec_phase_next = d->rec_phase[slot] ^ 1u;
-        // the chunk's tiles from rec_end on store int32 into the caller's pinned arrays (the direct share)
-        d->rec_tiles = (std::max<int64_t>(0, std::min(n, J.rec_end - off)) + 63) / 64;
-        d->dir_score = d->rec_tiles * 64 < n ? J.d_score + off : nullptr;
-        d->dir_end = d->rec_tiles * 64 < n ? J.d_end + off : nullptr;
-    }
     hipStream_t ks = d->stream;
     if (C.timing) {
         HIPCHK(d, hipEventRecord(d->t_ev[2 * k], ks));
@@ -1520,188 +1435,6 @@ int issue_chunk(const Call& C, Job& J, int64_t k) {
     return OVL_OK;
 }
 
-// Streamed tile records of chunk k (sink 3; ovl_kernels.hip put_tile_rec, ovl_expand.h): the host pool expands
-// the records into the caller's arrays as they arrive, while the chunk's kernel still runs.  The chunk's tiles
-// go in groups of kRecGroupTiles round-robin to the pool's parts, so every part has records landing throughout
-// the kernel; a part's passes take every complete record among its tiles, skipping incomplete ones (records of
-// one round of waves land in any order), and poll when a pass found nothing.
-//   The call needs the kernel's end only when the chunk has direct tiles (int32 stores the host cannot see
-// arrive) or timing is on (`need_end`): then part 0 -- the calling thread -- waits for the chunk's event after
-// its own tiles.  Otherwise the results are complete once every record is read: bad pairs arrive as special
-// words (the kernel sets no host flag for record tiles), nothing of this call is left to land in host memory,
-// and the stream orders the next call's launches after this kernel, so the call returns ~5 us before the
-// kernel's completion signal could be seen (tools/launch_probe.hip).
-//   A kernel that fails must not leave a part polling forever: part 0 queries the event while it polls, any
-// part queries it after kLostPolls fruitless polls, and a record still incomplete well after the kernel has
-// finished -- which the kernel's end makes impossible -- ends the call with OVL_E_INTERNAL.  The special words
-// read are zeroed during the next record chunk's drain (below), and tiles above this chunk's that an earlier,
-// larger chunk left in this slot get this launch's phase, so the slot's next launch finds every dword it does not
-// write yet in the other phase.
-int stream_chunk(const Call& C, Job& J, int64_t k) {
-    constexpr uint32_t kLostPolls = 1u << 14;
-    Dev* d = J.d;
-    const int64_t off = J.cb[(size_t)k];
-    const int64_t g = J.lo + off;
-    const int64_t n = J.cb[(size_t)k + 1] - off;
-    const int slot = J.slot[(size_t)k];
-    const int64_t nrec = std::max<int64_t>(0, std::min(n, J.rec_end - off));  // pairs of the records
-    const int64_t nt = (nrec + 63) / 64;
-    const bool need_end = nrec < n || C.timing;
-    uint32_t* rec = reinterpret_cast<uint32_t*>(d->st_out + (size_t)slot * 2 * (size_t)d->st_cap);
-    uint32_t* sp = rec + d->st_cap;
-    const uint32_t phase = d->rec_phase[slot] ^ 1u;
-    int32_t* S = C.out_s + (g - C.out_base);
-    int32_t* E = C.out_e + (g - C.out_base);
-    const ovl_expand::RecK rk{C.match, C.mismatch};
-    static const bool a512 = ovl_expand::rec_avx512();
-    // non-temporal stores where the arrays are aligned: regular stores (read for ownership) measured 1.2-1.9x
-    // slower at every shard size (profiles/r05_rec_store_ab.json)
-    const bool al = ((uintptr_t)S & 63) == 0 && ((uintptr_t)E & 63) == 0;
-    const hipEvent_t ev = d->ev_k[slot];
-    // 0 the kernel may still run, 1 it has finished, 2 error (kernel failure or an incomplete record)
-    std::atomic<int> state{0};
-    std::atomic<int64_t> specials{0}, bad{0};
-    std::atomic<hipError_t> herr{hipSuccess};
-    const auto query = [&] {  // the kernel's event; false on a failure
-        const hipError_t q = hipEventQuery(ev);
-        if (q == hipSuccess) {
-            int z = 0;
-            if (state.compare_exchange_strong(z, 1, std::memory_order_acq_rel) && g_trace) g_trace->mark('k', k);
-        } else if (q != hipErrorNotReady) {
-            herr.store(q);
-            state.store(2, std::memory_order_release);
-            return false;
-        }
-        return true;
-    };
-    CopyPool& pool = CopyPool::get();
-    const std::vector<size_t> parts = pool.cut(64 * 64, 64);
-    const int64_t P = (int64_t)parts.size() - 1;
-    const int64_t ngroups = (nt + kRecGroupTiles - 1) / kRecGroupTiles;
-    // The special words the record chunk before this one read (the previous slot of the rotation) are zeroed here,
-    // once this chunk's kernel is seen running (a record of it complete, or its end): the stream ran that chunk's
-    // kernel to its end first, and the slot is not written again until the chunk after the next, issued after this
-    // drain.  A host store into a line of a kernel that still runs can be lost (ovl_expand.h).
-    const int prev = (slot + kSlots - 1) % kSlots;
-    std::vector<uint32_t*>& clear = d->rec_dirty[prev];
-    const bool clear_prev = prev != slot && !clear.empty();
-    std::atomic<bool> started{false};
-    std::vector<std::vector<uint32_t*>> taken_by((size_t)P);
-    pool.parallel_parts(parts, [&](size_t i, size_t, size_t) {
-        uint32_t polls = 0;  // fruitless polls in a row
-        int64_t after = 0;   // polls since the kernel was seen finished
-        // one poll of an incomplete record or special word: false ends the part (error)
-        const auto wait = [&]() -> bool {
-            _mm_pause();
-            const int st = state.load(std::memory_order_acquire);
-            if (st == 2) return false;
-            if (st == 1) {
-                if (++after > (int64_t(1) << 22)) {  // (~0.1 s after the kernel's end)
-                    state.store(2, std::memory_order_release);
-                    return false;
-                }
-                return true;
-            }
-            ++polls;
-            if ((i == 0 && (polls & 63) == 0) || (polls & (kLostPolls - 1)) == 0) return query();
-            return true;
-        };
-        // this part's tiles (its groups, in order); a pass expands every complete record among them and skips
-        // the incomplete ones until kRecSkip of them, so a pass costs a few polls when little has landed
-        std::vector<int32_t> pend;
-        pend.reserve((size_t)((nt / P) + 2 * kRecGroupTiles));
-        for (int64_t gi = (int64_t)i; gi < ngroups; gi += P)
-            for (int64_t t = gi * kRecGroupTiles, t1 = std::min(nt, (gi + 1) * kRecGroupTiles); t < t1; ++t)
-                pend.push_back((int32_t)t);
-        int64_t m = 0;
-        int nbad = 0;
-        bool first = i == 0 && g_trace;
-        // (the special words read, in a part-local vector handed over at the end: the parts' vector objects share
-        // cache lines, and updating them per tile from every thread measured ~5x slower expansion)
-        std::vector<uint32_t*> taken;
-        uint32_t* tk[64];
-        bool cleared = !clear_prev;
-        const auto clear_share = [&] {  // (this part's share of the previous chunk's special words)
-            const size_t len = clear.size(), lo = len * i / (size_t)P, hi = len * (i + 1) / (size_t)P;
-            for (size_t q = lo; q < hi; ++q) *(volatile uint32_t*)clear[q] = 0u;
-            cleared = true;
-        };
-        while (!pend.empty()) {
-            size_t keep = 0, skipped = 0, x = 0, took = 0;
-            for (; x < pend.size() && skipped < kRecSkip; ++x) {
-                const int64_t t = pend[x];
-                const size_t cnt = (size_t)std::min<int64_t>(64, nrec - 64 * t);
-                uint32_t* r = rec + 32 * t;
-                int got;
-                if (a512 && cnt == 64) {
-                    bool ready = false;
-                    got = ovl_expand::rec_tile_avx512(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, phase, al, &ready,
-                                                      &nbad, tk);
-                    if (!ready) got = -2;
-                } else {
-                    got = ovl_expand::rec_tile_scalar(S + 64 * t, E + 64 * t, r, sp + 64 * t, rk, cnt, phase, &nbad, tk);
-                }
-                if (got >= 0) {
-                    m += got;
-                    ++took;
-                    taken.insert(taken.end(), tk, tk + got);
-                    if (!cleared) {
-                        started.store(true, std::memory_order_relaxed);
-                        clear_share();
-                    }
-                    if (first) {
-                        g_trace->mark('f', k);
-                        first = false;
-                    }
-                } else {
-                    pend[keep++] = (int32_t)t;
-                    ++skipped;
-                }
-            }
-            for (; x < pend.size(); ++x) pend[keep++] = pend[x];
-            pend.resize(keep);
-            if (took) polls = 0;
-            else if (!pend.empty() && !wait()) return;
-            if (!cleared && started.load(std::memory_order_relaxed)) clear_share();
-        }
-        // (a part out of tiles clears its share once the kernel is seen running: another part's record, or its end)
-        while (!cleared) {
-            if (started.load(std::memory_order_relaxed) || state.load(std::memory_order_acquire) == 1) {
-                clear_share();
-            } else if (!wait()) {
-                return;
-            }
-        }
-        specials.fetch_add(m, std::memory_order_relaxed);
-        bad.fetch_add(nbad, std::memory_order_relaxed);
-        _mm_sfence();  // (this part's non-temporal stores drained before the part is reported done)
-        taken_by[i] = std::move(taken);
-        if (i == 0 && need_end) {  // the kernel's end (its event): direct tiles, timing
-            if (g_trace) g_trace->mark('p', k);
-            while (state.load(std::memory_order_acquire) == 0 && query()) _mm_pause();
-        }
-    });
-    _mm_sfence();
-    if (state.load() == 2) {
-        // the slot's dwords and special words are in no known state: reallocated (zeroed) by the next call
-        (void)hipStreamSynchronize(d->stream);
-        free_staging(d->st_out);
-        d->st_cap = 0;
-        const hipError_t e = herr.load();
-        if (e != hipSuccess) return fail(d, OVL_E_HIP, "HIP error %d (%s) in the scoring kernel", (int)e,
-                                         hipGetErrorString(e));
-        return fail(d, OVL_E_INTERNAL, "a result record was incomplete after its kernel finished");
-    }
-    for (int64_t w = 32 * nt; w < 32 * d->rec_hw[slot]; ++w) rec[w] ^= 0x80000000u;
-    d->rec_phase[slot] = (uint8_t)phase;
-    if (clear_prev) clear.clear();
-    for (auto& v : taken_by) d->rec_dirty[slot].insert(d->rec_dirty[slot].end(), v.begin(), v.end());
-    J.n_esc += specials.load();
-    J.n_bad += bad.load();
-    J.ended = need_end;  // (the stream's earlier launches end before this chunk's)
-    return OVL_OK;
-}
-
 // Pageable outputs: copy chunk k out of its staging slot once its results are there (the kernel that stored
 // them has finished).
 int drain_chunk(const Call& C, Job& J, int64_t k) {
@@ -1710,11 +1443,6 @@ int drain_chunk(const Call& C, Job& J, int64_t k) {
     const int64_t g = J.lo + off;
     const int64_t n = J.cb[(size_t)k + 1] - off;
     const int slot = J.slot[(size_t)k];
-    if (J.om[(size_t)k] == 3) {
-        const int rc = stream_chunk(C, J, k);
-        if (g_trace) g_trace->mark('d', k);
-        return rc;
-    }
     HIPCHK(d, wait_event(d, d->ev_k[slot]));
     if (g_trace) g_trace->mark('w', k);
     struct Drained {
@@ -1780,14 +1508,14 @@ int run_job(const Call& C, Job& J, bool sync) {
         if (rc != OVL_OK) break;
         while (J.drained <= k) {
             const int64_t j = J.drained;
-            if (chunk_staged(C, J, j) && k - j < (J.om[(size_t)j] == 3 ? 1 : kSlots - 1)) break;
+            if (chunk_staged(C, J, j) && k - j < kSlots - 1) break;
             if (chunk_staged(C, J, j) && (rc = drain_chunk(C, J, j)) != OVL_OK) break;
             ++J.drained;
         }
     }
     for (; rc == OVL_OK && J.drained < J.nchunks; ++J.drained)
         if (chunk_staged(C, J, J.drained)) rc = drain_chunk(C, J, J.drained);
-    if (rc == OVL_OK && sync && J.nchunks > 0 && J.ended) {
+    if (rc == OVL_OK && sync && J.nchunks > 0) {
         HIPCHK(J.d, hipSetDevice(J.d->device));
         HIPCHK(J.d, hipStreamSynchronize(J.d->stream));
     }
@@ -1856,7 +1584,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         }
     }
     for (Job& J : jobs) {
-        if (J.nchunks == 0 || !J.ended) continue;  // (streamed records, all read: nothing left to land)
+        if (J.nchunks == 0) continue;
         HIPCHK(c, hipSetDevice(J.d->device));
         HIPCHK(c, hipStreamSynchronize(J.d->stream));
     }
@@ -1866,8 +1594,8 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     for (Job& J : jobs) {
         Dev* d = J.d;
         if (J.nchunks == 0) continue;
-        if ((J.ended && *(volatile uint32_t*)d->h_flag) || J.n_bad > 0) {
-            if (J.ended) *d->h_flag = 0;
+        if (*(volatile uint32_t*)d->h_flag) {
+            *d->h_flag = 0;
             rc = fail(c, OVL_E_INDEX, "a pair index is outside [0, %d)", d->n_reads);
         }
         if (C.timing) {
@@ -1886,20 +1614,13 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     }
     c->t_kernel_ms = kms;
     c->t_call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    int64_t link = 0, packed = 0, ix = 0, dec = 0, res_all = 0, rec = 0, esc = 0;
+    int64_t link = 0, packed = 0, ix = 0, dec = 0, res_all = 0;
     for (const Job& J : jobs) {
         const int64_t n = J.hi - J.lo;
         if (n <= 0) continue;
-        const int64_t np = J.n_packed ? std::min(J.rec_end, J.cb[(size_t)J.n_packed]) : 0;
+        const int64_t np = J.n_packed ? J.cb[(size_t)J.n_packed] : 0;
         packed += np;
-        int64_t res = 8 * (n - np);  // results: int32 pairs, 2 bytes per packed pair, 128 per record + specials
-        for (int64_t k = 0; k < J.n_packed; ++k) {
-            const int64_t nk = std::min(J.cb[(size_t)k + 1], np) - std::min(J.cb[(size_t)k], np);
-            res += J.om[(size_t)k] == 3 ? 128 * ((nk + 63) / 64) : 2 * nk;
-            if (J.om[(size_t)k] == 3) rec += nk;
-        }
-        res += 4 * J.n_esc;
-        esc += J.n_esc;
+        const int64_t res = 8 * (n - np) + 2 * np;  // results: int32 pairs, 2 bytes per packed pair
         res_all += res;
         link += (C.compact ? J.d->cp_link : (C.h_a ? 8 * n : 0)) + res;
         if (C.compact)
@@ -1909,8 +1630,8 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
     c->x_link_bytes = link;
     c->x_packed_pairs = packed;
     c->x_res_bytes = res_all;
-    c->x_rec_pairs = rec;
-    c->x_esc = esc;
+    c->x_rec_pairs = 0;  // (tile records: the resident grid's calls, resident_call)
+    c->x_esc = 0;
     c->x_ix_pairs = ix;
     c->x_dec_pairs = dec;
     return rc;

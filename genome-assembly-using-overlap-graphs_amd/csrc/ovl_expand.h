@@ -180,17 +180,17 @@ __attribute__((target("avx512f,avx512bw"))) inline void expand_avx512(int32_t* s
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Streamed tile records (ovl_kernels.hip put_tile_rec, sink 3): tile t's record is 32 dwords at r = rec + 32 t,
+// Tile records (ovl_kernels.hip put_ring_rec, the resident grid's ring): tile t's record is 32 dwords at r = rec + 32 t,
 //   r[w] = phase << 31 | c[w + 32] << 15 | c[w]    (c[l]: the 15-bit code of the tile's pair l)
 // c = j(j + 1)/2 + X (end j, X mismatches over L = j compared bases): score = match*j + (mismatch - match)*X.
 // c = 0x7FFF: the pair's special word sp[l] holds it --
 //   1 << 31 | j << 16 | X << 8 | n: score = match*n + (mismatch - match)*X, end j;  0xFFFFFFFF: (-1, -1).
-// A record is complete when every dword's bit 31 is the launch's phase (rec_tile_ready_scalar).  A special word is
-// zero until it lands: the decoders take a tile only once all of its special words have landed, report the words
-// they read (`taken`), and the caller zeroes them once the kernel that wrote them has ended (ovl_api.cpp
-// stream_chunk) -- a host store into a line that a running kernel writes was measured to come back with the
-// device's value (escape words zeroed on the box while their kernel ran were found nonzero again, ~1 in 2,000 at
-// cfg3, round 5).  j from c: the largest j with j(j + 1)/2 <= c is floor((sqrt(8c + 1) - 1) / 2), exact in float for
+// A record is complete when every dword's bit 31 is the lap's phase (rec_tile_ready_scalar).  The decoders take a
+// tile only once all of its special words have landed (get(l) != 0): the ring's 8-byte words carry the request's
+// sequence number (RingSp), so no host store ever zeroes a word a running kernel may write -- one that does was
+// measured to come back with the device's value (round 5's launched record transport, ~1 in 2,000 words at cfg3).
+// The side-array forms (rec_tile_scalar / rec_tile_avx512: 4-byte words, zero until they land, the words read
+// reported in `taken`) serve the CPU tests (tests/c/rec_test.cpp) and tools/rec_expand_probe.cpp.  j from c: the largest j with j(j + 1)/2 <= c is floor((sqrt(8c + 1) - 1) / 2), exact in float for
 // c < 2^15 (8c + 1 is a perfect square exactly when X = 0, and otherwise lies >= 1 from one, far above float's
 // error at 2^18).
 
@@ -254,7 +254,7 @@ inline int rec_tile_scalar_t(int32_t* s, int32_t* e, const uint32_t* r, const Re
     return m;
 }
 
-// the launch form (sink 3): special words in a side array, zero until they land; the words read go to taken[0 ..)
+// the side-array form: special words zero until they land; the words read go to taken[0 ..)
 inline int rec_tile_scalar(int32_t* s, int32_t* e, const uint32_t* r, uint32_t* sp, const RecK& k, size_t cnt,
                            uint32_t phase, int* bad, uint32_t** taken) {
     int m = 0;
@@ -356,7 +356,7 @@ inline bool rec_avx512() {
 #endif
 }
 
-// The record encoder (put_tile_rec restated on the host), for the CPU tests of the decoders: pairs [0, cnt) of a tile
+// The record encoder (put_ring_rec's codes restated on the host), for the CPU tests of the decoders: pairs [0, cnt) of a tile
 // from (sc, en, n) -- n read a's length (j > n: a window pair), en -1 a bad pair; specials into sp.  Returns the
 // specials' count.
 inline int encode_rec_tile(uint32_t* r, uint32_t* sp, const RecK& k, const int32_t* sc, const int32_t* en,

@@ -40,12 +40,7 @@ struct OvlUngappedArgs {
                              // copy engine moves it into HBM on the second stream, where the kernel reads it
     int32_t host_out;    // result sink of uniform_kernel (put_pair): 0 int32 arrays in HBM, 1 host-mapped int32
                          // arrays (non-temporal stores), 2 host-mapped packed (end, mismatches) per pair in
-                         // out_score as uint16, the score of the few pairs that need it in out_end; 3 host-mapped
-                         // streamed tile records (throughput mode: ovl_kernels.hip put_tile_rec)
-    uint32_t rec_phase;  // host_out 3: the phase bit of this launch's record dwords (0 or 1); tiles [0, rec_tiles)
-    int64_t rec_tiles;   // are records, the pairs of the others are stored as int32 into dir_score / dir_end
-    int32_t* dir_score;  // (host-mapped caller arrays, indexed like the launch's pairs)
-    int32_t* dir_end;
+                         // out_score as uint16, the score of the few pairs that need it in out_end
     hipEvent_t ev_start; // non-null (timing): uniform_kernel's launch records these at the kernel's own start and
     hipEvent_t ev_stop;  // end (hipExtLaunchKernelGGL), without the dispatch wait that stream events include
 };

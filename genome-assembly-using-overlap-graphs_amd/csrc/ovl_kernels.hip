@@ -108,47 +108,6 @@ __device__ __forceinline__ float pack_inv(int32_t match, int32_t mismatch) {
     return match != mismatch ? 1.0f / (float)(match - mismatch) : 0.f;
 }
 
-// OM 3: streamed tile records.  A 64-pair tile's results as one 128-byte record at out_score + 32 * tile
-// (dwords), which host threads read while the kernel still runs (ovl_expand.h rec_tile_ready_scalar /
-// rec_tile_scalar / rec_tile_avx512):
-//   dword w (w < 32) = phase << 31 | c[w + 32] << 15 | c[w]   (c[l]: lane l's 15-bit code)
-// The phase bit (the host flips it each time it reuses the staging slot) tells the host which dwords this
-// launch has written: every dword is one aligned 32-bit store, so a dword whose phase bit is the launch's
-// holds the launch's payload, and a record is complete when all 32 are.  No fence, no counter, no
-// acknowledgement wait on the device (the rejected one-grid transport paid an L2 write-back per wave for its
-// counters).  Code c of a pair with end j <= n (read a's length; L = j compared bases, aligners.py:27-48 with
-// gaps that cannot win, so score = match*j + (mismatch - match)*X) is j(j + 1)/2 + X, X <= j <= 254 (< 0x7FFF).
-// Every other pair has c = 0x7FFF and a special word in out_end[p] (zero until it lands; the host zeroes the words it
-// read once this kernel has ended, ovl_api.cpp stream_chunk):
-//   1 << 31 | j << 16 | X << 8 | n   a shorter read a inside b's window (j > n: L = n, score = match*n +
-//                                    (mismatch - match)*X);
-//   0xFFFFFFFF                       a bad pair (-1, -1).
-// 2 link bytes per pair (+ 4 per special), a fixed layout whatever the mismatch counts.  Every lane of the
-// wavefront calls it (the cross-half exchange); lanes with !mine code 0, which the host never reads.
-__device__ __forceinline__ void put_tile_rec(int32_t* out_score, int32_t* out_end, int64_t tile, int64_t p, bool mine,
-                                             int32_t sc, int32_t en, int32_t n, int32_t match, float inv,
-                                             uint32_t phase, int lane) {
-    uint32_t c = 0;
-    if (mine) {
-        if (en < 0) {
-            c = 0x7FFFu;
-            __builtin_nontemporal_store(0xFFFFFFFFu, reinterpret_cast<uint32_t*>(out_end) + p);
-        } else if (en > n) {
-            // X = (match*n - score) / (match - mismatch), an exact quotient below 2^8: float is exact
-            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * n - sc) * inv);
-            c = 0x7FFFu;
-            __builtin_nontemporal_store(0x80000000u | (uint32_t)en << 16 | x << 8 | (uint32_t)n,
-                                        reinterpret_cast<uint32_t*>(out_end) + p);
-        } else {
-            const uint32_t x = (uint32_t)__builtin_rintf((float)(match * en - sc) * inv);
-            c = ((uint32_t)en * (uint32_t)(en + 1) >> 1) + x;
-        }
-    }
-    const uint32_t hi = (uint32_t)__shfl_xor((int)c, 32, 64);
-    if (lane < 32)
-        __builtin_nontemporal_store(phase << 31 | hi << 15 | c, reinterpret_cast<uint32_t*>(out_score) + tile * 32 + lane);
-}
-
 // popcount(v) + acc as one v_bcnt_u32_b32 with its accumulator operand; kept as a chain (the compiler
 // would otherwise sum a block's word counts with an extra v_add3)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t v, uint32_t acc) {
@@ -893,11 +852,9 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
     int32_t* __restrict__ out_score, int32_t* __restrict__ out_end, uint32_t* __restrict__ err_flag,
     const int32_t* __restrict__ heavy_ids, const uint8_t* __restrict__ tile_flags, int32_t heavy_n,
     int64_t tile_base, const uint16_t* __restrict__ ix_b16, const uint8_t* __restrict__ ix_d8,
-    const int32_t* __restrict__ ix_base, uint32_t rec_phase, int64_t rec_tiles, int32_t* __restrict__ dir_score,
-    int32_t* __restrict__ dir_end) {
+    const int32_t* __restrict__ ix_base) {
     using T = typename Key<KM>::T;
     constexpr int P = 2;
-    static_assert(OM != 3 || (KM == 0 && !LAT), "streamed tile records (OM 3): throughput mode, int32 keys");
     constexpr int SROW = (W * P + 3) & ~3;
     constexpr int TROW = (W * P + 3) & ~3;
     // t-truncated pairs in the sweep (snapshot): throughput mode with int32 keys.  Not in latency mode,
@@ -928,9 +885,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
         const bool mine = slot < count;
         int4 e = make_int4(0, 0, 0, 0);
         if (mine) e = ring[(head + slot) & (RING - 1)];
-        // (OM 3 never pushes a side pair: TT scores every pair in the sweep)
-        general_unit<P, W, KM, (OM == 3 ? 1 : OM)>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs,
-                                                   lw, match, mismatch, out_score, out_end, err_flag);
+        general_unit<P, W, KM, OM>(mine, e.x, e.y, e.z, sfx, pfx, len, n_reads, lane >> (6 - rs), rs, lw, match,
+                                   mismatch, out_score, out_end, err_flag);
         head += count;
     };
 #ifdef OVL_TRACE
@@ -1067,10 +1023,8 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             tmask |= 1u << (__builtin_amdgcn_readlane(tm, (int)__builtin_ctzll(bm)) & 31);
         OVL_TR_CLOCK(1, Sw[0] ^ Tw[0]);
         if constexpr (!LAT) {
-            // (a record tile's bad pair travels as its special word: the host may return before this kernel ends,
-            // so the host flag -- read after the end -- is only for the direct tiles)
-            if (mine && !ok && (OM != 3 || tile >= rec_tiles)) ovl_flag_error(err_flag);
-            const bool push = OM != 3 && ok && !uni && !tt;
+            if (mine && !ok) ovl_flag_error(err_flag);
+            const bool push = ok && !uni && !tt;
             const uint64_t pm = __ballot(push);
             if (push)
                 ring[(tail + __popcll(pm & ((1ull << lane) - 1ull))) & (RING - 1)] = make_int4((int32_t)p, a, b, 0);
@@ -1097,21 +1051,7 @@ __global__ __launch_bounds__(256, UNI_OCC(W, KM)) void uniform_kernel(
             }
         }
         OVL_TR_CLOCK(3, (uint32_t)best);
-        if constexpr (OM == 3) {
-            // (TT: every pair of the tile is this wave's, so its record is complete here; a wave past the last
-            // tile stores nothing)
-            if (tile < n_tiles) {
-                int32_t sc, en;
-                Key<KM>::decode(best, sc, en);
-                if (tile < rec_tiles) {
-                    put_tile_rec(out_score, out_end, tile, p, mine, ok ? sc : -1, ok ? en : -1, na, match,
-                                 pack_inv(match, mismatch), rec_phase, lane);
-                } else if (mine) {  // the call's direct share: int32 straight into the caller's pinned arrays
-                    put_result<true>(dir_score + p, ok ? sc : -1);
-                    put_result<true>(dir_end + p, ok ? en : -1);
-                }
-            }
-        } else if (mine && (uni || tt || (!LAT && !ok))) {
+        if (mine && (uni || tt || (!LAT && !ok))) {
             int32_t sc, en;
             Key<KM>::decode(best, sc, en);
             put_pair<OM>(out_score, out_end, p, ok ? sc : -1, ok ? en : -1, na, match, pack_inv(match, mismatch));
@@ -1159,8 +1099,19 @@ __global__ __launch_bounds__(256) void general_kernel(
 
 // ----------------------------------------------------------------------------- resident grid
 
-// One tile's results as a ring record (ovl_grid.h OvlResidentBody): put_tile_rec's codes, the phase bit of the ring
-// lap, and a special pair's word as one 8-byte store {payload, seq} (payload: put_tile_rec's special word).  The
+// One tile's results as a ring record (ovl_grid.h OvlResidentBody), which host threads read while the grid runs
+// (ovl_expand.h rec_tile_ready_scalar / rec_tile_scalar_t / rec_tile_avx512_t):
+//   dword w (w < 32) = phase << 31 | c[w + 32] << 15 | c[w]   (c[l]: lane l's 15-bit code)
+// The phase bit (the ring lap's) tells the host which dwords this request has written: every dword is one aligned
+// 32-bit store, so a dword whose phase bit is the lap's holds this request's payload, and a record is complete
+// when all 32 are.  Code c of a pair with end j <= n (read a's length; L = j compared bases, aligners.py:27-48
+// with gaps that cannot win, so score = match*j + (mismatch - match)*X) is j(j + 1)/2 + X, X <= j <= 254
+// (< 0x7FFF).  Every other pair has c = 0x7FFF and a special word, stored as one 8-byte {payload, seq}:
+//   1 << 31 | j << 16 | X << 8 | n   a shorter read a inside b's window (j > n: L = n, score = match*n +
+//                                    (mismatch - match)*X);
+//   0xFFFFFFFF                       a bad pair (-1, -1).
+// 2 link bytes per pair (+ 8 per special).  Every lane of the wavefront calls it (the cross-half exchange); lanes
+// with !mine code 0, which the host never reads.  The
 // stores are non-temporal 128-byte lines into fine-grained host memory, which the XCD's L2 keeps (write-back) until
 // the wavefront's release fence after its last tile of the request (resident_kernel): a resident grid never reaches
 // the end-of-kernel write-back.  (Measured against the alternatives, target point, N = 8 / N = 1 shards: write-through
@@ -2012,14 +1963,12 @@ static void launch_uniform_4(const OvlUngappedArgs& g, unsigned blocks, hipStrea
         hipExtLaunchKernelGGL(uniform_kernel<W, KM, LAT, OM, IX>, dim3(blocks), dim3(256), 0, stream, g.ev_start,
                               g.ev_stop, 0, g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full,
                               g.match, g.mismatch, g.out_score, g.out_end, g.err_flag, g.heavy_ids, g.tile_flags,
-                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base, g.rec_phase, g.rec_tiles, g.dir_score,
-                              g.dir_end);
+                              g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
         return;
     }
     uniform_kernel<W, KM, LAT, OM, IX><<<blocks, 256, 0, stream>>>(
         g.sfx, g.pfx, g.len, g.n_reads, g.a_idx, g.b_idx, g.n_pairs, g.lw, g.full, g.match, g.mismatch, g.out_score,
-        g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base,
-        g.rec_phase, g.rec_tiles, g.dir_score, g.dir_end);
+        g.out_end, g.err_flag, g.heavy_ids, g.tile_flags, g.heavy_n, g.tile_base, g.ix_b16, g.ix_d8, g.ix_base);
 }
 
 template <int W, int KM, bool LAT>
@@ -2035,10 +1984,6 @@ static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStrea
                 launch_uniform_4<W, KM, LAT, 2, true>(g, blocks, stream);
                 return true;
             }
-            if (g.host_out == 3) {
-                launch_uniform_4<W, KM, LAT, 3, true>(g, blocks, stream);
-                return true;
-            }
         }
         return false;
     }
@@ -2048,12 +1993,6 @@ static bool launch_uniform_m(const OvlUngappedArgs& g, unsigned blocks, hipStrea
         case 2:
             if constexpr (KM == 0) {  // packed results: int32 keys only (the host asks for them only then)
                 launch_uniform_4<W, KM, LAT, 2>(g, blocks, stream);
-                return true;
-            }
-            return false;
-        case 3:
-            if constexpr (KM == 0 && !LAT) {  // streamed tile records: throughput mode, int32 keys
-                launch_uniform_4<W, KM, LAT, 3>(g, blocks, stream);
                 return true;
             }
             return false;
@@ -2157,9 +2096,7 @@ extern "C" hipError_t ovl_launch_ungapped(const OvlUngappedArgs* g, hipStream_t 
     if (g->n_pairs <= 0) return hipSuccess;
     bool ok;
     if (g->host_out >= 2 && (g->lw <= 0 || g->key64)) return hipErrorInvalidValue;  // packed: uniform, int32 keys
-    if (g->host_out == 3 && (g->rs_log2 > 0 || g->lw > 254 || g->rec_phase > 1 || g->rec_tiles < 0 ||
-                             (g->rec_tiles * 64 < g->n_pairs && (!g->dir_score || !g->dir_end))))
-        return hipErrorInvalidValue;  // streamed tile records: throughput mode, j <= 254, a phase bit
+    if (g->host_out < 0 || g->host_out > 2) return hipErrorInvalidValue;
     if (g->ix_b16 && (g->lw <= 0 || g->key64 || g->rs_log2 > 0 || g->heavy_ids || !g->ix_d8 || !g->ix_base))
         return hipErrorInvalidValue;  // host-encoded lists: uniform throughput mode only
     if (g->lw > 0) {

@@ -1,7 +1,7 @@
-// Streamed tile records (genome-assembly-using-overlap-graphs_amd/csrc/ovl_expand.h, ovl_kernels.hip
-// put_tile_rec): (1) every code j(j + 1)/2 + X, X <= j <= 254, decodes to (j, X); (2) random tiles -- window pairs
+// Tile records (genome-assembly-using-overlap-graphs_amd/csrc/ovl_expand.h; ovl_kernels.hip put_ring_rec, the
+// resident grid's ring, whose decoders rec_tile_*_t these side-array forms share): (1) every code j(j + 1)/2 + X, X <= j <= 254, decodes to (j, X); (2) random tiles -- window pairs
 // and bad pairs among them (special words), ends of 0, partial last tiles -- encoded by the host restatement of
-// put_tile_rec (encode_rec_tile) in either phase decode through the scalar form and, where this CPU runs it, the
+// the record encoder (encode_rec_tile) in either phase decode through the scalar form and, where this CPU runs it, the
 // AVX-512 form, at aligned and misaligned destinations, to every (score, end), count their bad pairs and report
 // exactly the special words they read (zeroed here as the caller does after the kernel's end); (3) a record with
 // one dword still in the other phase is not ready, and the AVX-512 form then writes nothing; (4) a record one of

@@ -22,8 +22,8 @@ def test_expand_variants_match_scalar(tmp_path):
 
 
 def test_tile_records_decode(tmp_path):
-    """The streamed tile records of ovl_kernels.hip put_tile_rec (sink 3: 15-bit codes j(j + 1)/2 + X and a phase
-    bit per dword, special words apart): tests/c/rec_test.cpp checks every code, random tiles in both phases
+    """The tile records of the resident grid's ring (ovl_kernels.hip put_ring_rec: 15-bit codes j(j + 1)/2 + X and
+    a phase bit per dword, special words apart; the decoders' side-array form): tests/c/rec_test.cpp checks every code, random tiles in both phases
     through the scalar and (where this CPU runs it) AVX-512 decoders, the readiness test on incomplete records,
     the special words each decode reports for zeroing, and a special word that has not landed."""
     exe = tmp_path / "rec_test"

@@ -145,11 +145,11 @@ def test_one_shot_abi_call(oracle_mod, target):
         np.testing.assert_array_equal(e, re_)
 
 
-@pytest.mark.parametrize("pack", ["1", "2"])
+@pytest.mark.parametrize("pack", ["1", "0"])
 def test_compact_adaptive_share(oracle_mod, target, pack):
-    """Host-list calls into pinned arrays: 2-byte packing (OVL_PACK=1) keeps its own adaptive direct share (the
-    host also encodes the list), the packed part within 20-98 % of the pairs; streamed records (the default)
-    take every pair as records.  Exact results call after call."""
+    """Host-list calls into pinned arrays: 2-byte packing (OVL_PACK=1, the default) keeps its own adaptive direct
+    share (the host also encodes the list), the packed part within 20-98 % of the pairs; OVL_PACK=0 packs none.
+    Exact results call after call."""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = target
     ref_s, ref_e = oracle_mod.batch_closed_form(reads, a, b)
@@ -167,7 +167,7 @@ def test_compact_adaptive_share(oracle_mod, target, pack):
         if pack == "1":
             assert all(0.19 <= x <= 0.99 for x in shares), shares
         else:
-            assert all(x == 1.0 for x in shares), shares
+            assert all(x == 0.0 for x in shares), shares
 
 
 def _pair_link_bytes(eng, n):
@@ -240,11 +240,10 @@ def test_ix_tile_jumps_fall_back(oracle_mod, target):
         eng.close()
 
 
-@pytest.mark.parametrize("pack", ["1", "2"])
+@pytest.mark.parametrize("pack", ["1", "0"])
 def test_ix_small_call_latency_mode(oracle_mod, target, pack):
-    """100 K pairs, compact: with 2-byte packing (OVL_PACK=1) few enough for the latency-mode launch, which takes
-    the decoded list (runs: < 3 B per pair); streamed records (the default) always launch in throughput mode,
-    which reads the list in place (3 B per pair + 4 B per tile)."""
+    """100 K pairs, compact: few enough for the latency-mode launch, which takes the decoded list (runs: < 3 B per
+    pair), with 2-byte packed results (OVL_PACK=1) and with int32 results (OVL_PACK=0)."""
     reads, a, b = target
     a, b = a[:100_000], b[:100_000]
     n = a.shape[0]
@@ -255,12 +254,8 @@ def test_ix_small_call_latency_mode(oracle_mod, target, pack):
         s, e = eng.score(a, b)
         np.testing.assert_array_equal(s, ref_s)
         np.testing.assert_array_equal(e, ref_e)
-        if pack == "1":
-            assert _pair_link_bytes(eng, n) < 3 * n
-            assert eng.last_pair_list() == {"in_place_pairs": 0, "decoded_pairs": n}
-        else:
-            assert eng.last_pair_list() == {"in_place_pairs": n, "decoded_pairs": 0}
-            assert _pair_link_bytes(eng, n) == 3 * n + 4 * ((n + 63) // 64)
+        assert _pair_link_bytes(eng, n) < 3 * n
+        assert eng.last_pair_list() == {"in_place_pairs": 0, "decoded_pairs": n}
     finally:
         eng.close()
 

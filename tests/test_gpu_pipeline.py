@@ -101,8 +101,7 @@ def test_pipeline_host_list_pinned_and_pageable(oracle_mod, cfg2, cfg2_ref, chun
         eng.close()
 
 
-@pytest.mark.parametrize("pack,pct", [("1", "25"), ("1", "0"), ("1", "60"), ("1", "100"), ("0", "25"),
-                                      ("2", "25"), ("2", "0"), ("2", "100")])
+@pytest.mark.parametrize("pack,pct", [("1", "25"), ("1", "0"), ("1", "60"), ("1", "100"), ("0", "25")])
 @pytest.mark.parametrize("chunk", ["0", "1000"])
 def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk):
     """Results cross the link packed (uint16 score | end << 8) and are expanded on the host: pinned,
@@ -140,14 +139,7 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
             else:
                 want = n
             assert x["packed_pairs"] == want, (name, x)
-            if pack == "2":  # streamed records: 128 B per tile of each chunk plus 4 per special pair
-                r = eng.last_transfer()
-                rec = r["result_bytes"] - 8 * (n - want) - 4 * r["escapes"]
-                tiles = (want + 63) // 64
-                assert r["record_pairs"] == want and 128 * tiles <= rec <= 128 * (tiles + n // 1000 + 2), (name, r)
-                assert x["link_bytes"] == 8 * n + r["result_bytes"], (name, x, r)
-            else:
-                assert x["link_bytes"] == 8 * n + 2 * want + 8 * (n - want), (name, x)
+            assert x["link_bytes"] == 8 * n + 2 * want + 8 * (n - want), (name, x)
         # the resident candidate list into a misaligned pageable pair of arrays
         eng.candidates(5)
         out = (np.empty(a.shape[0] + 1, np.int32)[1:], np.empty(a.shape[0], np.int32))
@@ -170,15 +162,13 @@ def test_packed_results_host_arrays(oracle_mod, cfg2, cfg2_ref, pack, pct, chunk
         eng.close()
 
 
-@pytest.mark.parametrize("pack", ["1", "2"])
 @pytest.mark.parametrize("scoring", [(10, -1), (1, -1), (2, 2), (-1, 3), (5, -7)])
-def test_tile_records(oracle_mod, cfg2, pack, scoring):
-    """Packed chunks cross the link as streamed tile records (OVL_PACK=2, opt-in: ovl_kernels.hip put_tile_rec,
-    15-bit codes and a phase bit per dword, expanded by host threads while the kernel runs; OVL_PACK=1, the
-    default, keeps 2 bytes per pair expanded after each chunk): cfg2's list tiled six times (731 K pairs) with
-    bad pairs, under scorings with match == mismatch and mismatch > match, into pinned, pageable and misaligned
-    arrays, all packed and with a direct share; every (score, end) equals the oracle's, and the call's link bytes
-    are the records' (128 per tile + 4 per special pair) or 2 per pair."""
+def test_packed_chunks_scorings(oracle_mod, cfg2, scoring):
+    """Packed chunks (2 bytes per pair, expanded by host threads after each chunk): cfg2's list tiled six times
+    (731 K pairs) with bad pairs, under scorings with match == mismatch and mismatch > match, into pinned, pageable
+    and misaligned arrays, all packed and with a direct share, twice each; every (score, end) equals the oracle's,
+    and the call's link bytes are 2 per packed pair."""
+    pack = "1"
     from ovlgraph import OvlError
     from ovlgraph.hostmem import pinned_empty
     reads, a0, b0 = cfg2
@@ -200,7 +190,7 @@ def test_tile_records(oracle_mod, cfg2, pack, scoring):
                     "pageable": (np.empty(n, np.int32), np.empty(n, np.int32)),
                     "misaligned": (np.empty(n + 1, np.int32)[1:], np.empty(n + 3, np.int32)[3:])}
             for name, out in outs.items():
-                for rep in range(2):  # (the second call reuses the slot in the other phase)
+                for rep in range(2):  # (the second call reuses the staging slots)
                     out[0][:] = 7
                     out[1][:] = 7
                     with pytest.raises(OvlError, match="OVL_E_INDEX"):
@@ -211,50 +201,15 @@ def test_tile_records(oracle_mod, cfg2, pack, scoring):
                     np_ = x["packed_pairs"]
                     assert np_ > 0 and x["link_bytes"] == 8 * n + x["result_bytes"], x
                     res = x["result_bytes"] - 8 * (n - np_)  # the packed part's result bytes
-                    if pack == "1":
-                        assert res == 2 * np_ and x["record_pairs"] == 0, (name, x)
-                    else:
-                        assert x["record_pairs"] == np_, (name, x)
-                        tiles = (np_ + 63) // 64
-                        assert res == 128 * tiles + 4 * x["escapes"], (name, x)
-                        assert x["escapes"] >= len(bad) - 1, (name, x)  # (the bad pairs are specials)
+                    assert res == 2 * np_ and x["record_pairs"] == 0, (name, x)
         finally:
             eng.close()
 
 
-def test_tile_records_phases(oracle_mod, cfg2, cfg2_ref):
-    """The staging slots' phase invariant over calls of changing sizes (ovl_api.cpp issue_chunk /
-    stream_chunk): one engine scores prefixes of cfg2's list that grow, shrink and repeat, as one chunk and in
-    many chunks (slot reuse in both phases, partial last tiles), each call exact against the oracle; a call
-    that leaves stale records of a larger earlier call above its own tiles must not let the next larger call
-    read them as its own."""
-    from ovlgraph.hostmem import pinned_empty
-    reads, a, b = cfg2
-    N = a.shape[0]
-    sizes = [N, N // 3 + 17, N, N // 2 + 1, 70_000, N - 64, N // 3 + 17, N, 65_536, N]
-    for chunk in ("0", "40000"):
-        eng = _engine_env({"OVL_PACK": "2", "OVL_PACK_MIN": "0", "OVL_PACK_DIRECT_PCT": "0", "OVL_PIPE_CHUNK": chunk,
-                           "OVL_PAIRS_FORM": "plain"})
-        try:
-            eng.set_reads(reads)
-            out = (pinned_empty(N), pinned_empty(N))
-            for i, n in enumerate(sizes):
-                out[0][:] = -7
-                out[1][:] = -7
-                eng.score(a[:n], b[:n], out=(out[0][:n], out[1][:n]))
-                np.testing.assert_array_equal(out[0][:n], cfg2_ref[0][:n], err_msg=f"chunk {chunk} call {i}")
-                np.testing.assert_array_equal(out[1][:n], cfg2_ref[1][:n], err_msg=f"chunk {chunk} call {i}")
-                assert eng.last_transfer()["record_pairs"] == n, (chunk, i)
-        finally:
-            eng.close()
-
-
-def test_tile_records_across_read_sets(oracle_mod):
-    """Streamed records over many calls of one engine: cfg2 and cfg3 alternating, each scored as listed (the compact
+def test_packed_across_read_sets(oracle_mod):
+    """Packed results over many calls of one engine: cfg2 and cfg3 alternating, each scored as listed (the compact
     list read in place), permuted (decoded) and from the resident candidate list, twice each, every call exact
-    against the oracle.  Covers the staging slots' rotation and the zeroing of the escape words each record chunk
-    read, which waits until that chunk's kernel has ended (a host store into a line of a running kernel's records
-    was measured to come back with the device's value: stale words then decoded into later calls)."""
+    against the oracle (the staging slots and the heavy tiles reused across read sets)."""
     from ovlgraph.candidates import dedup_reads, enumerate_candidates
     from ovlgraph.reads import config_reads
     sets = {}
@@ -263,7 +218,7 @@ def test_tile_records_across_read_sets(oracle_mod):
         a, b = enumerate_candidates(reads, 5)
         rs, re_ = oracle_mod.batch_ungapped(reads, a, b)
         sets[cfg] = (reads, a, b, rs, re_, np.random.default_rng(1).permutation(a.shape[0]))
-    with _engine_env({"OVL_PACK": "2", "OVL_RESIDENT": "0"}) as eng:
+    with _engine_env({"OVL_RESIDENT": "0"}) as eng:
         for rnd in range(2):
             for cfg in ("cfg2", "cfg3"):
                 reads, a, b, rs, re_, perm = sets[cfg]
@@ -282,14 +237,13 @@ def test_tile_records_across_read_sets(oracle_mod):
                             ws, we = rs[perm], re_[perm]
                         np.testing.assert_array_equal(sc, ws, err_msg=f"{rnd} {cfg} {name} {it}")
                         np.testing.assert_array_equal(en, we, err_msg=f"{rnd} {cfg} {name} {it}")
-                        assert eng.last_transfer()["record_pairs"] == a.shape[0]
+                        assert eng.last_transfer()["packed_pairs"] > 0
 
 
 def test_packed_adaptive_share(oracle_mod, cfg2, cfg2_ref):
     """The direct share of 2-byte packed calls into pinned arrays (OVL_PACK=1) adapts call by call (no
     OVL_PACK_DIRECT_PCT): every call's results stay exact and the packed part stays within its bounds (50-98 % of
-    the pairs).  (Streamed records, OVL_PACK=2, have no direct share unless OVL_PACK_DIRECT_PCT sets one:
-    test_step_transport_vs_oracle.)"""
+    the pairs)."""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b = cfg2
     eng = _engine_env({"OVL_PACK_MIN": "0", "OVL_PACK": "1", "OVL_RESIDENT": "0"})
@@ -713,16 +667,15 @@ def test_cfg5_full_gapped_lane_vs_wavefront_and_oracle(oracle_mod, cfg5):
 @pytest.mark.parametrize("cfg", ["target", "cfg3"])
 @pytest.mark.parametrize("pct", [None, "15"])
 def test_step_transport_vs_oracle(oracle_mod, cfg, pct):
-    """Whole resident list into pinned arrays through streamed tile records (OVL_PACK=2: one launch whose records
-    host threads expand while it runs; with OVL_PACK_DIRECT_PCT its last tiles stored as int32 straight into the
-    arrays) equals the oracle call after call, into reused and fresh arrays; ovl_last_transfer counts 128 B per
-    record tile, 4 B per special pair and 8 B per direct pair.  (The default 2-byte transport of the bench step:
-    test_packed_adaptive_share, test_gpu_bench_dist.py.)"""
+    """Whole resident list into pinned arrays through the bench step's transport (packed chunks of 2 bytes per pair
+    expanded by host threads, the last pairs stored as int32 straight into the arrays; the share adaptive or fixed
+    by OVL_PACK_DIRECT_PCT) equals the oracle call after call, into reused and fresh arrays; ovl_last_transfer
+    counts 2 B per packed pair and 8 B per direct pair."""
     from ovlgraph.candidates import dedup_reads
     from ovlgraph.hostmem import pinned_empty
     from ovlgraph.reads import config_reads
     reads, _ = dedup_reads(config_reads(cfg, seed=0))
-    env = {"OVL_PACK": "2", "OVL_RESIDENT": "0"}  # (the launch transport; the resident grid: test_gpu_resident.py)
+    env = {"OVL_RESIDENT": "0"}  # (the launch transport; the resident grid: test_gpu_resident.py)
     if pct:
         env["OVL_PACK_DIRECT_PCT"] = pct
     eng = _engine_env(env)
@@ -739,13 +692,11 @@ def test_step_transport_vs_oracle(oracle_mod, cfg, pct):
             np.testing.assert_array_equal(out[0], ref_s, err_msg=f"call {it}")
             np.testing.assert_array_equal(out[1], ref_e, err_msg=f"call {it}")
             x = eng.last_transfer()
-            assert (0 < x["packed_pairs"] < n) if pct else x["packed_pairs"] == n, x
-            # (no pair list crosses: the link bytes are the results', tile records for the packed pairs -- 128 B
-            # per 64 pairs and 4 B per special pair -- and 8 B per direct pair)
+            assert 0 < x["packed_pairs"] < n, x
+            # (no pair list crosses: the link bytes are the results', 2 B per packed and 8 B per direct pair)
             assert x["link_bytes"] == x["result_bytes"], x
-            q = x["record_pairs"]
-            assert x["result_bytes"] == 128 * ((q + 63) // 64) + 4 * x["escapes"] + 2 * (x["packed_pairs"] - q) + \
-                8 * (n - x["packed_pairs"]), x
+            assert x["result_bytes"] == 2 * x["packed_pairs"] + 8 * (n - x["packed_pairs"]), x
+            assert x["record_pairs"] == 0, x
         fresh = eng.score_candidates()
         np.testing.assert_array_equal(fresh[0], ref_s)
         np.testing.assert_array_equal(fresh[1], ref_e)

@@ -1,6 +1,6 @@
 // Host-only probe of the streamed-record expansion (diagnostic tool, not part of libovl): n pairs of tile records
 // (ovl_expand.h encode_rec_tile: 10-bit codes, ~4 % escapes; all complete, flushed from the CPU caches as if a device had just written them)
-// expanded into int32 arrays by the CopyPool (ovl_pool.h) the way ovl_api.cpp stream_chunk does -- groups of
+// expanded into int32 arrays by the CopyPool (ovl_pool.h) the way ovl_resident.h drain does -- groups of
 // G tiles round-robin over the parts -- for several shard sizes, group sizes and thread counts; microseconds per
 // call (median of reps) and the implied output write rate.
 // Build: g++ -O2 -std=c++17 -pthread -I genome-assembly-using-overlap-graphs_amd/csrc tools/rec_expand_probe.cpp -o build/rec_expand_probe
