@@ -218,7 +218,8 @@ int ovl_score_candidates_range(ovl_ctx* ctx, int64_t lo, int64_t hi, int32_t mat
  * uniform kernel's form (ungapped plan, int32 keys, <= 4 symbols, reads <= 254 bases) are served by a kernel that
  * stays on the device between calls, fed requests through pinned memory -- a call pays no launch and no completion
  * signal.  It leaves by itself after ~20 ms without a request, when another entry point of the context needs the
- * device, and at ovl_destroy; OVL_RESIDENT=0 routes every call through the launch pipeline.  ovl_quiesce makes the
+ * device, and at ovl_destroy.  Opt-in: OVL_RESIDENT=1 at context creation (the default, 0, routes every call
+ * through the launch pipeline, which the grid did not beat on the boxes measured).  ovl_quiesce makes the
  * context's grids leave now (before a whole-device synchronisation such as torch.cuda.synchronize(), which would
  * otherwise wait for the idle deadline); the next call relaunches them.  ovl_resident_stats reports how many grids
  * are resident, their launches (relaunches: calls that found their grid gone) and whether a failed call disabled
