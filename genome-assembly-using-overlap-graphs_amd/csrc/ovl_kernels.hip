@@ -1238,7 +1238,10 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 // blocks leave after twice that without a new forward, so a grid whose block 0 never ran still ends.
 // PF: tiles software-pipelined (fewer, fatter wavefronts: 2-4 per SIMD) or one tile at a time (UNI_OCC(W, 0)
 // wavefronts per SIMD, uniform_kernel's register budget)
-#define RES_OCC(W, PF) ((PF) ? ((W) >= 3 ? 2 : 4) : UNI_OCC(W, 0))
+#ifndef OVL_RES_PF_OCC
+#define OVL_RES_PF_OCC 2  // (build macro for A/B builds: the software-pipelined form's waves per SIMD at W >= 3)
+#endif
+#define RES_OCC(W, PF) ((PF) ? ((W) >= 3 ? OVL_RES_PF_OCC : 4) : UNI_OCC(W, 0))
 template <int W, bool PF>
 __global__ __launch_bounds__(256, RES_OCC(W, PF)) void resident_kernel(
     const uint32_t* __restrict__ sfx, const uint32_t* __restrict__ pfx, const int32_t* __restrict__ len,
