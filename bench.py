@@ -932,8 +932,9 @@ def strong_scaling(name: str, world: int, rank: int, dev, backend: str, steps: i
 GATHER_DESC = ("dest=host: every rank's kernels store its shard's (score, end) over its own GPU's PCIe link "
                "straight into its slice of one pinned host buffer that rank 0 owns (POSIX shared memory, each "
                "rank pins its pages); a step fence of per-rank counters in the buffer's header page orders the "
-               "steps (rank 0 returns when every slice has landed; no collective per step); SURVEY §8e's "
-               "per-device D2H into pinned host slices")
+               "steps (rank 0 returns when every slice has landed; no collective per step), two result slots "
+               "(step k into slot k % 2: a rank may score step k while rank 0 still waits for step k - 1); "
+               "SURVEY §8e's per-device D2H into pinned host slices")
 
 
 def sharded_list(name: str, world: int, rank: int, dev, backend: str, args):

@@ -121,29 +121,32 @@ _shm_seq = 0
 
 
 class SharedResults:
-    """A (score, end) host buffer of n pairs shared by the ranks of one node (POSIX shm).
+    """(score, end) host buffers of n pairs shared by the ranks of one node (POSIX shm).
 
     Rank 0 creates it, the others attach by name; each rank pins only the pages of its own
-    slices (``ovl_host_register``), so its GPU's stores land in place.  A header page ahead of
-    the two columns holds the step fence (``publish`` / ``wait_all`` / ``release`` /
-    ``wait_released``): one int64 counter per rank, each on its own 64-byte line and written by
-    that rank only, plus rank 0's release counter.
+    slices (``ovl_host_register``), so its GPU's stores land in place.  ``slots`` copies of the two
+    columns (each column padded to whole pages, so no two ranges share a page): step k writes
+    slot k % slots.  A header page ahead of them holds the step fence (``publish`` / ``wait_all`` /
+    ``release`` / ``wait_released``): one int64 counter per rank, each on its own 64-byte line and
+    written by that rank only, plus rank 0's release counter.  ``score`` / ``end`` are slot 0.
     """
 
     LINE = 64
     PAGE = 4096
     TIMEOUT_S = 300.0
 
-    def __init__(self, n_pairs: int, group=None, tag: str = ""):
+    def __init__(self, n_pairs: int, group=None, tag: str = "", slots: int = 1):
         import torch.distributed as dist
         from multiprocessing import resource_tracker, shared_memory
 
         global _shm_seq
         self.n = int(n_pairs)
+        self.slots = max(1, int(slots))
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.hdr_bytes = -(-self.LINE * (self.world + 1) // self.PAGE) * self.PAGE
-        size = self.hdr_bytes + max(8, 8 * self.n)
+        self.col = -(-max(4, 4 * self.n) // self.PAGE) * self.PAGE // 4  # int32 per column, whole pages
+        size = self.hdr_bytes + 8 * self.col * self.slots
         _shm_seq += 1  # several buffers may be alive at once (one per ShardedStep)
         name = [f"ovl_{os.getpid()}_{_shm_seq}_{tag}"[:30] if self.rank == 0 else None]
         if self.rank == 0:
@@ -161,10 +164,15 @@ class SharedResults:
         self.hdr = np.frombuffer(self.shm.buf, dtype=np.int64, count=self.hdr_bytes // 8)
         self.done = self.hdr[: stride * self.world: stride]  # done[r]: the last step rank r published
         self.released = self.hdr[stride * self.world: stride * self.world + 1]  # rank 0: last step consumed
-        self.buf = np.frombuffer(self.shm.buf, dtype=np.int32, count=2 * self.n, offset=self.hdr_bytes)
-        self.score = self.buf[: self.n]
-        self.end = self.buf[self.n:]
+        self.buf = np.frombuffer(self.shm.buf, dtype=np.int32, count=2 * self.col * self.slots,
+                                 offset=self.hdr_bytes)
+        self.score, self.end = self.slot(0)
         self._pinned: List[int] = []
+
+    def slot(self, s: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(score, end) arrays of slot s."""
+        o = 2 * self.col * s
+        return self.buf[o: o + self.n], self.buf[o + self.col: o + self.col + self.n]
 
     # ---- the step fence: no collective, a few cache lines of shared host memory
     def publish(self, step: int) -> None:
@@ -198,17 +206,18 @@ class SharedResults:
         self._spin(lambda: int(self.released[0]) >= step, f"rank 0 to release step {step}")
 
     def pin(self, lo: int, hi: int) -> None:
-        """Pin the pages that hold pairs [lo, hi) of both columns in this process."""
+        """Pin the pages that hold pairs [lo, hi) of both columns of every slot in this process."""
         if hi <= lo:
             return
         from . import _lib
         L = _lib.load()
         base = self.buf.ctypes.data
-        page = 4096
-        for first, last in ((lo, hi), (self.n + lo, self.n + hi)):
+        page = self.PAGE
+        for c in range(2 * self.slots):
+            first, last = c * self.col + lo, c * self.col + hi
             s = (base + 4 * first) // page * page
             e = -(-(base + 4 * last) // page) * page
-            s = max(s, base // page * page)
+            s = max(s, base + 4 * c * self.col)  # (columns start on pages: no page of another column)
             rc = L.ovl_host_register(ctypes.c_void_p(s), e - s)
             if rc != 0:
                 raise _lib.OvlError(rc, _lib.last_error())
@@ -245,9 +254,12 @@ class ShardedStep:
       store into the rank's pinned slice).  On rank 0 ``step()`` returns once every slice of
       this step has landed; on the other ranks once their own slice has.  The order comes from
       the step fence in the buffer's header page (``fence="shm"``, the default): each rank
-      publishes its step number after its call returns, rank 0 waits for all of them, and a
-      rank writes step k only after rank 0 has called step k (so it is done reading step
-      k - 1).  No collective runs per step.  ``fence="barrier"`` puts a ``dist.barrier`` after
+      publishes its step number after its call returns, rank 0 waits for all of them, and step k
+      goes to result slot k % ``slots``, which a rank writes only after rank 0 is done reading
+      step k - ``slots`` (it has called step k - ``slots`` + 1).  With two slots (the default) a
+      rank may score step k while rank 0 still waits for a slower rank's step k - 1, so one
+      rank's late step does not hold every other rank at the next one; every step's results are
+      still complete in rank 0's buffer when its ``step()`` returns.  No collective runs per step.  ``fence="barrier"`` puts a ``dist.barrier`` after
       every step instead (the round-3 form; a barrier over RCCL costs tens of microseconds,
       about what a shard of the target list takes to score at N = 8);
     * ``dest="rank0"``: the shard's results stay in HBM and ``dist.gather`` collects them on
@@ -260,7 +272,8 @@ class ShardedStep:
     def __init__(self, reads: Sequence[str], a_idx=None, b_idx=None, k: Optional[int] = None,
                  match: int = 10, mismatch: int = -1, indel: int = INDEL_DEFAULT, group=None,
                  engine: Optional[OverlapEngine] = None, local_scorer: Optional[Callable] = None,
-                 dest: str = "host", balance: bool = True, band: int = -1, fence: str = "shm"):
+                 dest: str = "host", balance: bool = True, band: int = -1, fence: str = "shm",
+                 slots: int = 2):
         import torch
         import torch.distributed as dist
 
@@ -304,14 +317,19 @@ class ShardedStep:
         self.width = max(1, max(h - l for l, h in self.bounds))
         self.shared = None
         self._launch = None
+        self._launches = []
         if dest == "host":
-            self.shared = SharedResults(self.n_pairs, group, tag=str(os.environ.get("MASTER_PORT", "")))
+            self.shared = SharedResults(self.n_pairs, group, tag=str(os.environ.get("MASTER_PORT", "")),
+                                        slots=slots if fence == "shm" else 1)
             if self.eng is not None:
                 self.shared.pin(lo, hi)
                 if self.on_device_list and hi > lo:
-                    # one foreign call per step (ctypes arguments converted once)
-                    self._launch = self.eng.range_scorer(lo, hi, (self.shared.score[lo:hi], self.shared.end[lo:hi]),
-                                                         match, mismatch, indel, band)
+                    # one foreign call per step (ctypes arguments converted once), one per result slot
+                    for sl in range(self.shared.slots):
+                        sc, en = self.shared.slot(sl)
+                        self._launches.append(self.eng.range_scorer(lo, hi, (sc[lo:hi], en[lo:hi]),
+                                                                    match, mismatch, indel, band))
+                    self._launch = self._launches[0]
         else:
             self.packed = torch.full((2, self.width), -1, dtype=torch.int32, device=self.device)
             self.rows = ([torch.empty_like(self.packed) for _ in range(self.world)] if self.rank == 0 else None)
@@ -349,15 +367,17 @@ class ShardedStep:
         if self.dest == "host":
             self.steps += 1
             k = self.steps
+            sl = k % self.shared.slots
             if self.fence == "shm":
                 if self.rank == 0:
                     self.shared.release(k - 1)  # rank 0 is done with step k - 1's results
                 else:
-                    self.shared.wait_released(k - 1)
-            if self._launch is not None:
-                self._launch()
+                    self.shared.wait_released(k - self.shared.slots)  # (slot sl last held that step)
+            if self._launches:
+                self._launches[sl]()
             elif hi > lo:
-                out = (self.shared.score[lo:hi], self.shared.end[lo:hi])
+                sc, en = self.shared.slot(sl)
+                out = (sc[lo:hi], en[lo:hi])
                 if self.eng is None:
                     sc, en = self._local()
                     out[0][:] = sc
@@ -390,7 +410,8 @@ class ShardedStep:
         if self.rank != 0:
             return None
         if self.dest == "host":
-            return self.shared.score.copy(), self.shared.end.copy()
+            sc, en = self.shared.slot(self.steps % self.shared.slots)
+            return sc.copy(), en.copy()
         score = np.empty(self.n_pairs, dtype=np.int32)
         end = np.empty(self.n_pairs, dtype=np.int32)
         for r, (l, h) in enumerate(self.bounds):
@@ -401,7 +422,8 @@ class ShardedStep:
 
     def close(self) -> None:
         import torch.distributed as dist
-        self._launch = None  # (holds views of the shared buffer)
+        self._launch = None  # (these hold views of the shared buffer)
+        self._launches = []
         if self.shared is not None:
             if self.fence == "shm" and self.rank == 0:
                 self.shared.release(self.steps)

@@ -153,3 +153,67 @@ def test_shm_fence_orders_steps_world3():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert bad == []
+
+
+def _slots_worker(rank, world, port, q):
+    """Two result slots (the default): a rank scores step k only once rank 0 is done reading step k - 2, and with
+    rank 0 slow it does run ahead by one step (its step k while rank 0 still waits for step k - 1); every step's
+    results are whole on rank 0 when its step returns."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.join(os.path.dirname(here), "genome-assembly-using-overlap-graphs_amd")]
+    import torch.distributed as dist
+    from ovlgraph.sharded import ShardedStep
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 999
+    a = np.arange(n, dtype=np.int32)
+    b = (a + 1) % n
+    seen = {"k": 0, "ahead": 0, "bad": []}
+    holder = {}
+
+    def scorer(_reads, x, y):
+        seen["k"] += 1
+        k = seen["k"]
+        if rank == 0:
+            time.sleep(0.004)
+        else:
+            rel = int(holder["st"].shared.released[0])
+            if rel < k - 2:
+                seen["bad"].append(("early", k, rel))
+            if rel == k - 2:
+                seen["ahead"] += 1
+        return np.full(x.shape[0], k, np.int32), x.copy()
+
+    st = ShardedStep(["A"] * n, a, b, local_scorer=scorer, dest="host", balance=False)
+    holder["st"] = st
+    assert st.shared.slots == 2
+    for k in range(1, 31):
+        st.step()
+        if rank == 0:
+            sc, en = st.results()
+            if not (np.all(sc == k) and np.array_equal(en, a)):
+                seen["bad"].append(("results", k))
+    st.close()
+    q.put((rank, seen["bad"], seen["ahead"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shm_fence_two_slots_world3():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slots_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, bad, ahead in got:
+        assert bad == [], (rank, bad)
+        if rank > 0:
+            assert ahead > 0, (rank, ahead)  # (rank 0 sleeps 4 ms per step: the others run one step ahead)
