@@ -101,22 +101,23 @@ int ovl_set_timing(ovl_ctx* ctx, int32_t on);
 int ovl_last_timing(const ovl_ctx* ctx, double* kernel_ms, double* call_ms);
 /* The scoring launches of the last host-array call made with timing on, in issue order: *out_n = count;
  * entry i < cap gives the device ordinal, the result sink (1 int32 stored into host memory; 2 packed 2 B/pair
- * into host staging, expanded by host threads after the launch; 3 streamed tile records into host staging,
- * expanded by host threads while the launch runs; 0, HBM, only in ovl_score_device), the pairs and the launch's
+ * into host staging, expanded by host threads after the launch; 0, HBM, only in ovl_score_device), the pairs and
+ * the launch's
  * duration in ms (HIP events recorded by the kernel's own launch for ungapped chunks, else on its stream).
  * Any output pointer may be NULL. */
 int ovl_last_launches(const ovl_ctx* ctx, int32_t cap, int32_t* device, int32_t* sink, int64_t* pairs, double* ms,
                       int32_t* out_n);
 /* Link traffic of the last host-array scoring call (always recorded): link_bytes = pair-list bytes the
  * devices read from host memory + result bytes they stored there (ovl_last_results: 2 per pair in packed
- * chunks, 128 per 64-pair tile record plus 4 per special pair, 8 per pair otherwise; the few pairs of a 2 B/pair chunk
- * whose score travels separately add 4 each and are not counted); packed_pairs = pairs whose results crossed
- * packed and were expanded on the host. */
+ * chunks, 8 per pair otherwise; the resident grid's calls 128 per 64-pair tile record plus 8 per special pair; the
+ * few pairs of a 2 B/pair chunk whose score travels separately add 4 each and are not counted); packed_pairs =
+ * pairs whose results crossed packed and were expanded on the host. */
 int ovl_last_transfer(const ovl_ctx* ctx, int64_t* link_bytes, int64_t* packed_pairs);
 /* The results' part of the last host-array call's link bytes (always recorded): result_bytes = what the kernels
- * stored into host memory for the results (8 per int32 pair, 2 per packed pair, 128 per streamed tile record of
- * 64 pairs plus 4 per special pair); record_pairs = pairs that crossed as streamed tile records; escapes = the
- * special pairs among them (a shorter read a inside b's window, or a bad pair), whose 4-byte word travels apart. */
+ * stored into host memory for the results (8 per int32 pair, 2 per packed pair; a resident-grid call 128 per
+ * tile record of 64 pairs plus 8 per special pair); record_pairs = pairs that crossed as the resident grid's tile
+ * records; escapes = the special pairs among them (a shorter read a inside b's window, or a bad pair), whose word
+ * travels apart. */
 int ovl_last_results(const ovl_ctx* ctx, int64_t* result_bytes, int64_t* record_pairs, int64_t* escapes);
 /* How the last host-array call's pair list reached the kernels (always recorded): in_place_pairs = pairs of
  * chunks the scoring kernel read in their compact encoding (b as uint16, a as tile deltas); decoded_pairs =
