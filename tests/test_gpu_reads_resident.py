@@ -47,3 +47,36 @@ def test_resident_reads_follow_every_change(oracle_mod):
         eng.set_reads(reads)
         with pytest.raises(Exception):
             eng.score_candidates()
+
+
+def test_resident_reads_digest_over_parts(oracle_mod):
+    """A read set of ~0.7 MB (the digest runs in 256 KiB parts on the host pool, 256-byte blocks of 32 lanes, then
+    a tail): one base changed in each part -- at the start of the set, in the middle part's lane blocks, in the
+    last bytes (the tail) -- reaches the device every time, and the unchanged set stays resident."""
+    from ovlgraph import OverlapEngine
+    rng = np.random.default_rng(11)
+    reads = _reads(rng, 6000, 100, 130)
+    total = sum(len(r) for r in reads)
+    assert total > 2 * (1 << 18)
+    starts = np.cumsum([0] + [len(r) for r in reads])
+
+    def read_at(byte):
+        return int(np.searchsorted(starts, byte, side="right") - 1)
+
+    with OverlapEngine(0) as eng:
+        for byte in (3, (1 << 18) + 5000, total - 2):
+            i = read_at(byte)
+            others = rng.integers(0, len(reads), 400, dtype=np.int32)
+            a = np.concatenate([np.full(400, i, np.int32), others])
+            b = np.concatenate([others, np.full(400, i, np.int32)])
+            changed = list(reads)
+            r = changed[i]
+            k = byte - starts[i]
+            changed[i] = r[:k] + ("A" if r[k] != "A" else "G") + r[k + 1:]
+            want = [oracle_mod.batch_dp(rs, a, b) for rs in (reads, changed)]
+            # (the change must show in some pair's result, or the check below could not see a stale set)
+            assert not (np.array_equal(want[0][0], want[1][0]) and np.array_equal(want[0][1], want[1][1]))
+            for rs, (es, ee) in zip((reads, changed, reads), want + want[:1]):
+                sc, en = eng.score_pairs(rs, a, b)
+                np.testing.assert_array_equal(sc, es, err_msg=f"byte {byte}")
+                np.testing.assert_array_equal(en, ee, err_msg=f"byte {byte}")
