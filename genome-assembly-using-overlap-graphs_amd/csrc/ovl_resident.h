@@ -1,6 +1,6 @@
 // ovl_resident.h — host side of the resident scoring grid (ovl_kernels.hip resident_kernel): one per device of a
 // context, launched on the first eligible call and left running, so a call posts a request into pinned memory and
-// expands the ring records as they land -- no launch, no completion event (DESIGN.md §5.3).  Host code only,
+// expands the ring records as they land -- no launch, no completion event (DESIGN.md §5.4).  Host code only,
 // included by ovl_api.cpp.
 //
 // Protocol (ovl_kernels.h OvlResidentCtl / OvlResidentBody):

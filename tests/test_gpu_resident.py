@@ -1,7 +1,7 @@
 """GPU: the resident scoring grid (ovl_kernels.hip resident_kernel, ovl_resident.h) against the oracle.
 
 With OVL_RESIDENT=1 (opt-in), ovl_score_candidates(_range) calls of the uniform kernel's form go to a kernel that
-stays on the device between calls and takes requests through pinned memory (DESIGN.md §5.3).  Every result is compared bit for bit with the
+stays on the device between calls and takes requests through pinned memory (DESIGN.md §5.4).  Every result is compared bit for bit with the
 oracle's closed form (oracle/ovl_oracle.c, the restatement of aligners.py:27-57 where gaps cannot win), call after
 call: into reused and fresh, pinned and pageable, aligned and misaligned arrays; over shards that start inside a
 tile, enough calls for the record ring to wrap many laps; after the grid left by itself (idle) or was asked to
