@@ -102,13 +102,16 @@ def test_resident_whole_list_call_after_call(oracle_mod, cfg):
         eng.close()
 
 
-def test_resident_shards_and_ring_laps(cfg2_case):
+@pytest.mark.parametrize("form", ["1", "1x3x1x4x2", "1x4x0x4x0"])
+def test_resident_shards_and_ring_laps(cfg2_case, form):
     """Shards of the list (bounds from ovl_candidates_shards, starting inside tiles) in a shuffled order, 240
-    calls: the ring (2,048 tiles here) wraps ~30 laps, each request's tiles carry their lap's phase."""
+    calls: the ring (2,048 tiles here) wraps ~30 laps, each request's tiles carry their lap's phase.  Forms
+    (OVL_RESIDENT): the default (2 blocks per CU, software-pipelined tiles, one fence per block); 3 blocks per CU
+    with one fence per wavefront; one tile at a time at 4 blocks per CU."""
     from ovlgraph.hostmem import pinned_empty
     reads, a, b, (ref_s, ref_e) = cfg2_case
     rng = np.random.default_rng(3)
-    eng = _engine()
+    eng = _engine({"OVL_RESIDENT": form})
     try:
         eng.set_reads(reads)
         eng.enumerate_candidates(5)
