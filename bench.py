@@ -596,7 +596,9 @@ def band_pmc(band: int):
     tools/cfg5_pmc_summary.py: each counter in its own rocprofv3 pass of the same bench command, so not live):
     valu_isa_frac (VALU pipe issue share at 4 cycles per wave64 instruction), waves_per_simd (mean resident),
     lds_bank_conflict_frac (conflict cycles over LDS-array cycles).  None when the profile lacks the band."""
-    src = os.path.join("profiles", "r05_cfg5_pmc.json")
+    src = next((os.path.join("profiles", f"{r}_cfg5_pmc.json") for r in ("r06", "r05")
+                if os.path.exists(os.path.join(ROOT, "profiles", f"{r}_cfg5_pmc.json"))),
+               os.path.join("profiles", "r05_cfg5_pmc.json"))
     try:
         with open(os.path.join(ROOT, src)) as f:
             ks = json.load(f)["bands"][str(band)]["kernels"]

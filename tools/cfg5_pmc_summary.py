@@ -1,7 +1,7 @@
-"""Summarise tools/gpu_r05_cfg5_pmc.sh into profiles/r05_cfg5_pmc.json (BASELINE configs[4], the kernel of every
-point of the cfg5 band sweep).
+"""Summarise tools/gpu_r05_cfg5_pmc.sh into profiles/<round>_cfg5_pmc.json (BASELINE configs[4], the kernel of every
+point of the cfg5 band sweep; <round> from CFG5_PMC_ROUND, default r06).
 
-    python tools/cfg5_pmc_summary.py gpurun_out/r05cfg5 [gpurun_out/<later run> ...]   (a later run's bands win)
+    python tools/cfg5_pmc_summary.py gpurun_out/r06cfg5a [gpurun_out/<later run> ...]   (a later run's bands win)
 
 Per kernel (averaged per launch, each counter from its own pass):
   waves_per_simd = 4 * SQ_WAVE_CYCLES / (duration * shader clock * 1024 SIMDs)  (SQ_WAVE_CYCLES counts quad-cycles);
@@ -105,7 +105,7 @@ def main():
         if line and line.get("band_sweep"):
             pt = line["band_sweep"]["points"][0]
         out["bands"][band] = {"kernels": ks, "bench_point_same_run": pt, "run": os.path.basename(os.path.dirname(d))}
-    path = os.path.join(root, "profiles", "r05_cfg5_pmc.json")
+    path = os.path.join(root, "profiles", os.environ.get("CFG5_PMC_ROUND", "r06") + "_cfg5_pmc.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1)[:6000])
 
