@@ -839,7 +839,10 @@ __device__ __forceinline__ void general_unit(bool mine, int64_t p, int32_t a, in
 //    side work overlaps the sweep instead of trailing it.
 // waves per SIMD the kernel is compiled for (VGPR budget 512 / occupancy): the
 // most that fits without spilling
-#define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : 4))) \
+#ifndef OVL_UNI_OCC_W78
+#define OVL_UNI_OCC_W78 4  // (build macro for A/B builds: int32-key waves per SIMD at W = 7, 8)
+#endif
+#define UNI_OCC(W, KM) ((KM) == 0 ? ((W) <= 4 ? 8 : ((W) <= 5 ? 7 : ((W) <= 6 ? 6 : OVL_UNI_OCC_W78))) \
                                   : ((W) <= 4 ? 7 : ((W) <= 5 ? 6 : ((W) <= 6 ? 5 : 4))))
 // IX: the pair list is read in its compact encoding (b = ix_b16[p], 0xFFFF a bad index; a = ix_base[tile] +
 // ix_d8[p]), which the copy engine moved into HBM beside the previous chunk's launch (3 bytes per pair plus 4 per
