@@ -1489,7 +1489,10 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
         quiesce(jobs);
         return rc;
     }
-    // pack_share: the direct share of packed calls into pinned arrays follows which side finished last.  The
+    #ifndef OVL_SHARE_WAIT_US
+#define OVL_SHARE_WAIT_US 8.0  // (build macro for A/B builds: the host's wait for the direct chunk that counts)
+#endif
+// pack_share: the direct share of packed calls into pinned arrays follows which side finished last.  The
     // host pool has expanded every packed chunk now; if the direct chunk is already done, the link idled
     // while the host worked (more direct), if the host still waits for it, the host idles (more packed).
     for (Job& J : jobs) {
@@ -1504,7 +1507,7 @@ int run_pipeline(ovl_ctx* c, const Call& C, std::vector<Job>& jobs) {
             HIPCHK(c, wait_event(d, d->ev_last));
             const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
             double& share = C.compact ? d->pack_pct_h : d->pack_pct;
-            if (us > 8.0) share = std::max(2.0, share - 1.0);
+            if (us > OVL_SHARE_WAIT_US) share = std::max(2.0, share - 1.0);
         }
     }
     for (Job& J : jobs) {
