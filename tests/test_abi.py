@@ -42,6 +42,9 @@ def test_null_args_are_errors_not_crashes():
     assert L.ovl_create(0, None) == -1
     assert L.ovl_set_reads(None, None, None, 0) == -1
     assert L.ovl_score_host(None, None, None, 0, 10, -1, -(2 ** 31), -1, None, None) == -1
+    assert L.ovl_quiesce(None) == -1
+    assert L.ovl_resident_stats(None, None, None, None, None) == -1
+    assert L.ovl_devices_for(None, 10, None) == -1
     assert L.ovl_destroy(None) == 0
     assert isinstance(_lib.last_error(None), str)
 
